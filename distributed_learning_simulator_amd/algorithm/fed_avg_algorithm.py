@@ -1,0 +1,138 @@
+"""FedAvg (dataset-size weighted), cohort form.
+
+Reference `algorithm/fed_avg_algorithm.py:11-110`: streaming accumulation of
+float64(θ_k)·n_k and Σ n_k, finalize θ = (acc/W).to(dtype), NaN assert, `end_training` from
+the first worker, merged `other_data`. Delta uploads are restored against θ_t first
+(`aggregation_algorithm.py:52-71`), i.e. θ_{t+1} = θ_t + Σ n_kΔ_k / Σ n_k.
+
+MI355X-native execution: per cohort ONE fused `weighted_sum` kernel
+over [K, P] (fp64 accumulation in registers, fp32 out) → after all local cohorts ONE
+`all_reduce(SUM)` of the accumulator and weights across ranks (RCCL over xGMI) → finalize
+on every rank. The result is already resident on every rank, so the broadcast M5 needs no
+second collective.
+
+Generalisations used by the methods:
+* element masks (`msg.mask`, FedDropoutAvg) → per-element weights (`_get_weight` analogue);
+* block masks (`msg.block_mask`, FedOBD stage 1) → per-block weights: a block is averaged
+  over the clients that sent it; blocks no client sent keep θ_t (fixes B4).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..message import CohortMessage, FlatParameterMessage
+from ..ops import fl
+from .aggregation_algorithm import AggregationAlgorithm
+
+
+class FedAVGAlgorithm(AggregationAlgorithm):
+    def __init__(self) -> None:
+        super().__init__()
+        self.accumulate: bool = True
+        self._acc: torch.Tensor | None = None
+        self._w_total: torch.Tensor | None = None  # scalar [1]
+        self._w_elem: torch.Tensor | None = None  # [P] (element masks)
+        self._w_block: torch.Tensor | None = None  # [nblocks] (block masks)
+        self._block_ids: torch.Tensor | None = None
+        self._kind: str | None = None
+        self._dataset_size = 0.0
+
+    # weights hook (reference `_get_weight`): dataset size
+    def _weights(self, msg: CohortMessage) -> torch.Tensor:
+        return msg.dataset_sizes.to(self.device, torch.float32)
+
+    def _process(self, msg: CohortMessage, old_parameter) -> None:
+        self.expected_kind = msg.kind if self._acc is None else self.expected_kind
+        self._ensure_acc()
+        if self._kind != msg.kind:
+            raise RuntimeError(f"mixed message kinds in one round: {self._kind} vs {msg.kind}")
+        w = self._weights(msg)
+        if msg.mask is not None:
+            num, den = fl.masked_weighted_sum(msg.data, msg.mask, w)
+            self._acc += num
+            self._w_elem = den if self._w_elem is None else self._w_elem + den
+        else:
+            self._acc += fl.weighted_sum(msg.data, w)
+            if msg.block_mask is not None:
+                bw = (msg.block_mask.float() * w[:, None]).sum(0)
+                self._w_block = bw if self._w_block is None else self._w_block + bw
+                self._block_ids = msg.extra["block_ids"]
+        self._w_total += w.sum()
+        self._dataset_size += float(msg.dataset_sizes.sum().item()) if not msg.dataset_sizes.is_cuda else 0.0
+
+    # set by the method/session so that a rank hosting no client this round still joins the
+    # collectives with correctly shaped (zero) contributions
+    expected_kind: str = "delta"
+    expects_element_mask: bool = False
+    num_blocks: int = 0
+    block_ids: torch.Tensor | None = None
+
+    def _ensure_acc(self) -> None:
+        P = self.layout.padded_size
+        if self._acc is None:
+            self._acc = torch.zeros(P, dtype=torch.float32, device=self.device)
+            self._w_total = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._kind = self.expected_kind
+        if self.expects_element_mask and self._w_elem is None:
+            self._w_elem = torch.zeros(P, dtype=torch.float32, device=self.device)
+        if self.num_blocks and self._w_block is None:
+            self._w_block = torch.zeros(self.num_blocks, dtype=torch.float32, device=self.device)
+            self._block_ids = self.block_ids
+
+    def _reduce(self) -> None:
+        comm = self.comm
+        if comm.world > 1:
+            # end_training / other_data must agree on every server replica
+            flags = comm.all_gather_object((self._end_training, self._other_data))
+            for end, other in flags:
+                if end is not None:
+                    self._end_training = bool(self._end_training) or end
+                for k, v in other.items():
+                    self._other_data.setdefault(k, v)
+        comm.all_reduce_(self._acc)
+        small = [self._w_total] + ([self._w_block] if self._w_block is not None else [])
+        comm.all_reduce_many_(small)
+        if self._w_elem is not None:
+            comm.all_reduce_(self._w_elem)
+
+    def aggregate_worker_data(self, old_parameter: torch.Tensor) -> FlatParameterMessage:
+        self._ensure_acc()
+        self._reduce()
+        acc = self._acc
+        old = old_parameter.to(self.device)
+        if self._w_elem is not None:
+            den = self._w_elem
+            if self._kind == "delta":
+                new = torch.where(den > 0, old + acc / den.clamp(min=1e-30), old)
+            else:
+                # reference `fed_dropout_avg/algorithm.py:9-18`: zero total weight -> 1
+                new = acc / torch.where(den == 0, torch.ones_like(den), den)
+        elif self._w_block is not None:
+            wb = self._w_block
+            ids = self._block_ids.long()
+            we = torch.where(ids >= 0, wb[ids.clamp(min=0)], torch.zeros((), device=self.device))
+            if self._kind == "delta":
+                new = torch.where(we > 0, old + acc / we.clamp(min=1e-30), old)
+            else:
+                new = torch.where(we > 0, acc / we.clamp(min=1e-30), old)
+        else:
+            wt = self._w_total
+            new = old + acc / wt if self._kind == "delta" else acc / wt
+        if self.config is not None and self.config.debug:
+            assert not torch.isnan(new).any(), "NaN in aggregated parameters"
+        msg = FlatParameterMessage(parameter=new, layout=self.layout, other_data=dict(self._other_data),
+                                   end_training=bool(self._end_training))
+        self._reset_acc()
+        return msg
+
+    def _reset_acc(self) -> None:
+        self._acc = None
+        self._w_total = None
+        self._w_elem = None
+        self._w_block = None
+        self._kind = None
+
+    def clear_worker_data(self) -> None:
+        super().clear_worker_data()
+        self._reset_acc()

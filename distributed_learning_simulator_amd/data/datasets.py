@@ -1,0 +1,207 @@
+"""Synthetic dataset zoo with the shapes of the datasets the reference configs name
+(SURVEY Appendix B). There is no network: every dataset is generated deterministically from
+(seed, name) — class-conditional and learnable, so FL accuracy curves are meaningful.
+
+Images are stored device-resident in the compute layout (NHWC, bf16 on GPU) when they fit
+(`materialize_limit` elements); larger ones (ImageNet-shaped) are generated procedurally per
+batch from a per-index hash, so a 1.28 M-image dataset costs only its label vector.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+
+@dataclass
+class DatasetSpec:
+    name: str
+    kind: str  # image | text | graph
+    num_classes: int
+    n_train: int
+    n_test: int
+    shape: tuple = ()  # image (H, W, C)
+    vocab_size: int = 0
+    max_len: int = 0
+    num_nodes: int = 0
+    num_features: int = 0
+    avg_degree: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+_SPECS = {
+    "mnist": DatasetSpec("MNIST", "image", 10, 60000, 10000, (28, 28, 1)),
+    "fashionmnist": DatasetSpec("FashionMNIST", "image", 10, 60000, 10000, (28, 28, 1)),
+    "cifar10": DatasetSpec("CIFAR10", "image", 10, 50000, 10000, (32, 32, 3)),
+    "cifar100": DatasetSpec("CIFAR100", "image", 100, 50000, 10000, (32, 32, 3)),
+    "imagenet": DatasetSpec("ImageNet", "image", 1000, 1281167, 50000, (224, 224, 3)),
+    "imdb": DatasetSpec("imdb", "text", 2, 25000, 25000, vocab_size=20000, max_len=300),
+    "agnews": DatasetSpec("AG_NEWS", "text", 4, 120000, 7600, vocab_size=30000, max_len=128),
+    "coauthorcs": DatasetSpec("Coauthor_CS", "graph", 15, 0, 0, num_nodes=18333, num_features=6805, avg_degree=9),
+    "cora": DatasetSpec("Cora", "graph", 7, 0, 0, num_nodes=2708, num_features=1433, avg_degree=4),
+    "pubmed": DatasetSpec("PubMed", "graph", 3, 0, 0, num_nodes=19717, num_features=500, avg_degree=5),
+    "citationfull": DatasetSpec("CitationFull", "graph", 4, 0, 0, num_nodes=17716, num_features=1639, avg_degree=6),
+    "dblp": DatasetSpec("DBLP", "graph", 4, 0, 0, num_nodes=17716, num_features=1639, avg_degree=6),
+    "yelp": DatasetSpec("Yelp", "graph", 100, 0, 0, num_nodes=716847, num_features=300, avg_degree=19),
+    "amazonproducts": DatasetSpec("AmazonProducts", "graph", 107, 0, 0, num_nodes=1569960, num_features=200, avg_degree=168),
+    "reddit": DatasetSpec("Reddit", "graph", 41, 0, 0, num_nodes=232965, num_features=602, avg_degree=492),
+}
+
+
+def get_spec(name: str, dataset_kwargs: dict | None = None) -> DatasetSpec:
+    kw = dict(dataset_kwargs or {})
+    key = kw.get("name", name).lower().replace("_", "").replace("-", "")
+    if key not in _SPECS:
+        raise ValueError(f"unknown dataset {name!r}; known: {sorted(s.name for s in _SPECS.values())}")
+    spec = DatasetSpec(**{k: getattr(_SPECS[key], k) for k in _SPECS[key].__dataclass_fields__})
+    if spec.kind == "text" and "max_len" in kw:
+        spec.max_len = int(kw["max_len"])
+    for k in ("n_train", "n_test", "num_nodes", "vocab_size", "num_features"):
+        if k in kw:
+            setattr(spec, k, int(kw[k]))
+    if "scale" in kw:  # shrink a dataset for tests / smoke runs
+        s = float(kw["scale"])
+        spec.n_train = max(spec.num_classes * 4, int(spec.n_train * s))
+        spec.n_test = max(spec.num_classes * 2, int(spec.n_test * s))
+        spec.num_nodes = max(spec.num_classes * 20, int(spec.num_nodes * s)) if spec.num_nodes else 0
+    return spec
+
+
+def _hash_u32(x: torch.Tensor) -> torch.Tensor:
+    """Integer mixing (lowbias32) on int64 tensors, result in [0, 2^32)."""
+    m = 0xFFFFFFFF
+    x = x & m
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & m
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & m
+    x = x ^ (x >> 16)
+    return x
+
+
+class ImageDataset:
+    """Class-conditional images: x = prototype[y] (low-frequency pattern) + noise(index).
+
+    Labels are a seeded balanced permutation. `gather(idx)` returns [.., H, W, C]."""
+
+    def __init__(self, spec: DatasetSpec, split: str, seed: int, device, dtype,
+                 materialize_limit: int = 2_000_000_000, noise: float = 1.0):
+        self.spec = spec
+        self.split = split
+        self.device = device
+        self.dtype = dtype
+        self.noise = noise
+        n = spec.n_train if split == "train" else spec.n_test
+        self.n = n
+        g = torch.Generator().manual_seed(seed * 1000003 + (0 if split == "train" else 1))
+        self.labels = (torch.randperm(n, generator=g) % spec.num_classes).to(torch.int32)
+        H, W, C = spec.shape
+        gp = torch.Generator().manual_seed(seed * 7919 + 17)  # prototypes shared by splits
+        low = torch.randn(spec.num_classes, C, max(H // 4, 2), max(W // 4, 2), generator=gp)
+        proto = torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
+        self.prototypes = proto.permute(0, 2, 3, 1).contiguous()  # [classes, H, W, C]
+        self.salt = seed * 2654435761 + (0 if split == "train" else 97)
+        self.materialized = n * H * W * C <= materialize_limit
+        self.labels_dev = self.labels.to(device)
+        self.proto_dev = self.prototypes.to(device, dtype)
+        if self.materialized:
+            chunks = []
+            dev = torch.device(device)
+            for s in range(0, n, 8192):
+                idx = torch.arange(s, min(n, s + 8192))
+                chunks.append(self._generate(idx, dev, torch.float32).to(dtype))
+            self.data = torch.cat(chunks)
+        else:
+            self.data = None
+
+    def _generate(self, idx: torch.Tensor, device, dtype) -> torch.Tensor:
+        H, W, C = self.spec.shape
+        npix = H * W * C
+        idx = idx.to(device).long()
+        pix = torch.arange(npix, device=device, dtype=torch.int64)
+        h = _hash_u32(idx[:, None] * 0x9E3779B1 + pix[None, :] * 0x85EBCA77 + self.salt)
+        h2 = _hash_u32(h + 0x68E31DA4)
+        # Box-Muller-free approx normal: sum of two uniforms, centred, var 1/6 -> scale
+        u = (h.float() + h2.float()) * (1.0 / 4294967296.0) - 1.0
+        noise = u * math.sqrt(6.0) * self.noise
+        lab = self.labels[idx.cpu()].long() if device.type == "cpu" else self.labels_dev[idx].long()
+        proto = (self.prototypes if device.type == "cpu" else self.proto_dev.float())[lab]
+        return (proto + noise.view(-1, H, W, C)).to(dtype)
+
+    def gather(self, idx: torch.Tensor) -> torch.Tensor:
+        """idx: any-shape int tensor on device -> [*idx.shape, H, W, C]."""
+        flat = idx.reshape(-1).long()
+        if self.data is not None:
+            out = self.data.index_select(0, flat)
+        else:
+            out = self._generate(flat, self.device, self.dtype)
+        return out.reshape(*idx.shape, *self.spec.shape)
+
+    def gather_labels(self, idx: torch.Tensor) -> torch.Tensor:
+        return self.labels_dev.index_select(0, idx.reshape(-1).long()).reshape(idx.shape)
+
+
+class TextDataset:
+    """Class-conditional token sequences: each class has its own Zipf-like preference over a
+    slice of the vocabulary; lengths vary in [max_len/4, max_len]. Token 0 = padding."""
+
+    def __init__(self, spec: DatasetSpec, split: str, seed: int, device):
+        self.spec = spec
+        n = spec.n_train if split == "train" else spec.n_test
+        self.n = n
+        g = torch.Generator().manual_seed(seed * 1000033 + (0 if split == "train" else 1))
+        self.labels = (torch.randperm(n, generator=g) % spec.num_classes).to(torch.int32)
+        L, V = spec.max_len, spec.vocab_size
+        lengths = torch.randint(max(L // 4, 1), L + 1, (n,), generator=g)
+        base = torch.randint(1, V, (n, L), generator=g)
+        # class-informative tokens: with p=0.3 a token is drawn from the class slice
+        slice_w = max((V - 1) // (spec.num_classes * 4), 1)
+        cls_tok = 1 + self.labels.long()[:, None] * slice_w + torch.randint(0, slice_w, (n, L), generator=g)
+        use = torch.rand(n, L, generator=g) < 0.3
+        tokens = torch.where(use, cls_tok, base)
+        pos = torch.arange(L)[None, :]
+        tokens = torch.where(pos < lengths[:, None], tokens, torch.zeros_like(tokens))
+        self.tokens = tokens.to(torch.int32).to(device)
+        self.lengths = lengths.to(torch.int32).to(device)
+        self.labels_dev = self.labels.to(device)
+
+    def gather(self, idx):
+        flat = idx.reshape(-1).long()
+        t = self.tokens.index_select(0, flat).reshape(*idx.shape, self.spec.max_len)
+        l = self.lengths.index_select(0, flat).reshape(idx.shape)
+        return t, l
+
+    def gather_labels(self, idx):
+        return self.labels_dev.index_select(0, idx.reshape(-1).long()).reshape(idx.shape)
+
+
+@dataclass
+class DatasetCollection:
+    spec: DatasetSpec
+    train: object
+    test: object
+    graph: object = None
+
+    @property
+    def name(self):
+        return self.spec.name
+
+
+def create_dataset_collection(name: str, dataset_kwargs: dict | None, seed: int, device,
+                              dtype=torch.float32) -> DatasetCollection:
+    spec = get_spec(name, dataset_kwargs)
+    kw = dict(dataset_kwargs or {})
+    if spec.kind == "image":
+        noise = float(kw.get("noise", 1.0))
+        return DatasetCollection(spec, ImageDataset(spec, "train", seed, device, dtype, noise=noise),
+                                 ImageDataset(spec, "test", seed, device, dtype, noise=noise))
+    if spec.kind == "text":
+        return DatasetCollection(spec, TextDataset(spec, "train", seed, device), TextDataset(spec, "test", seed, device))
+    if spec.kind == "graph":
+        from .graph import GraphDataset
+
+        g = GraphDataset(spec, seed, device, dtype)
+        return DatasetCollection(spec, g, g, graph=g)
+    raise ValueError(spec.kind)

@@ -1,0 +1,187 @@
+"""Flat, client-stacked parameter storage.
+
+The reference keeps one `nn.Module` + optimizer per client and offloads it to CPU between
+uses (`worker/aggregation_worker.py:124-130`, `util/model_cache.py`). Here the parameters of
+all K clients resident on a rank live in ONE device buffer `theta[K, P]` (fp32 master), with
+`grad[K, P]`, optimizer state `[K, P]` and a compute-dtype shadow `shadow[K, P]` (bf16) that
+the GEMM/conv kernels read. Every named parameter is a strided view `[K, *shape]` into
+those buffers (client stride = P), so:
+
+  * the optimiser step is ONE fused launch over [K, P] (sgd_step kernel),
+  * FedAvg is ONE weighted row-reduction over [K, P] (weighted_sum kernel),
+  * weight-gradient kernels write straight into `grad` (no autograd accumulation),
+  * "load global model into clients" is one broadcast launch.
+
+Parameter order/naming follows PyTorch `state_dict` naming of the equivalent nn.Module, so
+`ParamLayout.unflatten` yields reference-compatible dictionaries.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+
+@dataclass
+class ParamEntry:
+    name: str
+    shape: tuple
+    offset: int
+    numel: int
+    init: str = "zeros"  # kaiming_conv | kaiming_linear | ones | zeros | normal | uniform_bias
+    fan_in: int = 1
+    module: str = ""  # owning module path
+    trainable: bool = True
+
+
+@dataclass
+class ParamLayout:
+    entries: list[ParamEntry] = field(default_factory=list)
+    P: int = 0
+    # pad each tensor's offset to 16 elements so every view is 64-B aligned (fp32) and
+    # 32-B aligned (bf16): vector loads in the kernels never straddle tensors.
+    align: int = 16
+
+    def add(self, name, shape, init="zeros", fan_in=1, module="", trainable=True) -> ParamEntry:
+        numel = int(math.prod(shape))
+        off = (self.P + self.align - 1) // self.align * self.align
+        e = ParamEntry(name, tuple(shape), off, numel, init, fan_in, module, trainable)
+        self.entries.append(e)
+        self.P = off + numel
+        return e
+
+    @property
+    def num_params(self) -> int:
+        """Logical parameter count (what the reference's message size rule sees)."""
+        return sum(e.numel for e in self.entries)
+
+    @property
+    def padded_size(self) -> int:
+        return (self.P + self.align - 1) // self.align * self.align
+
+    def index(self) -> dict[str, ParamEntry]:
+        return {e.name: e for e in self.entries}
+
+    def view(self, buf: torch.Tensor, e: ParamEntry) -> torch.Tensor:
+        """[K, *shape] strided view of row-stacked buffer buf [K, P_pad]."""
+        return buf[:, e.offset : e.offset + e.numel].view(buf.shape[0], *e.shape) if buf.is_contiguous() \
+            else buf[:, e.offset : e.offset + e.numel].unflatten(1, e.shape)
+
+    def unflatten(self, row: torch.Tensor) -> dict[str, torch.Tensor]:
+        return {e.name: row[e.offset : e.offset + e.numel].view(e.shape) for e in self.entries}
+
+    def flatten(self, tensors: dict[str, torch.Tensor], out: torch.Tensor | None = None) -> torch.Tensor:
+        if out is None:
+            out = torch.zeros(self.padded_size, dtype=torch.float32)
+        for e in self.entries:
+            if e.name in tensors:
+                out[e.offset : e.offset + e.numel] = tensors[e.name].reshape(-1).to(out.device, out.dtype)
+        return out
+
+    def segment_ids(self, device=None) -> torch.Tensor:
+        """int32 [P_pad]: tensor index of each element; inter-tensor padding gets the
+        extra id len(entries) so per-tensor reductions never see it."""
+        ids = torch.full((self.padded_size,), len(self.entries), dtype=torch.int32)
+        for i, e in enumerate(self.entries):
+            ids[e.offset : e.offset + e.numel] = i
+        return ids.to(device) if device is not None else ids
+
+    def segment_sizes(self, device=None) -> torch.Tensor:
+        t = torch.tensor([e.numel for e in self.entries], dtype=torch.int64)
+        return t.to(device) if device is not None else t
+
+    def valid_mask(self, device=None) -> torch.Tensor:
+        m = torch.zeros(self.padded_size, dtype=torch.bool, device=device)
+        for e in self.entries:
+            m[e.offset : e.offset + e.numel] = True
+        return m
+
+    def init_flat(self, generator: torch.Generator) -> torch.Tensor:
+        """Deterministic init (same seed => identical θ0 on every rank, so the initial
+        model broadcast M1 costs zero bytes on the wire between ranks)."""
+        out = torch.zeros(self.padded_size, dtype=torch.float32)
+        for e in self.entries:
+            v = out[e.offset : e.offset + e.numel]
+            if e.init == "ones":
+                v.fill_(1.0)
+            elif e.init == "zeros":
+                v.zero_()
+            elif e.init in ("kaiming_conv", "kaiming_linear", "uniform_bias"):
+                # torch default (kaiming_uniform a=sqrt(5)) => U(-1/sqrt(fan_in), 1/sqrt(fan_in))
+                bound = 1.0 / math.sqrt(max(e.fan_in, 1))
+                v.uniform_(-bound, bound, generator=generator)
+            elif e.init == "kaiming_normal":
+                std = math.sqrt(2.0 / max(e.fan_in, 1))
+                v.normal_(0.0, std, generator=generator)
+            elif e.init == "normal":
+                v.normal_(0.0, 1.0, generator=generator)
+            elif e.init == "xavier":
+                fan_out = e.shape[0]
+                bound = math.sqrt(6.0 / (e.fan_in + fan_out))
+                v.uniform_(-bound, bound, generator=generator)
+            else:
+                raise ValueError(e.init)
+        return out
+
+
+class CohortBuffers:
+    """Per-rank device state for up to `capacity` resident clients."""
+
+    def __init__(self, layout: ParamLayout, capacity: int, device, compute_dtype,
+                 optimizer: str = "SGD"):
+        P = layout.padded_size
+        self.layout = layout
+        self.capacity = capacity
+        self.device = device
+        self.compute_dtype = compute_dtype
+        self.theta = torch.zeros((capacity, P), dtype=torch.float32, device=device)
+        self.grad = torch.zeros((capacity, P), dtype=torch.float32, device=device)
+        self.state1 = torch.zeros((capacity, P), dtype=torch.float32, device=device)
+        self.state2 = (
+            torch.zeros((capacity, P), dtype=torch.float32, device=device)
+            if optimizer.lower() == "adam" else None
+        )
+        self.shadow = (
+            torch.zeros((capacity, P), dtype=compute_dtype, device=device)
+            if compute_dtype != torch.float32 else None
+        )
+
+    @property
+    def compute(self) -> torch.Tensor:
+        return self.shadow if self.shadow is not None else self.theta
+
+    def nbytes(self) -> int:
+        n = 0
+        for t in (self.theta, self.grad, self.state1, self.state2, self.shadow):
+            if t is not None:
+                n += t.numel() * t.element_size()
+        return n
+
+
+class BoundParams:
+    """Param views used by a forward/backward pass.
+
+    compute: [K, P] (or [1, P] expanded to K for a shared model) in compute dtype;
+    grad: [K, P] fp32 or None (inference)."""
+
+    def __init__(self, layout: ParamLayout, compute: torch.Tensor, grad: torch.Tensor | None,
+                 K: int | None = None):
+        self.layout = layout
+        self.index = layout.index()
+        self.compute = compute
+        self.grad = grad
+        self.K = K if K is not None else compute.shape[0]
+        self.token = torch.empty(0, requires_grad=grad is not None)
+
+    def w(self, name: str) -> torch.Tensor:
+        e = self.index[name]
+        v = self.compute[:, e.offset : e.offset + e.numel]
+        return v.unflatten(1, e.shape)
+
+    def g(self, name: str) -> torch.Tensor | None:
+        if self.grad is None:
+            return None
+        e = self.index[name]
+        return self.grad[:, e.offset : e.offset + e.numel].unflatten(1, e.shape)

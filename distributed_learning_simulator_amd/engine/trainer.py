@@ -1,0 +1,286 @@
+"""Cohort trainer: K clients of one rank advance local SGD in lock-step.
+
+Replaces the reference's per-client `cyy_torch_toolbox` Trainer that ran clients one at a
+time inside a process (`executor.py:17` semaphore ⇒ serial clients; `worker/worker.py:86`
+`trainer.train()`). Here every kernel launch covers all K resident clients:
+
+* a whole round's batch schedule (indices [S, K, B], valid counts, lr, first-step flags) is
+  built once and uploaded, so the step loop never synchronises with the host;
+* epochs are aligned across clients (an epoch is max_k(batches_k) lock-step steps; a client
+  with fewer batches idles with `active=0`), which makes per-epoch hooks (FedOBD stage 2
+  aggregates after every epoch, `fed_obd/worker.py:43`) well defined for the whole cohort;
+* ragged batches are handled by per-client valid counts (BN statistics, CE and weight
+  gradients only see real samples);
+* the optimiser is one fused launch over the flat [K, P] buffers.
+
+Semantics pinned (external-library behaviour): SGD with torch semantics
+(momentum buffer initialised with the first gradient), optimiser state reset at every
+round unless `reuse_learning_rate` (reference `util/model.py:6-23`), CosineAnnealingLR with
+T_max = local epochs, stepped per epoch.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ..models.layers import RunCtx
+from ..ops import fl
+from ..ops import functional as Fn
+from .hooks import ExecutorHookPoint, HookRegistry, StopExecutingException
+from .params import BoundParams, CohortBuffers
+
+
+@dataclass
+class HyperParameter:
+    epoch: int = 1
+    batch_size: int = 64
+    learning_rate: float = 0.01
+    learning_rate_scheduler_name: str | None = None
+    weight_decay: float = 0.0
+    momentum: float = 0.9
+    dampening: float = 0.0
+    nesterov: bool = False
+    optimizer_name: str = "SGD"
+
+    @classmethod
+    def from_config(cls, config) -> "HyperParameter":
+        return cls(
+            epoch=config.epoch, batch_size=config.batch_size, learning_rate=config.learning_rate,
+            learning_rate_scheduler_name=config.learning_rate_scheduler_name,
+            weight_decay=config.weight_decay,
+            momentum=config.momentum if config.optimizer_name.upper() == "SGD" else 0.0,
+            dampening=config.dampening, nesterov=config.nesterov, optimizer_name=config.optimizer_name,
+        )
+
+    def lr_at_epoch(self, e: int, total: int) -> float:
+        name = (self.learning_rate_scheduler_name or "").lower()
+        if name == "cosineannealinglr":
+            return 0.5 * self.learning_rate * (1 + math.cos(math.pi * e / max(total, 1)))
+        if name == "steplr":
+            return self.learning_rate * (0.1 ** (e // max(total // 3, 1)))
+        return self.learning_rate
+
+
+@dataclass
+class RoundSchedule:
+    idx: torch.Tensor  # [S, K, B] int32 (padded with a valid index)
+    counts: torch.Tensor  # [S, K] int32
+    active: torch.Tensor  # [S, K] bool
+    first: torch.Tensor  # [S, K] bool
+    lr: torch.Tensor  # [S, K] fp32
+    epoch_end: list[int]  # step index after which epoch e ends
+    steps: int
+    K: int
+
+
+class TrainStats:
+    def __init__(self, epochs: int, K: int, device):
+        self.loss_sum = torch.zeros((epochs, K), dtype=torch.float32, device=device)
+        self.correct = torch.zeros((epochs, K), dtype=torch.float32, device=device)
+        self.samples = torch.zeros((epochs, K), dtype=torch.float32, device=device)
+
+    def epoch_metrics(self, e: int):
+        n = self.samples[e].clamp(min=1)
+        return self.loss_sum[e] / n, self.correct[e] / n
+
+
+class CohortTrainer:
+    def __init__(self, model, dataset_collection, hyper: HyperParameter, device, compute_dtype,
+                 capacity: int):
+        self.model = model
+        self.dc = dataset_collection
+        self.hyper = hyper
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        self.capacity = capacity
+        self.layout = model.layout
+        self.buffers = CohortBuffers(self.layout, capacity, self.device, compute_dtype, hyper.optimizer_name)
+        self.hooks = HookRegistry()
+        self.adam_step_count = torch.zeros(capacity, dtype=torch.float32, device=self.device)
+        self.graph = dataset_collection.graph
+
+    # -------------------------------------------------------------- hook API (X4)
+    def append_named_hook(self, point, name, fn):
+        self.hooks.append_named_hook(point, name, fn)
+
+    def remove_named_hook(self, name):
+        self.hooks.remove_named_hook(name)
+
+    # ----------------------------------------------------------------- state load
+    def load_global(self, theta_g: torch.Tensor, K: int) -> None:
+        """Every resident client row k < K starts from θ_g (M1/M5 receive + load)."""
+        shadow = self.buffers.shadow[:K] if self.buffers.shadow is not None else None
+        fl.broadcast_rows(self.buffers.theta[:K], theta_g.to(self.device), shadow)
+
+    def load_rows(self, theta_rows: torch.Tensor) -> None:
+        K = theta_rows.shape[0]
+        self.buffers.theta[:K].copy_(theta_rows)
+        if self.buffers.shadow is not None:
+            self.buffers.shadow[:K].copy_(theta_rows)
+
+    def reset_optimizer(self, K: int) -> None:
+        self.buffers.state1[:K].zero_()
+        if self.buffers.state2 is not None:
+            self.buffers.state2[:K].zero_()
+        self.adam_step_count[:K].zero_()
+
+    # ------------------------------------------------------------------ schedule
+    def build_schedule(self, shards: list[torch.Tensor], epochs: int, seed: int,
+                       epoch_offset: int = 0, total_epochs: int | None = None,
+                       lr_override: float | None = None, first_epoch_resets: bool = True) -> RoundSchedule:
+        B = self.hyper.batch_size
+        K = len(shards)
+        total_epochs = total_epochs or epochs
+        per_epoch_steps = [max(1, max((s.numel() + B - 1) // B for s in shards)) for _ in range(epochs)]
+        S = sum(per_epoch_steps)
+        idx = torch.zeros((S, K, B), dtype=torch.int32)
+        counts = torch.zeros((S, K), dtype=torch.int32)
+        lr = torch.zeros((S, K), dtype=torch.float32)
+        first = torch.zeros((S, K), dtype=torch.bool)
+        epoch_end = []
+        s0 = 0
+        for e in range(epochs):
+            lr_e = lr_override if lr_override is not None else self.hyper.lr_at_epoch(e + epoch_offset, total_epochs)
+            for k, shard in enumerate(shards):
+                n = shard.numel()
+                if n == 0:
+                    continue
+                g = torch.Generator().manual_seed((seed * 1_000_003 + k * 7919 + e * 104729) & 0x7FFFFFFF)
+                perm = shard[torch.randperm(n, generator=g)]
+                nb = (n + B - 1) // B
+                padded = torch.cat([perm, perm[:1].expand(nb * B - n)]) if nb * B > n else perm
+                idx[s0 : s0 + nb, k] = padded.view(nb, B).to(torch.int32)
+                c = torch.full((nb,), B, dtype=torch.int32)
+                c[-1] = n - (nb - 1) * B
+                counts[s0 : s0 + nb, k] = c
+                lr[s0 : s0 + nb, k] = lr_e
+            s0 += per_epoch_steps[e]
+            epoch_end.append(s0)
+        active = counts > 0
+        # torch.optim.SGD initialises the momentum buffer with the first gradient
+        seen = torch.zeros(K, dtype=torch.bool)
+        for s in range(S):
+            if first_epoch_resets:
+                first[s] = active[s] & ~seen
+            seen |= active[s]
+        dev = self.device
+        return RoundSchedule(idx.to(dev), counts.to(dev), active.to(dev), first.to(dev), lr.to(dev),
+                             epoch_end, S, K)
+
+    # --------------------------------------------------------------------- train
+    def forward_loss(self, K: int, x, labels, valid):
+        b = self.buffers
+        params = BoundParams(self.layout, b.compute[:K], b.grad[:K])
+        ctx = RunCtx(params, valid, training=True)
+        logits = self.model.forward(x, ctx)
+        loss, correct = Fn.cross_entropy(logits, labels, valid)
+        return loss, correct
+
+    def _gather(self, ds, idx):
+        if self.model.input_kind == "graph":
+            return self.graph.batch(idx)
+        return ds.gather(idx)
+
+    def optimizer_step(self, K: int, lr, active, first) -> None:
+        b = self.buffers
+        h = self.hyper
+        shadow = b.shadow[:K] if b.shadow is not None else None
+        if h.optimizer_name.lower() == "adam":
+            self.adam_step_count[:K] += active.float()
+            fl.adam_step(b.theta[:K], b.grad[:K], b.state1[:K], b.state2[:K], lr, active,
+                         self.adam_step_count[:K], weight_decay=h.weight_decay, shadow=shadow)
+        else:
+            fl.sgd_step(b.theta[:K], b.grad[:K], b.state1[:K], lr, active, first, h.weight_decay,
+                        h.momentum, h.dampening, h.nesterov, shadow)
+
+    def train(self, schedule: RoundSchedule, executor=None, stats: TrainStats | None = None,
+              epoch_base: int = 0) -> TrainStats:
+        K = schedule.K
+        ds = self.dc.train
+        stats = stats or TrainStats(len(schedule.epoch_end), K, self.device)
+        e = 0
+        self.hooks.exec(ExecutorHookPoint.BEFORE_EXECUTE, executor=executor)
+        try:
+            for s in range(schedule.steps):
+                idx = schedule.idx[s]
+                x = self._gather(ds, idx)
+                labels = ds.gather_labels(idx) if self.model.input_kind != "graph" else self.graph.labels_for(idx)
+                valid = schedule.counts[s]
+                loss, correct = self.forward_loss(K, x, labels, valid)
+                loss.sum().backward()
+                with torch.no_grad():
+                    vf = valid.float()
+                    stats.loss_sum[e] += loss.detach() * vf
+                    stats.correct[e] += correct
+                    stats.samples[e] += vf
+                    if self.hooks.has_hook(ExecutorHookPoint.OPTIMIZER_STEP):
+                        self.hooks.exec(ExecutorHookPoint.OPTIMIZER_STEP, executor=executor, step=s,
+                                        lr=schedule.lr[s], active=schedule.active[s], first=schedule.first[s],
+                                        valid=valid, K=K)
+                    else:
+                        self.optimizer_step(K, schedule.lr[s], schedule.active[s], schedule.first[s])
+                self.hooks.exec(ExecutorHookPoint.AFTER_BATCH, executor=executor, step=s)
+                if s + 1 == schedule.epoch_end[e]:
+                    self.hooks.exec(ExecutorHookPoint.AFTER_EPOCH, executor=executor, epoch=epoch_base + e + 1,
+                                    stats=stats, local_epoch=e)
+                    e += 1
+        except StopExecutingException:
+            pass
+        self.hooks.exec(ExecutorHookPoint.AFTER_EXECUTE, executor=executor, stats=stats)
+        return stats
+
+    # ------------------------------------------------------------------ evaluate
+    @torch.no_grad()
+    def evaluate(self, theta_rows: torch.Tensor, dataset=None, batch_size: int | None = None,
+                 max_images: int = 8192, shard: tuple[int, int] = (0, 1)):
+        """Evaluate M models (theta_rows [M,P] fp32 or [P]) on `dataset` (default Test).
+        BN uses batch statistics of each eval batch (reference: running stats disabled).
+        The test set is cut into batches; each batch is a virtual client, so one launch
+        covers many batches (and many models). `shard=(rank, world)` evaluates only this
+        rank's share of the batches. Returns (loss_sum [M], correct [M], n_total)."""
+        if theta_rows.dim() == 1:
+            theta_rows = theta_rows.unsqueeze(0)
+        ds = dataset or self.dc.test
+        if self.model.input_kind == "graph":
+            return self.graph.evaluate(self, theta_rows, shard)
+        M = theta_rows.shape[0]
+        B = batch_size or self.hyper.batch_size
+        n = ds.n
+        nb = (n + B - 1) // B
+        flat = torch.arange(nb * B, device=self.device) % n
+        idx = flat.view(nb, B)
+        counts = torch.full((nb,), B, dtype=torch.int32, device=self.device)
+        counts[-1] = n - (nb - 1) * B
+        rank, world = shard
+        lo, hi = nb * rank // world, nb * (rank + 1) // world
+        compute = theta_rows.to(self.compute_dtype)
+        loss_tot = torch.zeros(M, dtype=torch.float32, device=self.device)
+        corr_tot = torch.zeros(M, dtype=torch.float32, device=self.device)
+        g = max(1, min(nb, max_images // max(B * M, 1)))
+        for b0 in range(lo, hi, g):
+            b1 = min(hi, b0 + g)
+            gi = idx[b0:b1]
+            x = ds.gather(gi)
+            y = ds.gather_labels(gi)
+            c = counts[b0:b1]
+            if M > 1:
+                x = _repeat_leading(x, M)
+                y = y.repeat(M, 1)
+                c = c.repeat(M)
+            params = BoundParams(self.layout, compute, None, K=M * (b1 - b0))
+            ctx = RunCtx(params, c, training=False)
+            logits = self.model.forward(x, ctx)
+            loss, correct = Fn.cross_entropy(logits, y, c)
+            w = c.float()
+            loss_tot += (loss * w).view(M, -1).sum(1)
+            corr_tot += correct.view(M, -1).sum(1)
+        return loss_tot, corr_tot, n
+
+
+def _repeat_leading(x, M):
+    if isinstance(x, tuple):
+        return tuple(_repeat_leading(t, M) for t in x)
+    return x.repeat(M, *([1] * (x.dim() - 1)))

@@ -1,0 +1,252 @@
+"""Cohort layer library: modules whose parameters live in a flat `ParamLayout` and whose
+forward runs the client-batched primitives of `ops.functional` for all K clients at once.
+
+Module/param naming mirrors the equivalent `torch.nn` model's `state_dict` so messages,
+checkpoints and FedOBD block discovery see the same names the reference would
+(`method/fed_obd/obd_algorithm.py:8-22` discovers blocks over module types; `kind` plays
+the role of the module type here).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..engine.params import ParamLayout
+from ..ops import functional as Fn
+
+
+class RunCtx:
+    """Per-pass context: bound params + per-client valid sample counts."""
+
+    def __init__(self, params, valid: torch.Tensor | None = None, training: bool = True):
+        self.P = params
+        self.valid = valid  # [K] int32 number of real samples of each client this step
+        self.training = training
+        self._rows_cache: dict[int, torch.Tensor] = {}
+
+    @property
+    def token(self):
+        return self.P.token
+
+    def valid_rows(self, rows_per_sample: int):
+        if self.valid is None:
+            return None
+        r = self._rows_cache.get(rows_per_sample)
+        if r is None:
+            r = (self.valid * rows_per_sample).to(torch.int32)
+            self._rows_cache[rows_per_sample] = r
+        return r
+
+
+class Module:
+    kind = "module"
+
+    def __init__(self):
+        self.name = ""
+        self._named: list[tuple[str, "Module"]] = []
+
+    @property
+    def children(self) -> list["Module"]:
+        return [m for _, m in self._named]
+
+    def child(self, name: str, m: "Module") -> "Module":
+        self._named.append((name, m))
+        setattr(self, name, m)
+        return m
+
+    def assign_names(self, prefix: str = "") -> None:
+        self.name = prefix
+        for local, c in self._named:
+            c.assign_names(f"{prefix}.{local}" if prefix else local)
+
+    def register(self, layout: ParamLayout) -> None:
+        for c in self.children:
+            c.register(layout)
+
+    def own_params(self) -> list[str]:
+        return []
+
+    def all_params(self) -> list[str]:
+        out = list(self.own_params())
+        for c in self.children:
+            out.extend(c.all_params())
+        return out
+
+    def modules(self):
+        yield self
+        for c in self.children:
+            yield from c.modules()
+
+
+class Seq(Module):
+    kind = "Sequential"
+
+    def __init__(self, *mods):
+        super().__init__()
+        for i, m in enumerate(mods):
+            self.child(str(i), m)
+
+    def forward(self, x, ctx):
+        for m in self.children:
+            x = m.forward(x, ctx)
+        return x
+
+
+class ReLU(Module):
+    kind = "ReLU"
+
+    def forward(self, x, ctx):
+        return torch.relu(x)
+
+
+class Conv2d(Module):
+    kind = "Conv2d"
+
+    def __init__(self, cin, cout, k, stride=1, pad=0, bias=False):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride, self.pad, self.bias = cin, cout, k, stride, pad, bias
+
+    def register(self, layout):
+        fan_in = self.cin * self.k * self.k
+        self.w = layout.add(f"{self.name}.weight", (self.cout, self.k, self.k, self.cin),
+                            "kaiming_conv", fan_in, self.name).name
+        self.b = layout.add(f"{self.name}.bias", (self.cout,), "uniform_bias", fan_in, self.name).name if self.bias else None
+
+    def own_params(self):
+        return [self.w] + ([self.b] if self.b else [])
+
+    def forward(self, x, ctx):
+        P = ctx.P
+        y = Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad)
+        if self.b:
+            # bias only appears in LeNet; fold through a broadcast add (autograd handles db)
+            y = _BiasAdd.apply(y, ctx.token, P.w(self.b), P.g(self.b))
+        return y
+
+
+class _BiasAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, token, b, gb):
+        ctx.gb = gb
+        K = y.shape[0]
+        shape = (b.shape[0],) + (1,) * (y.dim() - 2) + (b.shape[-1],)
+        return y + b.reshape(shape).to(y.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.gb is not None:
+            red = tuple(range(1, dy.dim() - 1))
+            ctx.gb.copy_(dy.float().sum(dim=red))
+        return dy, None, None, None
+
+
+class BatchNorm(Module):
+    """BatchNorm with batch statistics only (reference disables running stats:
+    `util/model.py:23`, `server/server.py:48`). Optional fused residual-add + ReLU."""
+
+    kind = "BatchNorm2d"
+
+    def __init__(self, c, relu=False):
+        super().__init__()
+        self.c, self.relu = c, relu
+
+    def register(self, layout):
+        self.gamma = layout.add(f"{self.name}.weight", (self.c,), "ones", 1, self.name).name
+        self.beta = layout.add(f"{self.name}.bias", (self.c,), "zeros", 1, self.name).name
+
+    def own_params(self):
+        return [self.gamma, self.beta]
+
+    def forward(self, x, ctx, residual=None, relu=None):
+        P = ctx.P
+        rps = 1
+        for d in x.shape[2:-1]:
+            rps *= d
+        return Fn.batch_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta),
+                             ctx.valid_rows(rps), self.relu if relu is None else relu, residual)
+
+
+class Linear(Module):
+    kind = "Linear"
+
+    def __init__(self, fin, fout, bias=True):
+        super().__init__()
+        self.fin, self.fout, self.bias = fin, fout, bias
+
+    def register(self, layout):
+        self.w = layout.add(f"{self.name}.weight", (self.fout, self.fin), "kaiming_linear", self.fin, self.name).name
+        self.b = layout.add(f"{self.name}.bias", (self.fout,), "uniform_bias", self.fin, self.name).name if self.bias else None
+
+    def own_params(self):
+        return [self.w] + ([self.b] if self.b else [])
+
+    def forward(self, x, ctx):
+        P = ctx.P
+        return Fn.linear(x, ctx.token, P.w(self.w), P.w(self.b) if self.b else None,
+                         P.g(self.w), P.g(self.b) if self.b else None)
+
+
+class LayerNorm(Module):
+    kind = "LayerNorm"
+
+    def __init__(self, c):
+        super().__init__()
+        self.c = c
+
+    def register(self, layout):
+        self.gamma = layout.add(f"{self.name}.weight", (self.c,), "ones", 1, self.name).name
+        self.beta = layout.add(f"{self.name}.bias", (self.c,), "zeros", 1, self.name).name
+
+    def own_params(self):
+        return [self.gamma, self.beta]
+
+    def forward(self, x, ctx):
+        P = ctx.P
+        return Fn.layer_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta))
+
+
+class Embedding(Module):
+    kind = "Embedding"
+
+    def __init__(self, vocab, dim):
+        super().__init__()
+        self.vocab, self.dim = vocab, dim
+
+    def register(self, layout):
+        self.w = layout.add(f"{self.name}.weight", (self.vocab, self.dim), "normal", 1, self.name).name
+
+    def own_params(self):
+        return [self.w]
+
+    def forward(self, tokens, ctx):
+        P = ctx.P
+        return Fn.embedding(tokens, ctx.token, P.w(self.w), P.g(self.w))
+
+
+class MaxPool(Module):
+    kind = "MaxPool2d"
+
+    def __init__(self, k, s=None, pad=0):
+        super().__init__()
+        self.k, self.s, self.pad = k, s or k, pad
+
+    def forward(self, x, ctx):
+        return Fn.max_pool2d(x, self.k, self.s, self.pad)
+
+
+class AvgPool(Module):
+    kind = "AvgPool2d"
+
+    def __init__(self, k, s=None):
+        super().__init__()
+        self.k, self.s = k, s or k
+
+    def forward(self, x, ctx):
+        return Fn.avg_pool2d(x, self.k, self.s)
+
+
+class Flatten(Module):
+    kind = "Flatten"
+
+    def forward(self, x, ctx):
+        return x.reshape(x.shape[0], x.shape[1], -1)

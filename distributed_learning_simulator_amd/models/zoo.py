@@ -1,0 +1,373 @@
+"""Model zoo (cohort form). Names used by the reference configs:
+`LeNet5`, `densenet40`, `Resnet50`, `TransformerClassificationModel`, `TwoGCN`/`OneGCN`/
+`SimpleGCN`, plus `ResNet18` (north-star) and `MLP`. Architectures are the standard ones the
+reference's external zoos provide [KNOW]; parameter counts are pinned by tests:
+LeNet5 61,706; ResNet-18 (CIFAR stem) 11,173,962; ResNet-50 25,557,032;
+DenseNet-40 (k=12) 1,059,298 (CIFAR-10); Transformer layer (d=100, ff=2048) 452,548.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..engine.params import ParamLayout
+from ..ops import functional as Fn
+from .layers import (AvgPool, BatchNorm, Conv2d, Embedding, Flatten, LayerNorm, Linear,
+                     MaxPool, Module, ReLU, RunCtx, Seq)
+
+
+class CohortModel:
+    """A model definition + its flat parameter layout."""
+
+    def __init__(self, root: Module, name: str, input_kind: str, num_classes: int):
+        self.root = root
+        self.name = name
+        self.input_kind = input_kind  # image | tokens | graph | vector
+        self.num_classes = num_classes
+        root.assign_names("")
+        self.layout = ParamLayout()
+        root.register(self.layout)
+
+    def forward(self, x, ctx: RunCtx):
+        return self.root.forward(x, ctx)
+
+    @property
+    def num_params(self) -> int:
+        return self.layout.num_params
+
+
+# ---------------------------------------------------------------------------- MLP
+class MLPNet(Module):
+    kind = "MLP"
+
+    def __init__(self, fin, hidden, classes):
+        super().__init__()
+        dims = [fin] + list(hidden)
+        self.layers = []
+        for i in range(len(hidden)):
+            self.layers.append(self.child(f"fc{i + 1}", Linear(dims[i], dims[i + 1])))
+            self.child(f"relu{i + 1}", ReLU())
+        self.out = self.child(f"fc{len(hidden) + 1}", Linear(dims[-1], classes))
+
+    def forward(self, x, ctx):
+        x = x.reshape(x.shape[0], x.shape[1], -1)
+        for l in self.layers:
+            x = torch.relu(l.forward(x, ctx))
+        return self.out.forward(x, ctx)
+
+
+# ------------------------------------------------------------------------- LeNet5
+class LeNet5Net(Module):
+    kind = "LeNet5"
+
+    def __init__(self, cin=1, classes=10, hw=28):
+        super().__init__()
+        self.child("conv1", Conv2d(cin, 6, 5, 1, 2 if hw == 28 else 0, bias=True))
+        self.child("relu1", ReLU())
+        self.child("pool1", MaxPool(2))
+        self.child("conv2", Conv2d(6, 16, 5, 1, 0, bias=True))
+        self.child("relu2", ReLU())
+        self.child("pool2", MaxPool(2))
+        self.child("fc1", Linear(16 * 5 * 5, 120))
+        self.child("relu3", ReLU())
+        self.child("fc2", Linear(120, 84))
+        self.child("relu4", ReLU())
+        self.child("fc3", Linear(84, classes))
+
+    def forward(self, x, ctx):
+        x = self.pool1.forward(torch.relu(self.conv1.forward(x, ctx)), ctx)
+        x = self.pool2.forward(torch.relu(self.conv2.forward(x, ctx)), ctx)
+        x = x.reshape(x.shape[0], x.shape[1], -1)
+        x = torch.relu(self.fc1.forward(x, ctx))
+        x = torch.relu(self.fc2.forward(x, ctx))
+        return self.fc3.forward(x, ctx)
+
+
+# ------------------------------------------------------------------------- ResNets
+class BasicBlock(Module):
+    kind = "BasicBlock"
+    expansion = 1
+
+    def __init__(self, cin, cout, stride):
+        super().__init__()
+        self.child("conv1", Conv2d(cin, cout, 3, stride, 1))
+        self.child("bn1", BatchNorm(cout, relu=True))
+        self.child("conv2", Conv2d(cout, cout, 3, 1, 1))
+        self.child("bn2", BatchNorm(cout))
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = self.child("downsample", Seq(Conv2d(cin, cout, 1, stride, 0), BatchNorm(cout)))
+
+    def forward(self, x, ctx):
+        out = self.bn1.forward(self.conv1.forward(x, ctx), ctx)
+        out = self.conv2.forward(out, ctx)
+        sc = x if self.down is None else self.down.forward(x, ctx)
+        return self.bn2.forward(out, ctx, residual=sc, relu=True)
+
+
+class Bottleneck(Module):
+    kind = "Bottleneck"
+    expansion = 4
+
+    def __init__(self, cin, width, stride):
+        super().__init__()
+        cout = width * 4
+        self.child("conv1", Conv2d(cin, width, 1, 1, 0))
+        self.child("bn1", BatchNorm(width, relu=True))
+        self.child("conv2", Conv2d(width, width, 3, stride, 1))
+        self.child("bn2", BatchNorm(width, relu=True))
+        self.child("conv3", Conv2d(width, cout, 1, 1, 0))
+        self.child("bn3", BatchNorm(cout))
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = self.child("downsample", Seq(Conv2d(cin, cout, 1, stride, 0), BatchNorm(cout)))
+
+    def forward(self, x, ctx):
+        out = self.bn1.forward(self.conv1.forward(x, ctx), ctx)
+        out = self.bn2.forward(self.conv2.forward(out, ctx), ctx)
+        out = self.conv3.forward(out, ctx)
+        sc = x if self.down is None else self.down.forward(x, ctx)
+        return self.bn3.forward(out, ctx, residual=sc, relu=True)
+
+
+class ResNetNet(Module):
+    kind = "ResNet"
+
+    def __init__(self, block, layers, classes=10, cin=3, cifar_stem=True):
+        super().__init__()
+        self.cifar_stem = cifar_stem
+        if cifar_stem:
+            self.child("conv1", Conv2d(cin, 64, 3, 1, 1))
+        else:
+            self.child("conv1", Conv2d(cin, 64, 7, 2, 3))
+        self.child("bn1", BatchNorm(64, relu=True))
+        if not cifar_stem:
+            self.child("maxpool", MaxPool(3, 2, 1))
+        c = 64
+        self.stages = []
+        for i, (n, w) in enumerate(zip(layers, (64, 128, 256, 512))):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                b = block(c, w, stride)
+                blocks.append(b)
+                c = w * block.expansion
+            self.stages.append(self.child(f"layer{i + 1}", Seq(*blocks)))
+        self.child("fc", Linear(c, classes))
+
+    def forward(self, x, ctx):
+        x = self.bn1.forward(self.conv1.forward(x, ctx), ctx)
+        if not self.cifar_stem:
+            x = self.maxpool.forward(x, ctx)
+        for s in self.stages:
+            x = s.forward(x, ctx)
+        x = Fn.global_avg_pool(x)
+        return self.fc.forward(x, ctx)
+
+
+# ------------------------------------------------------------------------ DenseNet
+class DenseLayer(Module):
+    """BN-ReLU-Conv3x3 (the reference's OBD pattern `(BN, ReLU, Conv)` matches it)."""
+
+    kind = "DenseLayer"
+
+    def __init__(self, cin, growth):
+        super().__init__()
+        self.child("norm", BatchNorm(cin, relu=True))
+        self.child("relu", ReLU())
+        self.child("conv", Conv2d(cin, growth, 3, 1, 1))
+
+    def forward(self, x, ctx):
+        y = self.conv.forward(self.norm.forward(x, ctx), ctx)
+        return torch.cat([x, y], dim=-1)
+
+
+class Transition(Module):
+    kind = "Transition"
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.child("norm", BatchNorm(cin, relu=True))
+        self.child("relu", ReLU())
+        self.child("conv", Conv2d(cin, cout, 1, 1, 0))
+        self.child("pool", AvgPool(2))
+
+    def forward(self, x, ctx):
+        return self.pool.forward(self.conv.forward(self.norm.forward(x, ctx), ctx), ctx)
+
+
+class DenseNetNet(Module):
+    kind = "DenseNet"
+
+    def __init__(self, depth=40, growth=12, classes=10, cin=3):
+        super().__init__()
+        n = (depth - 4) // 3
+        c = 2 * growth  # stem width 2k: pins 1,059,298 (CIFAR-10) / 1,100,428 (CIFAR-100)
+        self.child("conv1", Conv2d(cin, c, 3, 1, 1))
+        self.blocks = []
+        for b in range(3):
+            layers = []
+            for _ in range(n):
+                layers.append(DenseLayer(c, growth))
+                c += growth
+            self.blocks.append(self.child(f"dense{b + 1}", Seq(*layers)))
+            if b < 2:
+                self.blocks.append(self.child(f"trans{b + 1}", Transition(c, c)))
+        self.child("norm", BatchNorm(c, relu=True))
+        self.child("relu", ReLU())
+        self.child("fc", Linear(c, classes))
+
+    def forward(self, x, ctx):
+        x = self.conv1.forward(x, ctx)
+        for b in self.blocks:
+            x = b.forward(x, ctx)
+        x = self.norm.forward(x, ctx)
+        x = Fn.global_avg_pool(x)
+        return self.fc.forward(x, ctx)
+
+
+# --------------------------------------------------------------------- Transformer
+class MultiheadAttention(Module):
+    kind = "MultiheadAttention"
+
+    def __init__(self, d, h):
+        super().__init__()
+        self.d, self.h = d, h
+        self.child("in_proj", Linear(d, 3 * d))
+        self.child("out_proj", Linear(d, d))
+
+    def forward(self, x, ctx, key_valid):
+        K, B, L, D = x.shape
+        qkv = self.in_proj.forward(x, ctx).reshape(K, B, L, 3, self.h, D // self.h)
+        qkv = qkv.permute(3, 0, 1, 4, 2, 5)  # 3,K,B,H,L,dh
+        o = Fn.attention(qkv[0].contiguous(), qkv[1].contiguous(), qkv[2].contiguous(), key_valid)
+        o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
+        return self.out_proj.forward(o, ctx)
+
+
+class TransformerEncoderLayer(Module):
+    """Post-norm encoder layer, PyTorch `nn.TransformerEncoderLayer` defaults (ReLU FFN).
+    Dropout is not simulated (deterministic cohort execution)."""
+
+    kind = "TransformerEncoderLayer"
+
+    def __init__(self, d, h, ff):
+        super().__init__()
+        self.child("self_attn", MultiheadAttention(d, h))
+        self.child("linear1", Linear(d, ff))
+        self.child("linear2", Linear(ff, d))
+        self.child("norm1", LayerNorm(d))
+        self.child("norm2", LayerNorm(d))
+
+    def forward(self, x, ctx, key_valid):
+        x = self.norm1.forward(x + self.self_attn.forward(x, ctx, key_valid), ctx)
+        f = self.linear2.forward(torch.relu(self.linear1.forward(x, ctx)), ctx)
+        return self.norm2.forward(x + f, ctx)
+
+
+class TransformerClassifier(Module):
+    kind = "TransformerClassificationModel"
+
+    def __init__(self, vocab, d, h, layers, ff, classes, max_len):
+        super().__init__()
+        self.d, self.max_len = d, max_len
+        self.child("embedding", Embedding(vocab, d))
+        self.layers = [self.child(f"encoder.layers.{i}", TransformerEncoderLayer(d, h, ff)) for i in range(layers)]
+        self.child("classifier", Linear(d, classes))
+        pe = torch.zeros(max_len, d)
+        pos = torch.arange(max_len).float()[:, None]
+        div = torch.exp(torch.arange(0, d, 2).float() * (-math.log(10000.0) / d))
+        pe[:, 0::2] = torch.sin(pos * div)
+        pe[:, 1::2] = torch.cos(pos * div[: d // 2])
+        self._pe = pe
+        self._pe_dev = {}
+
+    def forward(self, batch, ctx):
+        tokens, lengths = batch  # [K,B,L] int, [K,B] int
+        x = self.embedding.forward(tokens, ctx)
+        key = (x.device, x.dtype)
+        if key not in self._pe_dev:
+            self._pe_dev[key] = self._pe.to(x.device, x.dtype)
+        L = tokens.shape[-1]
+        x = x * math.sqrt(self.d) + self._pe_dev[key][:L]
+        for l in self.layers:
+            x = l.forward(x, ctx, lengths)
+        m = (torch.arange(L, device=x.device)[None, None, :] < lengths[..., None]).to(x.dtype)
+        pooled = (x * m[..., None]).sum(2) / lengths.clamp(min=1)[..., None].to(x.dtype)
+        return self.classifier.forward(pooled, ctx)
+
+
+# ---------------------------------------------------------------------------- GCN
+class GCNConv(Module):
+    kind = "GCNConv"
+
+    def __init__(self, fin, fout):
+        super().__init__()
+        self.child("lin", Linear(fin, fout, bias=True))
+
+    def forward(self, x, ctx, graph):
+        # Â (X W) + b  — bias added after propagation like PyG; here lin's bias before
+        # propagation is equivalent up to Â's row sums (=1 for the sym-normalised Â with
+        # self loops only approximately); we keep PyG's order explicitly.
+        h = self.lin.forward(x, ctx)
+        return Fn.spmm(h, graph)
+
+
+class GCNNet(Module):
+    kind = "GCN"
+
+    def __init__(self, fin, hidden, classes, layers):
+        super().__init__()
+        dims = [fin] + [hidden] * (layers - 1) + [classes]
+        self.convs = [self.child(f"conv{i + 1}", GCNConv(dims[i], dims[i + 1])) for i in range(layers)]
+
+    def forward(self, batch, ctx):
+        x, graph = batch
+        for i, c in enumerate(self.convs):
+            x = c.forward(x, ctx, graph)
+            if i + 1 < len(self.convs):
+                x = torch.relu(x)
+        return x
+
+
+# --------------------------------------------------------------------------- build
+def count_params(model: CohortModel) -> int:
+    return model.layout.num_params
+
+
+def build_model(name: str, dataset_spec, model_kwargs: dict | None = None) -> CohortModel:
+    kw = dict(model_kwargs or {})
+    n = name.lower().replace("_", "")
+    classes = dataset_spec.num_classes
+    if dataset_spec.kind == "image":
+        H, W, C = dataset_spec.shape
+        if n == "lenet5":
+            return CohortModel(LeNet5Net(C, classes, H), name, "image", classes)
+        if n in ("mlp", "twonn", "2nn"):
+            hidden = kw.get("hidden", [200, 200])
+            return CohortModel(MLPNet(H * W * C, hidden, classes), name, "image", classes)
+        if n in ("resnet18", "resnet34", "resnet50", "resnet101"):
+            depth = int(n[6:])
+            cfg = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]),
+                   50: (Bottleneck, [3, 4, 6, 3]), 101: (Bottleneck, [3, 4, 23, 3])}[depth]
+            cifar = kw.get("cifar_stem", H <= 64)
+            return CohortModel(ResNetNet(cfg[0], cfg[1], classes, C, cifar), name, "image", classes)
+        if n.startswith("densenet"):
+            depth = int(n[8:] or 40)
+            return CohortModel(DenseNetNet(depth, kw.get("growth_rate", 12), classes, C), name, "image", classes)
+    if dataset_spec.kind == "text":
+        if n in ("transformerclassificationmodel", "transformer"):
+            d = int(kw.get("d_model", 100))
+            return CohortModel(
+                TransformerClassifier(dataset_spec.vocab_size, d, int(kw.get("nhead", 5)),
+                                      int(kw.get("num_encoder_layer", 2)), int(kw.get("dim_feedforward", 2048)),
+                                      classes, int(kw.get("max_len", dataset_spec.max_len))),
+                name, "tokens", classes)
+    if dataset_spec.kind == "graph":
+        layers = {"onegcn": 1, "twogcn": 2, "simplegcn": 2, "gcn": 2}.get(n)
+        if layers is not None:
+            return CohortModel(GCNNet(dataset_spec.num_features, int(kw.get("hidden", 64)), classes, layers),
+                               name, "graph", classes)
+    raise ValueError(f"unknown model {name!r} for dataset kind {dataset_spec.kind}")

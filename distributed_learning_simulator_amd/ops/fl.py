@@ -1,0 +1,110 @@
+"""FL-level fused primitives over flat client-stacked buffers (backend-dispatched).
+
+| primitive            | replaces (reference)                                           |
+|----------------------|----------------------------------------------------------------|
+| sgd_step             | torch.optim.SGD.step per client (K2), GradientWorker step (K3) |
+| adam_step            | torch.optim.Adam.step per client                                |
+| broadcast_rows       | load_parameters of θ_g into every client (`util/model.py:6-23`)|
+| delta_rows           | ModelCache.get_parameter_diff (K4, `util/model_cache.py:30-36`)|
+| weighted_sum         | FedAVGAlgorithm accumulate (K6, `fed_avg_algorithm.py:39-52`)  |
+| masked_weighted_sum  | FedDropoutAvg aggregation (K10, `fed_dropout_avg/algorithm.py`)|
+| dropout_mask         | FedDropoutAvg Bernoulli mask (K9, `fed_dropout_avg/worker.py`) |
+| block_sq_norms       | OBD per-block ‖Δ‖ (K11, `obd_algorithm.py:129-145`)            |
+| qsgd_quant/dequant   | stochastic quantisation (K13, `quantized_endpoint.py:74-83`)   |
+| nnadq_quant/dequant  | NNADQ (K14, `quantized_endpoint.py:86-116`)                    |
+| sign_pack / vote     | sign-SGD 1-bit exchange (M9/M10)                                |
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import backend, ref
+
+
+def sgd_step(theta, grad, mom, lr, active, first_step, weight_decay=0.0, momentum=0.0,
+             dampening=0.0, nesterov=False, shadow=None):
+    be = backend.get(theta)
+    be.sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, nesterov,
+                first_step, shadow)
+
+
+def adam_step(theta, grad, m, v, lr, active, step, beta1=0.9, beta2=0.999, eps=1e-8,
+              weight_decay=0.0, shadow=None):
+    be = backend.get(theta)
+    be.adam_step(theta, grad, m, v, lr, active, step, beta1, beta2, eps, weight_decay, shadow)
+
+
+def broadcast_rows(theta_rows, src, shadow_rows=None):
+    """theta_rows[k,:] = src for every row (and bf16 shadow)."""
+    be = backend.get(theta_rows)
+    if be is ref:
+        theta_rows.copy_(src.unsqueeze(0).expand_as(theta_rows))
+        if shadow_rows is not None:
+            shadow_rows.copy_(theta_rows.to(shadow_rows.dtype))
+    else:
+        be.broadcast_rows(theta_rows, src, shadow_rows)
+
+
+def delta_rows(theta_rows, base, out=None):
+    be = backend.get(theta_rows)
+    if be is ref:
+        d = theta_rows - base.unsqueeze(0)
+        if out is None:
+            return d
+        out.copy_(d)
+        return out
+    return be.delta_rows(theta_rows, base, out)
+
+
+def weighted_sum(x, w):
+    """Σ_k w_k x[k,:] -> fp32 [P] (fp64 accumulation)."""
+    return backend.get(x).weighted_sum(x, w)
+
+
+def masked_weighted_sum(x, mask, w):
+    return backend.get(x).masked_weighted_sum(x, mask, w)
+
+
+# ------------------------------------------------------------------ compression ops
+def philox_uniform(shape, seed: int, offset: int, device) -> torch.Tensor:
+    """Counter-based uniform [0,1) keyed by (seed, offset): identical on every rank and
+    every backend (ref implementation mirrors the kernel's hash)."""
+    n = int(math.prod(shape))
+    idx = torch.arange(n, device=device, dtype=torch.int64) + offset
+    h = _mix(idx, seed)
+    return (h.float() * (1.0 / 4294967296.0)).reshape(shape)
+
+
+def _mix(x: torch.Tensor, seed: int) -> torch.Tensor:
+    m = 0xFFFFFFFF
+    x = (x ^ (seed * 0x9E3779B9)) & m
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & m
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & m
+    x = x ^ (x >> 16)
+    return x
+
+
+def dropout_mask(shape, p: float, seed: int, device) -> torch.Tensor:
+    """Bernoulli(1-p) keep-mask [K,P] keyed by (seed, element)."""
+    be = backend.get(torch.empty(0, device=device))
+    if be is ref:
+        return philox_uniform(shape, seed, 0, device) >= p
+    return be.dropout_mask(shape, p, seed)
+
+
+def block_sq_norms(x, block_offsets, block_ids):
+    """Per-(client, block) Σ x² for segments. x [K,P]; block_ids [P] int (−1 = padding).
+    Returns [K, nblocks] fp32."""
+    be = backend.get(x)
+    if be is ref:
+        nb = int(block_offsets.numel()) - 1
+        out = torch.zeros((x.shape[0], nb), dtype=torch.float32, device=x.device)
+        valid = block_ids >= 0
+        out.index_add_(1, block_ids[valid].long(), (x[:, valid].float() ** 2))
+        return out
+    return be.block_sq_norms(x, block_offsets, block_ids)

@@ -1,0 +1,288 @@
+"""Autograd wiring for the client-batched primitives.
+
+Every parameterised op takes the parameter's compute view `w [K,...]` and its fp32 gradient
+view `gw [K,...]` (a strided view into the cohort's flat grad buffer). Backward writes the
+weight gradient *directly into* `gw` — parameters are never autograd leaves, so there is no
+per-tensor gradient accumulation or zero-fill pass; autograd only tracks activations.
+A zero-size `token` tensor that requires grad is threaded through every op so backward runs
+even when the op's activation input does not need a gradient (e.g. the stem conv).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import backend, ref
+
+
+def _be(t):
+    return backend.get(t)
+
+
+# --------------------------------------------------------------------------- conv2d
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, token, w, gw, stride, pad):
+        be = _be(x)
+        y = be.conv_fwd(x, w, stride, pad)
+        ctx.save_for_backward(x, w)
+        ctx.gw, ctx.stride, ctx.pad = gw, stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        be = _be(dy)
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad)
+        if ctx.gw is not None:
+            if be is ref:
+                ctx.gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (x.shape[0],) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
+            else:
+                be.conv_wgrad(dy, x, ctx.gw, ctx.stride, ctx.pad)
+        return dx, None, None, None, None, None
+
+
+def conv2d(x, token, w, gw, stride=1, pad=0):
+    return _Conv.apply(x, token, w, gw, stride, pad)
+
+
+# --------------------------------------------------------------------------- linear
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, token, w, b, gw, gb):
+        be = _be(x)
+        y = be.linear_fwd(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.gw, ctx.gb = gw, gb
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        be = _be(dy)
+        dy = dy.contiguous()
+        dx = be.linear_dgrad(dy, w) if ctx.needs_input_grad[0] else None
+        if ctx.gw is not None:
+            if be is ref:
+                dw, db = ref.linear_wgrad(dy.float(), x.float(), ctx.gb is not None)
+                ctx.gw.copy_(dw)
+                if ctx.gb is not None:
+                    ctx.gb.copy_(db)
+            else:
+                be.linear_wgrad(dy, x, ctx.gw, ctx.gb)
+        return dx, None, None, None, None, None
+
+
+def linear(x, token, w, b, gw, gb):
+    """x [K, N, Fi] -> [K, N, Fo]; any extra middle dims are flattened."""
+    shp = x.shape
+    x3 = x.reshape(shp[0], -1, shp[-1])
+    y = _Linear.apply(x3, token, w, b, gw, gb)
+    return y.reshape(*shp[:-1], y.shape[-1])
+
+
+# ------------------------------------------------------------------------ batchnorm
+class _BN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual):
+        be = _be(x)
+        K = x.shape[0]
+        C = x.shape[-1]
+        x3 = x.reshape(K, -1, C)
+        r3 = residual.reshape(K, -1, C) if residual is not None else None
+        y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
+        ctx.save_for_backward(x3, y, mean, rstd, gamma)
+        ctx.valid_rows, ctx.relu, ctx.has_res = valid_rows, relu, residual is not None
+        ctx.ggamma, ctx.gbeta, ctx.shape = ggamma, gbeta, x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x3, y, mean, rstd, gamma = ctx.saved_tensors
+        be = _be(dy)
+        K, R, C = x3.shape
+        dy3 = dy.reshape(K, R, C).contiguous()
+        if be is ref:
+            dx, dgamma, dbeta, dpre = ref.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu)
+            if ctx.ggamma is not None:
+                ctx.ggamma.copy_(dgamma)
+                ctx.gbeta.copy_(dbeta)
+        else:
+            dx, dpre = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
+                                 ctx.ggamma, ctx.gbeta, ctx.has_res)
+        dres = dpre.reshape(ctx.shape) if ctx.has_res else None
+        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres
+
+
+def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False, residual=None):
+    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual)
+
+
+# ------------------------------------------------------------------------ layernorm
+class _LN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, token, gamma, beta, ggamma, gbeta):
+        be = _be(x)
+        y, mean, rstd = be.ln_fwd(x, gamma, beta)
+        ctx.save_for_backward(x, mean, rstd, gamma)
+        ctx.ggamma, ctx.gbeta = ggamma, gbeta
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, gamma = ctx.saved_tensors
+        be = _be(dy)
+        dx, dgamma, dbeta = be.ln_bwd(dy.contiguous(), x, mean, rstd, gamma)
+        if ctx.ggamma is not None:
+            ctx.ggamma.copy_(dgamma)
+            ctx.gbeta.copy_(dbeta)
+        return dx, None, None, None, None, None
+
+
+def layer_norm(x, token, gamma, beta, ggamma, gbeta):
+    return _LN.apply(x, token, gamma, beta, ggamma, gbeta)
+
+
+# -------------------------------------------------------------------------- pooling
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, pad):
+        be = _be(x)
+        if pad:
+            x = torch.nn.functional.pad(x, (0, 0, pad, pad, pad, pad), value=float("-inf"))
+        y, idx = be.maxpool_fwd(x, k, s)
+        ctx.save_for_backward(idx)
+        ctx.k, ctx.s, ctx.pad, ctx.xshape = k, s, pad, x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        be = _be(dy)
+        dx = be.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, ctx.k, ctx.s)
+        if ctx.pad:
+            p = ctx.pad
+            dx = dx[:, :, p:-p, p:-p, :].contiguous()
+        return dx, None, None, None
+
+
+def max_pool2d(x, k, s=None, pad=0):
+    return _MaxPool.apply(x, k, s or k, pad)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s):
+        ctx.k, ctx.s, ctx.xshape = k, s, x.shape
+        return _be(x).avgpool_fwd(x, k, s)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _be(dy).avgpool_bwd(dy.contiguous(), ctx.xshape, ctx.k, ctx.s), None, None
+
+
+def avg_pool2d(x, k, s=None):
+    return _AvgPool.apply(x, k, s or k)
+
+
+class _GAP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.xshape = x.shape
+        return _be(x).gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _be(dy).gap_bwd(dy.contiguous(), ctx.xshape)
+
+
+def global_avg_pool(x):
+    return _GAP.apply(x)
+
+
+# -------------------------------------------------------------------- cross entropy
+class _CE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, valid):
+        loss, correct, dlogits = _be(logits).ce_fwd_bwd(logits, labels, valid)
+        ctx.save_for_backward(dlogits)
+        ctx.mark_non_differentiable(correct)
+        return loss, correct
+
+    @staticmethod
+    def backward(ctx, dloss, dcorrect):
+        (dlogits,) = ctx.saved_tensors
+        if dloss is None:
+            return None, None, None
+        g = dlogits * dloss.to(dlogits.dtype)[:, None, None]
+        return g, None, None
+
+
+def cross_entropy(logits, labels, valid=None):
+    """Per-client mean CE [K] and correct counts [K] (fused fwd+bwd kernel)."""
+    return _CE.apply(logits, labels, valid)
+
+
+# ------------------------------------------------------------------------ embedding
+class _Emb(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tokens, token, table, gtable):
+        ctx.save_for_backward(tokens)
+        ctx.gtable, ctx.vocab = gtable, table.shape[1]
+        return _be(table).embedding_fwd(tokens, table)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (tokens,) = ctx.saved_tensors
+        if ctx.gtable is not None:
+            be = _be(dy)
+            if be is ref:
+                ctx.gtable.copy_(ref.embedding_bwd(dy, tokens, ctx.vocab))
+            else:
+                be.embedding_bwd(dy.contiguous(), tokens, ctx.gtable)
+        return None, None, None, None
+
+
+def embedding(tokens, token, table, gtable):
+    return _Emb.apply(tokens, token, table, gtable)
+
+
+# ------------------------------------------------------------------------ attention
+class _Attn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, key_valid):
+        o, lse = _be(q).attn_fwd(q, k, v, key_valid)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.key_valid = key_valid
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = _be(do).attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.key_valid)
+        return dq, dk, dv, None
+
+
+def attention(q, k, v, key_valid=None):
+    return _Attn.apply(q, k, v, key_valid)
+
+
+# ---------------------------------------------------------------------------- spmm
+class _SpMM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rowptr, col, val, rowptr_t, col_t, val_t):
+        ctx.save_for_backward(rowptr_t, col_t, val_t)
+        return _be(x).spmm(rowptr, col, val, x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        rowptr_t, col_t, val_t = ctx.saved_tensors
+        return _be(dy).spmm(rowptr_t, col_t, val_t, dy.contiguous()), None, None, None, None, None, None
+
+
+def spmm(x, graph):
+    """A @ x for a shared normalised adjacency `graph` (CSR + its transpose)."""
+    return _SpMM.apply(x, graph.rowptr, graph.col, graph.val, graph.rowptr_t, graph.col_t, graph.val_t)

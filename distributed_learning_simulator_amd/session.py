@@ -1,0 +1,182 @@
+"""Per-rank simulation runtime ("executor").
+
+Replaces the reference's process/greenlet machinery (`training.py:47-137`,
+`executor.py:16-96`, `algorithm_factory.py:12-61`): instead of one process per GPU group
+plus a server process, each rank (one process per GPU, torchrun-style env) hosts
+
+* a server replica (deterministic: same selection, same aggregation result everywhere),
+* one cohort worker for the clients this rank owns in the round (round-robin over the
+  *selected* clients: `selected[rank::world]` — balanced even under partial participation),
+* the device-resident dataset, model layout and `CohortTrainer`.
+
+Per round: local clients train in waves → uploads are encoded by the client endpoint and
+consumed by the local server replica (on-device, zero copy) → one all-reduce merges all
+ranks → finalize → next round's broadcast is already resident. Metrics per round go to
+`metrics.jsonl` (rounds/s and comm bytes/round, the BASELINE metric).
+"""
+
+from __future__ import annotations
+
+import copy
+import json
+import math
+import os
+import time
+
+import torch
+
+from .data.datasets import create_dataset_collection
+from .engine.trainer import CohortTrainer, HyperParameter
+from .method import CentralizedAlgorithmFactory
+from .models.zoo import build_model
+from .parallel.comm import Comm, get_comm, init_distributed
+from .practitioner import create_practitioners
+from .utils.logging import get_logger
+
+
+def resolve_dtype(config, device) -> torch.dtype:
+    name = (config.compute_dtype or "auto").lower()
+    if name == "auto":
+        return torch.bfloat16 if device.type == "cuda" else torch.float32
+    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
+            "float32": torch.float32}[name]
+
+
+class Session:
+    def __init__(self, config, practitioners=None, comm: Comm | None = None):
+        self.config = copy.deepcopy(config)
+        cfg = self.config
+        if not CentralizedAlgorithmFactory.has_algorithm(cfg.distributed_algorithm):
+            raise ValueError(f"unknown distributed_algorithm {cfg.distributed_algorithm!r}; registered: "
+                             f"{sorted(CentralizedAlgorithmFactory.config)}")
+        self.comm = comm or get_comm()
+        self.device = self.comm.device
+        self.is_main = self.comm.rank == 0
+        self.compute_dtype = resolve_dtype(cfg, self.device)
+        torch.manual_seed(cfg.seed)
+        self.dc = create_dataset_collection(cfg.dataset_name, cfg.dataset_kwargs, cfg.seed, self.device,
+                                            self.compute_dtype)
+        if practitioners is None:
+            labels = self.dc.train.labels if self.dc.spec.kind != "graph" else self.dc.graph.labels_cpu
+            practitioners = create_practitioners(cfg, labels)
+        else:
+            # reference algorithm_factory.py:15-23: worker ids = rank of practitioner id
+            practitioners = sorted(practitioners, key=lambda p: p.id)
+            for wid, p in enumerate(practitioners):
+                p.set_worker_id(wid)
+            cfg.worker_number = len(practitioners)
+        self.practitioners = {p.worker_id: p for p in practitioners}
+        self.model = build_model(cfg.model_name, self.dc.spec, cfg.model_kwargs)
+        self.layout = self.model.layout
+        n_sel = int(cfg.algorithm_kwargs.get("random_client_number", cfg.worker_number) or cfg.worker_number)
+        n_sel = min(n_sel, cfg.worker_number)
+        per_rank = math.ceil(n_sel / self.comm.world)
+        capacity = max(1, min(per_rank, cfg.cohort_size) if cfg.cohort_size else per_rank)
+        self.hyper = HyperParameter.from_config(cfg)
+        self.trainer = CohortTrainer(self.model, self.dc, self.hyper, self.device, self.compute_dtype, capacity)
+        algo = cfg.distributed_algorithm
+        self.server = CentralizedAlgorithmFactory.create_server(
+            algo, {"config": cfg, "session": self}, dict(cfg.endpoint_kwargs.get("server", {})))
+        self.worker = CentralizedAlgorithmFactory.create_client(
+            algo, {"config": cfg, "session": self}, dict(cfg.endpoint_kwargs.get("worker", {})))
+        self.server.endpoint.bind(self.layout, self.device, cfg.seed)
+        self.worker.endpoint.bind(self.layout, self.device, cfg.seed)
+        if self.server.algorithm is not None:
+            self.server.algorithm.bind(cfg, self.layout, self.device, self.comm, self.server)
+        self.metrics: list[dict] = []
+        self.bytes_up_total = 0
+        self.bytes_down_total = 0
+        get_logger().info(
+            "session: algo=%s model=%s params=%d workers=%d ranks=%d capacity/rank=%d device=%s dtype=%s",
+            algo, cfg.model_name, self.layout.num_params, cfg.worker_number, self.comm.world, capacity,
+            self.device, self.compute_dtype)
+
+    # ------------------------------------------------------------------ helpers
+    def local_clients(self, selected: list[int]) -> list[int]:
+        return list(selected[self.comm.rank :: self.comm.world])
+
+    def evaluate(self, rows: torch.Tensor):
+        """Sharded test evaluation of M parameter rows; returns (loss [M], acc [M]) lists."""
+        ls, cs, n = self.trainer.evaluate(rows, batch_size=self.config.eval_batch_size or None,
+                                          shard=(self.comm.rank, self.comm.world))
+        both = torch.stack([ls, cs])
+        self.comm.all_reduce_(both)
+        both = (both / n).cpu()
+        return both[0].tolist(), both[1].tolist()
+
+    def sync(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    # ---------------------------------------------------------------------- run
+    def run(self) -> dict:
+        cfg = self.config
+        server, worker = self.server, self.worker
+        t_start = time.perf_counter()
+        init = server._before_start()
+        theta_recv, down = server.send_result(init)
+        self.bytes_down_total += down
+        if hasattr(server, "run_rounds"):  # methods with their own round structure
+            server.run_rounds(self, theta_recv)
+        else:
+            while not server._stopped():
+                theta_recv = self.run_one_round(theta_recv)
+        self.sync()
+        total = time.perf_counter() - t_start
+        server._server_exit()
+        worker._after_training()
+        get_logger().info("training use %s seconds", total)
+        if self.is_main:
+            os.makedirs(cfg.save_dir, exist_ok=True)
+            with open(os.path.join(cfg.save_dir, "metrics.jsonl"), "wt", encoding="utf8") as f:
+                for m in self.metrics:
+                    f.write(json.dumps(m) + "\n")
+        result = {"performance": server.performance_stat, "metrics": self.metrics,
+                  "bytes_up": self.bytes_up_total, "bytes_down": self.bytes_down_total, "seconds": total}
+        algo = server.algorithm
+        if algo is not None and hasattr(algo, "shapley_values"):
+            result["sv"] = algo.shapley_values
+            result["sv_S"] = getattr(algo, "shapley_values_S", {})
+        return result
+
+    def run_one_round(self, theta_recv: torch.Tensor) -> torch.Tensor:
+        server, worker = self.server, self.worker
+        r = server.round_number
+        t0 = time.perf_counter()
+        selected = list(server.selected)
+        local = self.local_clients(selected)
+        if server.algorithm is not None:
+            server.algorithm.expected_kind = "delta" if getattr(worker, "_send_parameter_diff", True) else "parameter"
+        up0 = worker.endpoint.bytes_sent
+        for msg in worker.run_round(r, theta_recv, local):
+            server._process_worker_data(msg)
+        skipped = sorted(set(range(self.config.worker_number)) - set(selected))
+        if skipped:
+            server._process_worker_data(None, worker_ids=skipped)
+        up_local = worker.endpoint.bytes_sent - up0
+        result = server._aggregate_worker_data()
+        theta_recv, down = server.send_result(result)
+        up = self._sum_scalar(up_local)
+        self.record_round(r, t0, selected, up, down)
+        return theta_recv
+
+    def _sum_scalar(self, v: int) -> int:
+        if self.comm.world == 1:
+            return int(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
+        self.comm.all_reduce_(t)
+        return int(t.item())
+
+    def record_round(self, r, t0, selected, up, down, **extra) -> dict:
+        if self.config.extra.get("sync_round_timing", True):
+            self.sync()
+        wall = time.perf_counter() - t0
+        self.bytes_up_total += up
+        self.bytes_down_total += down
+        stat = self.server.performance_stat.get(r, {})
+        row = {"round": r, "wall_s": wall, "rounds_per_s": 1.0 / max(wall, 1e-9), "selected_clients": len(selected),
+               "comm_bytes_up": up, "comm_bytes_down": down, "comm_bytes_total": up + down,
+               "gpus": self.comm.world, **stat, **extra}
+        self.metrics.append(row)
+        get_logger().info("round %s done in %.3fs (up %.1f MiB, down %.1f MiB)", r, wall, up / 2**20, down / 2**20)
+        return row

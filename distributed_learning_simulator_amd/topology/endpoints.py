@@ -1,0 +1,176 @@
+"""Endpoints: the worker↔server transport of the cohort runtime.
+
+Reference: `ClientEndpoint.send/get/has_data/close`,
+`ServerEndpoint.send/get/broadcast/worker_num/close` over pickled Pipes, plus the
+quantising subclasses in `topology/quantized_endpoint.py:14-116`.
+
+Here a "send" never leaves the device. The client endpoint converts a `CohortMessage` into
+wire format *in place* (quantise → the receiver's dequantised view) and records the exact
+wire bytes per client; the server endpoint's `get` finishes decoding; `broadcast` applies
+downlink compression and charges bytes per receiving client. Byte counts follow the
+reference's `get_message_size` rule on the wire payload.
+
+Fixed reference defects: B2 — `get` passes `None` (skipped client) through
+and decodes once; B3 — client-side quantisation applies to the *uploaded payload* whatever
+its kind (Δ or θ), which is what FedPAQ's analysis charges (`analyze_log.py:263-272`).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..message import CohortMessage
+from ..ops import quant
+from ..utils.logging import get_logger
+
+
+class _Ctx:
+    def __init__(self, layout, device, seed: int):
+        self.layout = layout
+        self.device = device
+        self.seed = seed
+        self.seg_ids = layout.segment_ids(device)
+        self.seg_sizes = layout.segment_sizes(device)
+        self.dense_bytes = layout.num_params * 4
+
+
+class ClientEndpoint:
+    def __init__(self, **kwargs):
+        self.kwargs = kwargs
+        self.ctx: _Ctx | None = None
+        self.bytes_sent = 0
+        self.messages_sent = 0
+        self.dequant_server_data = False
+
+    def bind(self, layout, device, seed: int) -> None:
+        self.ctx = _Ctx(layout, device, seed)
+
+    def _dense_wire(self, msg: CohortMessage) -> list[int]:
+        if msg.block_mask is not None:
+            sizes = msg.extra["block_param_sizes"]  # [nblocks] logical elements
+            sel = (msg.block_mask.float() * sizes.float()[None, :]).sum(1)
+            return [int(v) * 4 for v in sel.tolist()]
+        return [self.ctx.dense_bytes] * msg.size
+
+    def encode(self, msg: CohortMessage, seed: int) -> CohortMessage:
+        msg.wire_bytes = self._dense_wire(msg)
+        return msg
+
+    def send(self, msg: CohortMessage, seed: int = 0) -> CohortMessage:
+        msg = self.encode(msg, seed)
+        self.bytes_sent += int(sum(msg.wire_bytes))
+        self.messages_sent += msg.size
+        return msg
+
+    def receive_broadcast(self, params: torch.Tensor) -> torch.Tensor:
+        return params
+
+    def close(self) -> None:
+        pass
+
+
+class ServerEndpoint:
+    def __init__(self, **kwargs):
+        self.kwargs = kwargs
+        self.ctx: _Ctx | None = None
+        self.bytes_broadcast = 0
+        self.quant_broadcast = False
+
+    def bind(self, layout, device, seed: int) -> None:
+        self.ctx = _Ctx(layout, device, seed)
+
+    def get(self, msg: CohortMessage | None) -> CohortMessage | None:
+        return msg
+
+    def encode_broadcast(self, params: torch.Tensor, seed: int) -> tuple[torch.Tensor, int]:
+        return params, self.ctx.dense_bytes
+
+    def broadcast(self, params: torch.Tensor, n_receivers: int, seed: int = 0) -> tuple[torch.Tensor, int]:
+        """Returns (what receivers reconstruct, total bytes for n_receivers)."""
+        received, per = self.encode_broadcast(params, seed)
+        total = per * n_receivers
+        self.bytes_broadcast += total
+        return received, total
+
+    def close(self) -> None:
+        pass
+
+
+# ------------------------------------------------------------------ quantised
+class QuantClientEndpoint(ClientEndpoint):
+    """Quantise uploads; optionally dequantise server data (`dequant_server_data`)."""
+
+    def quantize(self, msg: CohortMessage, seed: int) -> CohortMessage:
+        raise NotImplementedError
+
+    def encode(self, msg, seed):
+        return self.quantize(msg, seed)
+
+
+class QuantServerEndpoint(ServerEndpoint):
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.quant_broadcast = bool(kwargs.get("quant_broadcast", False))
+
+
+class StochasticQuantClientEndpoint(QuantClientEndpoint):
+    """FedPAQ / fed_obd_sq upload: 255-level stochastic quantisation
+    (reference `quantized_endpoint.py:74-77`)."""
+
+    levels = 255
+
+    def quantize(self, msg, seed):
+        dq, wire = quant.stochastic_quantize(msg.data, self.ctx.seg_ids, self.ctx.seg_sizes, seed, self.levels)
+        msg.data.copy_(dq)
+        if msg.block_mask is not None:
+            frac = self._dense_wire(msg)
+            wire = [int(round(w * f / self.ctx.dense_bytes)) for w, f in zip(wire, frac)]
+        msg.wire_bytes = wire
+        return msg
+
+
+class StochasticQuantServerEndpoint(QuantServerEndpoint):
+    levels = 255
+
+    def encode_broadcast(self, params, seed):
+        if not self.quant_broadcast:
+            return params, self.ctx.dense_bytes
+        dq, wire = quant.stochastic_quantize(params.unsqueeze(0), self.ctx.seg_ids, self.ctx.seg_sizes, seed, self.levels)
+        return dq[0], wire[0]
+
+
+class NNADQClientEndpoint(QuantClientEndpoint):
+    """FedOBD upload quantiser (reference `quantized_endpoint.py:86-101`); logs the
+    compression ratio with the phrase the reference's analyser parses
+    ("worker NNABQ compression ratio", `analyze_log.py:131-134`)."""
+
+    def __init__(self, weight: float | None = None, **kwargs):
+        super().__init__(**kwargs)
+        self.weight = weight
+
+    def quantize(self, msg, seed):
+        if self.weight is None:
+            return super().quantize(msg, seed)
+        seg_mask = msg.extra.get("segment_mask")
+        dq, wire, _ = quant.nnadq_quantize(msg.data, self.ctx.seg_ids, self.ctx.seg_sizes, self.weight, seg_mask)
+        msg.data.copy_(dq)
+        dense = self._dense_wire(msg)
+        msg.wire_bytes = wire
+        for cid, w, d in zip(msg.client_ids, wire, dense):
+            get_logger().debug("worker %d NNABQ compression ratio is %s", cid, w / max(d, 1))
+        msg.extra["compression_ratio"] = [w / max(d, 1) for w, d in zip(wire, dense)]
+        return msg
+
+
+class NNADQServerEndpoint(QuantServerEndpoint):
+    def __init__(self, weight: float | None = None, **kwargs):
+        super().__init__(**kwargs)
+        self.weight = weight
+
+    def encode_broadcast(self, params, seed):
+        if not self.quant_broadcast or self.weight is None:
+            return params, self.ctx.dense_bytes
+        dq, wire, _ = quant.nnadq_quantize(params.unsqueeze(0), self.ctx.seg_ids, self.ctx.seg_sizes, self.weight)
+        ratio = wire[0] / self.ctx.dense_bytes
+        get_logger().info("broadcast NNABQ compression ratio is %s", ratio)
+        return dq[0], wire[0]

@@ -1,0 +1,53 @@
+"""Wall-clock and device-event timers.
+
+The reference only times the whole run (`training.py:88,136`, "training use %s seconds").
+Here every round is split into phases (train / upload / aggregate / eval) so rounds/s can be
+attributed; device phases are timed with HIP events through `torch.cuda.Event` when on GPU.
+"""
+
+from __future__ import annotations
+
+import time
+from collections import defaultdict
+from contextlib import contextmanager
+
+import torch
+
+
+class TimeCounter:
+    def __init__(self) -> None:
+        self._start = time.perf_counter()
+
+    def reset(self) -> None:
+        self._start = time.perf_counter()
+
+    def elapsed_milliseconds(self) -> float:
+        return (time.perf_counter() - self._start) * 1000.0
+
+
+class PhaseTimer:
+    """Accumulates per-phase wall time. `sync=True` synchronises the device at phase
+    boundaries so the attribution is exact (used by the profiler-style reports, not in the
+    hot benchmark path)."""
+
+    def __init__(self, sync: bool = False) -> None:
+        self.sync = sync
+        self.totals: dict[str, float] = defaultdict(float)
+
+    @contextmanager
+    def phase(self, name: str):
+        if self.sync and torch.cuda.is_available():
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            if self.sync and torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self.totals[name] += time.perf_counter() - t0
+
+    def snapshot(self) -> dict[str, float]:
+        return dict(self.totals)
+
+    def reset(self) -> None:
+        self.totals.clear()

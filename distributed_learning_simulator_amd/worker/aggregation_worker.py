@@ -1,0 +1,82 @@
+"""FedAvg-family client cohort.
+
+Reference `worker/aggregation_worker.py:16-144`: defaults `send_parameter_diff=True`,
+`reuse_learning_rate=False`; `_get_sent_data` uploads Δ = θ − θ_g (or θ) with
+`dataset_size`; `_load_result_from_server` loads the broadcast model (optimizer state reset
+unless `reuse_learning_rate`, `util/model.py:6-23`); a `None` broadcast means "not selected
+this round" (fixed B1: the client just skips the round).
+
+Cohort execution: clients of this rank are processed in waves of at most `capacity` rows;
+each wave = load θ_g into K rows (one broadcast launch) → lock-step local training →
+Δ rows computed IN PLACE in the parameter buffer (one launch) → `endpoint.send` (wire
+format + byte accounting) → yielded to the server replica before the next wave reuses the
+buffers.
+"""
+
+from __future__ import annotations
+
+from typing import Iterator
+
+import torch
+
+from ..message import CohortMessage
+from ..ops import fl
+from .worker import Worker
+
+
+class AggregationWorker(Worker):
+    def __init__(self, config, endpoint, session=None, **kwargs):
+        super().__init__(config, endpoint, session, **kwargs)
+        self._send_parameter_diff = True
+        self._reuse_learning_rate = False
+        self._keep_optimizer_state = False
+        self._epochs = config.epoch
+
+    # ------------------------------------------------------------ round driver
+    def local_epochs(self) -> int:
+        return self._epochs
+
+    def run_round(self, round_num: int, theta_g: torch.Tensor, client_ids: list[int]) -> Iterator[CohortMessage]:
+        self._round_num = round_num
+        cap = self.trainer.capacity
+        for w0 in range(0, len(client_ids), cap):
+            wave = client_ids[w0 : w0 + cap]
+            yield self.train_wave(round_num, theta_g, wave)
+
+    def train_wave(self, round_num: int, theta_g: torch.Tensor, wave: list[int]) -> CohortMessage:
+        K = len(wave)
+        self._load_result_from_server(theta_g, K)
+        schedule = self.build_schedule(round_num, wave)
+        stats = self.trainer.train(schedule, executor=self)
+        self.log_train_stats(wave, stats, len(schedule.epoch_end) - 1)
+        msg = self._get_sent_data(wave, theta_g, stats)
+        return self.endpoint.send(msg, seed=self.upload_seed(round_num, wave[0]))
+
+    def build_schedule(self, round_num: int, wave: list[int]):
+        return self.trainer.build_schedule(
+            self.shards(wave), self.local_epochs(),
+            seed=self.config.seed * 100_003 + round_num * 1009 + wave[0],
+        )
+
+    def upload_seed(self, round_num: int, first_client: int) -> int:
+        return (self.config.seed * 7_368_787 + round_num * 104_729 + first_client) & 0x7FFFFFFF
+
+    # -------------------------------------------------------------- hooks
+    def _load_result_from_server(self, theta_g: torch.Tensor, K: int) -> None:
+        self.trainer.load_global(theta_g, K)
+        if not self._keep_optimizer_state:
+            # torch semantics: fresh optimizer => momentum buffer re-initialised with the first
+            # gradient (first-step flags in the schedule); Adam moments zeroed
+            self.trainer.reset_optimizer(K)
+
+    def _get_sent_data(self, wave: list[int], theta_g: torch.Tensor, stats) -> CohortMessage:
+        K = len(wave)
+        rows = self.trainer.buffers.theta[:K]
+        if self._send_parameter_diff:
+            data = fl.delta_rows(rows, theta_g, out=rows)
+            kind = "delta"
+        else:
+            data = rows
+            kind = "parameter"
+        return CohortMessage(client_ids=list(wave), dataset_sizes=self.dataset_sizes(wave).to(rows.device),
+                             kind=kind, data=data, layout=self.trainer.layout)

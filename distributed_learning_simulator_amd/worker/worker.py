@@ -1,0 +1,60 @@
+"""Worker role: a *cohort* of clients resident on one rank.
+
+Reference `worker/worker.py:15-95` (one `Worker` per client, serial inside a process,
+`trainer.train()` per round) and `worker/client.py:9-22` (blocking receive by polling).
+Here one `Worker` object stands for all clients a rank hosts in a round; they train
+together through the `CohortTrainer`. Client identity (practitioner, shard, dataset size)
+is kept per row. Hook-style overridable methods keep the reference's names:
+`_before_training`, `_get_sent_data`, `_load_result_from_server`, `_stopped`.
+"""
+
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ..utils.logging import get_logger
+
+
+class Worker:
+    def __init__(self, config, endpoint, session=None, **kwargs):
+        self.config = config
+        self.endpoint = endpoint
+        self.session = session
+        self._round_num = 0
+        self._force_stop = False
+        self.name = "worker cohort"
+
+    @property
+    def trainer(self):
+        return self.session.trainer
+
+    @property
+    def round_num(self) -> int:
+        return self._round_num
+
+    @property
+    def save_dir(self) -> str:
+        return os.path.join(self.config.save_dir, f"worker_rank{self.session.comm.rank}")
+
+    def shards(self, client_ids: list[int]) -> list[torch.Tensor]:
+        name = self.session.dc.spec.name
+        return [self.session.practitioners[c].indices(name) for c in client_ids]
+
+    def dataset_sizes(self, client_ids: list[int]) -> torch.Tensor:
+        name = self.session.dc.spec.name
+        return torch.tensor([self.session.practitioners[c].dataset_size(name) for c in client_ids],
+                            dtype=torch.float32)
+
+    def _stopped(self) -> bool:
+        return self._round_num > self.config.round or self._force_stop
+
+    def _after_training(self) -> None:
+        pass
+
+    def log_train_stats(self, client_ids, stats, epoch_index: int) -> None:
+        if get_logger().isEnabledFor(10):  # DEBUG: per-client lines (analyze_log parity)
+            loss, acc = stats.epoch_metrics(epoch_index)
+            for c, l, a in zip(client_ids, loss.tolist(), acc.tolist()):
+                get_logger().debug("worker %d round %d train loss %.4f accuracy %.4f", c, self._round_num, l, a)
