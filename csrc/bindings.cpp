@@ -1,0 +1,129 @@
+// pybind11 module `_dls_hip`: thin launch bindings. Python passes raw device pointers
+// (tensor.data_ptr()) and the current HIP stream handle; shapes/strides are validated on
+// the Python side (ops/hip.py) before any launch.
+#include <pybind11/pybind11.h>
+
+#include "dls.h"
+
+namespace py = pybind11;
+typedef uintptr_t ptr;
+
+template <typename T>
+static T* P(ptr p) {
+  return reinterpret_cast<T*>(p);
+}
+static hipStream_t S(ptr s) { return reinterpret_cast<hipStream_t>(s); }
+
+PYBIND11_MODULE(_dls_hip, m) {
+  m.doc() = "gfx950 kernels for the MI355X-native cohort FL simulator";
+
+  m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
+                      int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
+                      int relu, int K, ptr s) {
+    ConvNTParams p{P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), P<const bf16_t>(bias), x_cs, y_cs, w_cs, b_cs,
+                   B, H, W, C, OH, OW, KH, KW, stride, pad, dil, M, N, R, rep, relu};
+    conv_nt(p, K, S(s));
+  });
+  m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,
+                      int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, ptr s) {
+    ConvTNParams p{P<const bf16_t>(dy), P<const bf16_t>(x), P<float>(dw), dy_cs, x_cs, dw_cs, B, H, W, C, OH, OW, KH,
+                   KW, stride, pad, M, Co, R, 1, M};
+    conv_tn(p, K, S(s));
+  });
+  m.def("conv_tn_splitk", &conv_tn_splitk);
+  m.def("weight_flip_transpose", [](ptr w, ptr wt, long w_cs, int K, int Co, int KH, int KW, int Ci, ptr s) {
+    weight_flip_transpose(P<const bf16_t>(w), P<bf16_t>(wt), w_cs, K, Co, KH, KW, Ci, S(s));
+  });
+
+  m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
+                     int R, int C, int relu, float eps, int rep, ptr ws, ptr s) {
+    bn_fwd(P<const bf16_t>(x), P<const bf16_t>(gamma), P<const bf16_t>(beta), P<const bf16_t>(res), P<bf16_t>(y),
+           P<float>(mean), P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws), S(s));
+  });
+  m.def("bn_bwd", [](ptr dy, ptr x, ptr y, ptr mean, ptr rstd, ptr gamma, ptr valid, long g_cs, int K, int R, int C,
+                     int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr s) {
+    bn_bwd(P<const bf16_t>(dy), P<const bf16_t>(x), P<const bf16_t>(y), P<const float>(mean), P<const float>(rstd),
+           P<const bf16_t>(gamma), P<const int>(valid), g_cs, K, R, C, relu, P<bf16_t>(dx), P<bf16_t>(dpre),
+           P<float>(dgamma), P<float>(dbeta), dg_cs, P<float>(ws), S(s));
+  });
+  m.def("ln_fwd", [](ptr x, ptr gamma, ptr beta, ptr y, ptr mean, ptr rstd, long g_cs, int K, long rpc, int C,
+                     float eps, int rep, ptr s) {
+    ln_fwd(P<const bf16_t>(x), P<const bf16_t>(gamma), P<const bf16_t>(beta), P<bf16_t>(y), P<float>(mean),
+           P<float>(rstd), g_cs, K, rpc, C, eps, rep, S(s));
+  });
+  m.def("ln_bwd", [](ptr dy, ptr x, ptr mean, ptr rstd, ptr gamma, long g_cs, int K, long rpc, int C, ptr dx,
+                     ptr dgamma, ptr dbeta, long dg_cs, ptr s) {
+    ln_bwd(P<const bf16_t>(dy), P<const bf16_t>(x), P<const float>(mean), P<const float>(rstd),
+           P<const bf16_t>(gamma), g_cs, K, rpc, C, P<bf16_t>(dx), P<float>(dgamma), P<float>(dbeta), dg_cs, nullptr,
+           S(s));
+  });
+  m.def("col_sum", [](ptr x, ptr out, long out_cs, int K, long rows, int C, ptr s) {
+    col_sum(P<const bf16_t>(x), P<float>(out), out_cs, K, rows, C, S(s));
+  });
+
+  m.def("pool_fwd", [](ptr x, ptr y, ptr idx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
+                       int pad, int mode, ptr s) {
+    pool_fwd(P<const bf16_t>(x), P<bf16_t>(y), P<int>(idx), K, B, H, W, C, OH, OW, k, stride, pad, mode, S(s));
+  });
+  m.def("pool_bwd", [](ptr dy, ptr idx, ptr dx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
+                       int pad, int mode, ptr s) {
+    pool_bwd(P<const bf16_t>(dy), P<const int>(idx), P<bf16_t>(dx), K, B, H, W, C, OH, OW, k, stride, pad, mode, S(s));
+  });
+  m.def("gap_fwd", [](ptr x, ptr y, int KB, int HW, int C, ptr s) { gap_fwd(P<const bf16_t>(x), P<bf16_t>(y), KB, HW, C, S(s)); });
+  m.def("gap_bwd", [](ptr dy, ptr dx, int KB, int HW, int C, ptr s) { gap_bwd(P<const bf16_t>(dy), P<bf16_t>(dx), KB, HW, C, S(s)); });
+  m.def("ce_fwd_bwd", [](ptr logits, ptr labels, ptr valid, ptr loss, ptr correct, ptr dlogits, int K, int B, int NC,
+                         ptr s) {
+    ce_fwd_bwd(P<const bf16_t>(logits), P<const int>(labels), P<const int>(valid), P<float>(loss), P<float>(correct),
+               P<bf16_t>(dlogits), K, B, NC, S(s));
+  });
+  m.def("relu_bwd", [](ptr dy, ptr y, ptr dx, long n, ptr s) { relu_bwd(P<const bf16_t>(dy), P<const bf16_t>(y), P<bf16_t>(dx), n, S(s)); });
+
+  m.def("sgd_step", [](ptr theta, ptr grad, ptr mom, ptr shadow, ptr lr, ptr active, ptr first, int K, long Pn, long ld,
+                       float wd, float momentum, float dampening, int nesterov, ptr s) {
+    sgd_step(P<float>(theta), P<const float>(grad), P<float>(mom), P<bf16_t>(shadow), P<const float>(lr),
+             P<const uint8_t>(active), P<const uint8_t>(first), K, Pn, ld, wd, momentum, dampening, nesterov, S(s));
+  });
+  m.def("adam_step", [](ptr theta, ptr grad, ptr mm, ptr v, ptr shadow, ptr lr, ptr active, ptr step, int K, long Pn,
+                        long ld, float b1, float b2, float eps, float wd, ptr s) {
+    adam_step(P<float>(theta), P<const float>(grad), P<float>(mm), P<float>(v), P<bf16_t>(shadow), P<const float>(lr),
+              P<const uint8_t>(active), P<const float>(step), K, Pn, ld, b1, b2, eps, wd, S(s));
+  });
+  m.def("broadcast_rows", [](ptr theta, ptr shadow, ptr src, int K, long Pn, long ld, ptr s) {
+    broadcast_rows(P<float>(theta), P<bf16_t>(shadow), P<const float>(src), K, Pn, ld, S(s));
+  });
+  m.def("delta_rows", [](ptr theta, ptr base, ptr out, int K, long Pn, long ld, ptr s) {
+    delta_rows(P<const float>(theta), P<const float>(base), P<float>(out), K, Pn, ld, S(s));
+  });
+  m.def("weighted_sum", [](ptr x, ptr w, ptr out, int K, long Pn, long ld, ptr s) {
+    weighted_sum(P<const float>(x), P<const float>(w), P<float>(out), K, Pn, ld, S(s));
+  });
+  m.def("masked_weighted_sum", [](ptr x, ptr mask, ptr w, ptr num, ptr den, int K, long Pn, long ld, ptr s) {
+    masked_weighted_sum(P<const float>(x), P<const uint8_t>(mask), P<const float>(w), P<float>(num), P<float>(den), K, Pn,
+                        ld, S(s));
+  });
+  m.def("dropout_mask", [](ptr mask, long n, float p, uint32_t seed, ptr s) { dropout_mask(P<uint8_t>(mask), n, p, seed, S(s)); });
+  m.def("block_sq_norms", [](ptr x, ptr ids, ptr out, int K, long Pn, long ld, int nb, ptr s) {
+    block_sq_norms(P<const float>(x), P<const int>(ids), P<float>(out), K, Pn, ld, nb, S(s));
+  });
+  m.def("seg_minmax", [](ptr x, ptr seg, ptr mn, ptr mx, int K, long Pn, long ld, int nseg, ptr s) {
+    seg_minmax(P<const float>(x), P<const int>(seg), P<float>(mn), P<float>(mx), K, Pn, ld, nseg, S(s));
+  });
+  m.def("stochastic_qdq", [](ptr x, ptr seg, ptr mn, ptr mx, int K, long Pn, long ld, int nseg, uint32_t seed,
+                             int levels, ptr s) {
+    stochastic_qdq(P<float>(x), P<const int>(seg), P<const float>(mn), P<const float>(mx), K, Pn, ld, nseg, seed, levels,
+                   S(s));
+  });
+  m.def("sign_pack", [](ptr g, ptr out, int K, long Pn, long ld, ptr s) { sign_pack(P<const float>(g), P<uint8_t>(out), K, Pn, ld, S(s)); });
+  m.def("sign_vote", [](ptr packed, ptr active, ptr votes, int K, long Pn, ptr s) {
+    sign_vote(P<const uint8_t>(packed), P<const uint8_t>(active), P<int>(votes), K, Pn, S(s));
+  });
+  m.def("embedding_fwd", [](ptr tok, ptr table, ptr out, int K, long n_tok, int D, long t_cs, int rep, ptr s) {
+    embedding_fwd(P<const int>(tok), P<const bf16_t>(table), P<bf16_t>(out), K, n_tok, D, t_cs, rep, S(s));
+  });
+  m.def("embedding_bwd", [](ptr tok, ptr dy, ptr dtable, int K, long n_tok, int D, long t_cs, ptr s) {
+    embedding_bwd(P<const int>(tok), P<const bf16_t>(dy), P<float>(dtable), K, n_tok, D, t_cs, S(s));
+  });
+  m.def("gather_rows", [](ptr src, ptr idx, ptr dst, long n, long row_elems, ptr s) {
+    gather_rows(P<const bf16_t>(src), P<const int>(idx), P<bf16_t>(dst), n, row_elems, S(s));
+  });
+}

@@ -1,0 +1,71 @@
+// Shared helpers for the gfx950 (CDNA4, MI355X) kernels of the cohort FL simulator.
+// Wave64 everywhere; bf16 stored as raw uint16 and converted with RNE.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DLS_CHECK(x)                                                                  \
+  do {                                                                                \
+    hipError_t err__ = (x);                                                           \
+    if (err__ != hipSuccess) {                                                        \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(err__), __FILE__, \
+              __LINE__);                                                              \
+    }                                                                                 \
+  } while (0)
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// 8 bf16 packed in a uint4 (16 B)
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block id (guide §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD (shared L2) instead of round-robin.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int nxcd = 8;
+  if (nwg < nxcd) return orig;
+  const int q = nwg / nxcd, r = nwg % nxcd;
+  const int xcd = orig % nxcd, pos = orig / nxcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

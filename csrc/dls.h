@@ -1,0 +1,88 @@
+// Launch API of the gfx950 kernels (host side). All launches are asynchronous on the given
+// stream and never allocate or synchronise, so they can be captured into hipGraphs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+struct ConvNTParams {
+  const bf16_t* x;  // A source image [K][B][H][W][C]
+  const bf16_t* w;  // B rows [N][R] per weight row
+  bf16_t* y;        // [K][M][N]
+  const bf16_t* bias;
+  long x_cs, y_cs, w_cs, b_cs;
+  int B, H, W, C;
+  int OH, OW, KH, KW, stride, pad, dil;
+  int M, N, R;
+  int rep;
+  int relu;
+};
+
+struct ConvTNParams {
+  const bf16_t* dy;  // [K][M][Co]
+  const bf16_t* x;   // [K][B][H][W][C]
+  float* dw;         // [K] rows (stride dw_cs) of [Co][R]
+  long dy_cs, x_cs, dw_cs;
+  int B, H, W, C, OH, OW, KH, KW, stride, pad;
+  int M, Co, R;
+  int splitk, m_per_split;
+};
+
+void conv_nt(const ConvNTParams& p, int K, hipStream_t s);
+void conv_tn(ConvTNParams p, int K, hipStream_t s);
+int conv_tn_splitk(int K, int Co, int R, int M);
+void weight_flip_transpose(const bf16_t* w, bf16_t* wt, long w_cs, int K, int Co, int KH, int KW, int Ci,
+                           hipStream_t s);
+
+// ---------------------------------------------------------------- normalisation
+void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
+            float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
+            float* ws, hipStream_t s);
+void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
+            const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
+            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, hipStream_t s);
+void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,
+            long g_cs, int K, long rows_per_client, int C, float eps, int rep, hipStream_t s);
+void ln_bwd(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd, const bf16_t* gamma,
+            long g_cs, int K, long rows_per_client, int C, bf16_t* dx, float* dgamma, float* dbeta, long dg_cs,
+            float* ws, hipStream_t s);
+void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s);
+
+// ------------------------------------------------------------------- elementwise
+void pool_fwd(const bf16_t* x, bf16_t* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k,
+              int stride, int pad, int mode, hipStream_t s);
+void pool_bwd(const bf16_t* dy, const int* idx, bf16_t* dx, int K, int B, int H, int W, int C, int OH, int OW,
+              int k, int stride, int pad, int mode, hipStream_t s);
+void gap_fwd(const bf16_t* x, bf16_t* y, int KB, int HW, int C, hipStream_t s);
+void gap_bwd(const bf16_t* dy, bf16_t* dx, int KB, int HW, int C, hipStream_t s);
+void ce_fwd_bwd(const bf16_t* logits, const int* labels, const int* valid, float* loss, float* correct,
+                bf16_t* dlogits, int K, int B, int NC, hipStream_t s);
+void relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s);
+
+// ------------------------------------------------------------- FL / optimiser
+void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
+              const uint8_t* first, int K, long P, long ld, float wd, float momentum, float dampening, int nesterov,
+              hipStream_t s);
+void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shadow, const float* lr,
+               const uint8_t* active, const float* step, int K, long P, long ld, float b1, float b2, float eps,
+               float wd, hipStream_t s);
+void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s);
+void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s);
+void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s);
+void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
+                         long ld, hipStream_t s);
+void dropout_mask(uint8_t* mask, long n, float p, uint32_t seed, hipStream_t s);
+void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
+                    hipStream_t s);
+void seg_minmax(const float* x, const int* seg, float* mn, float* mx, int K, long P, long ld, int nseg,
+                hipStream_t s);
+void stochastic_qdq(float* x, const int* seg, const float* mn, const float* mx, int K, long P, long ld, int nseg,
+                    uint32_t seed, int levels, hipStream_t s);
+void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s);
+void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, long P, hipStream_t s);
+void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, long n_tok, int D, long t_cs,
+                   int rep, hipStream_t s);
+void embedding_bwd(const int* tokens, const bf16_t* dy, float* dtable, int K, long n_tok, int D, long t_cs,
+                   hipStream_t s);
+void gather_rows(const bf16_t* src, const int* idx, bf16_t* dst, long n, long row_elems, hipStream_t s);

@@ -1,0 +1,552 @@
+// Memory-bound kernels (gfx950): pooling, global-average-pool, fused softmax-CE fwd+bwd,
+// the fused optimiser steps over flat [K, P] client buffers, FedAvg weighted row reductions,
+// and the transport-compression kernels (dropout masks, stochastic quantisation, 1-bit sign
+// pack / majority vote). All vectorised to 16-B accesses where the layout allows.
+#include "common.h"
+#include "dls.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t seed) {
+  x ^= seed * 0x9E3779B9u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// ------------------------------------------------------------------ pooling (NHWC)
+// mode 0 = max (records argmax as flat input spatial index), 1 = average
+__global__ void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int* __restrict__ idx,
+                                long total, int H, int W, int C, int OH, int OW, int k, int stride, int pad,
+                                int mode) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C;
+  long t = i / C;
+  const int ow = t % OW;
+  t /= OW;
+  const int oh = t % OH;
+  const long img = t / OH;
+  const bf16_t* xi = x + img * H * W * C;
+  float best = -INFINITY, acc = 0.f;
+  int bi = -1;
+  for (int a = 0; a < k; ++a) {
+    const int ih = oh * stride - pad + a;
+    if (ih < 0 || ih >= H) continue;
+    for (int b = 0; b < k; ++b) {
+      const int iw = ow * stride - pad + b;
+      if (iw < 0 || iw >= W) continue;
+      const float v = bf2f(xi[((long)ih * W + iw) * C + c]);
+      if (mode == 0) {
+        if (v > best) {
+          best = v;
+          bi = ih * W + iw;
+        }
+      } else {
+        acc += v;
+      }
+    }
+  }
+  if (mode == 0) {
+    y[i] = f2bf(best);
+    idx[i] = bi;
+  } else {
+    y[i] = f2bf(acc / (float)(k * k));
+  }
+}
+
+// gather-form backward (no atomics): each input element sums the windows that cover it
+__global__ void pool_bwd_kernel(const bf16_t* __restrict__ dy, const int* __restrict__ idx, bf16_t* __restrict__ dx,
+                                long total, int H, int W, int C, int OH, int OW, int k, int stride, int pad,
+                                int mode) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C;
+  long t = i / C;
+  const int iw = t % W;
+  t /= W;
+  const int ih = t % H;
+  const long img = t / H;
+  const long obase = img * OH * OW * C;
+  float acc = 0.f;
+  const int oh_lo = max(0, (ih + pad - k + stride) / stride), oh_hi = min(OH - 1, (ih + pad) / stride);
+  const int ow_lo = max(0, (iw + pad - k + stride) / stride), ow_hi = min(OW - 1, (iw + pad) / stride);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    if (ih + pad - oh * stride < 0 || ih + pad - oh * stride >= k) continue;
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      if (iw + pad - ow * stride < 0 || iw + pad - ow * stride >= k) continue;
+      const long o = obase + ((long)oh * OW + ow) * C + c;
+      if (mode == 0) {
+        if (idx[o] == ih * W + iw) acc += bf2f(dy[o]);
+      } else {
+        acc += bf2f(dy[o]) / (float)(k * k);
+      }
+    }
+  }
+  dx[i] = f2bf(acc);
+}
+
+// global average pool: [KB][HW][C] -> [KB][C]
+__global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int HW, int C, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long img = i / C;
+  const int c = i % C;
+  const bf16_t* p = x + img * HW * C + c;
+  float s = 0.f;
+  for (int j = 0; j < HW; ++j) s += bf2f(p[(long)j * C]);
+  y[i] = f2bf(s / HW);
+}
+
+__global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int HW, int C, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C;
+  const long img = i / ((long)HW * C);
+  dx[i] = f2bf(bf2f(dy[img * C + c]) / HW);
+}
+
+// fused softmax cross-entropy: one wave per sample row; per-client mean over valid rows.
+// Writes loss[K] (mean), correct[K] and dlogits = (softmax - onehot)/n_k (0 on padded rows).
+__global__ void __launch_bounds__(256) ce_kernel(const bf16_t* __restrict__ logits, const int* __restrict__ labels,
+                                                 const int* __restrict__ valid, float* __restrict__ loss,
+                                                 float* __restrict__ correct, bf16_t* __restrict__ dlogits, int B,
+                                                 int NC) {
+  const int k = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const int nv = valid ? valid[k] : B;
+  const long off = ((long)k * B + row) * NC;
+  if (row >= nv) {
+    for (int c = lane; c < NC; c += 64) dlogits[off + c] = 0;
+    return;
+  }
+  const float inv_n = 1.f / (float)max(nv, 1);
+  float mx = -INFINITY;
+  int amax = 0;
+  for (int c = lane; c < NC; c += 64) {
+    const float v = bf2f(logits[off + c]);
+    if (v > mx) {
+      mx = v;
+      amax = c;
+    }
+  }
+  // wave argmax (first max index on ties)
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oi = __shfl_xor(amax, o, 64);
+    if (om > mx || (om == mx && oi < amax)) {
+      mx = om;
+      amax = oi;
+    }
+  }
+  float se = 0.f;
+  for (int c = lane; c < NC; c += 64) se += __expf(bf2f(logits[off + c]) - mx);
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  const int lab = labels[(long)k * B + row];
+  for (int c = lane; c < NC; c += 64) {
+    const float pr = __expf(bf2f(logits[off + c]) - lse);
+    dlogits[off + c] = f2bf((pr - (c == lab ? 1.f : 0.f)) * inv_n);
+  }
+  if (lane == 0) {
+    const float nll = lse - bf2f(logits[off + lab]);
+    atomicAdd(&loss[k], nll * inv_n);
+    if (amax == lab) atomicAdd(&correct[k], 1.f);
+  }
+}
+
+__global__ void relu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, bf16_t* __restrict__ dx,
+                                long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
+}
+
+// ------------------------------------------------------------- optimiser steps
+// grid: (chunks of P/4, K). float4 over the row; per-client lr / active / first-step flags.
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ theta, const float* __restrict__ grad,
+                                                  float* __restrict__ mom, bf16_t* __restrict__ shadow,
+                                                  const float* __restrict__ lr, const uint8_t* __restrict__ active,
+                                                  const uint8_t* __restrict__ first, long P4, long ld, float wd,
+                                                  float momentum, float dampening, int nesterov) {
+  const int k = blockIdx.y;
+  if (!active[k]) return;
+  const float a = lr[k];
+  const bool fs = first[k] != 0;
+  const long base = (long)k * ld;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
+    float4 t = reinterpret_cast<float4*>(theta + base)[i];
+    float4 g = reinterpret_cast<const float4*>(grad + base)[i];
+    float tv[4] = {t.x, t.y, t.z, t.w}, gv[4] = {g.x, g.y, g.z, g.w};
+    float mv[4];
+    if (momentum != 0.f) {
+      float4 m = reinterpret_cast<float4*>(mom + base)[i];
+      mv[0] = m.x;
+      mv[1] = m.y;
+      mv[2] = m.z;
+      mv[3] = m.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gg = gv[j] + wd * tv[j];
+      if (momentum != 0.f) {
+        mv[j] = fs ? gg : momentum * mv[j] + (1.f - dampening) * gg;
+        gg = nesterov ? gg + momentum * mv[j] : mv[j];
+      }
+      tv[j] -= a * gg;
+    }
+    reinterpret_cast<float4*>(theta + base)[i] = make_float4(tv[0], tv[1], tv[2], tv[3]);
+    if (momentum != 0.f) reinterpret_cast<float4*>(mom + base)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    if (shadow) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(tv[0]) | ((uint32_t)f2bf(tv[1]) << 16);
+      u.y = (uint32_t)f2bf(tv[2]) | ((uint32_t)f2bf(tv[3]) << 16);
+      reinterpret_cast<uint2*>(shadow + base)[i] = u;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ theta, const float* __restrict__ grad,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16_t* __restrict__ shadow, const float* __restrict__ lr,
+                                                   const uint8_t* __restrict__ active, const float* __restrict__ step,
+                                                   long P, long ld, float b1, float b2, float eps, float wd) {
+  const int k = blockIdx.y;
+  if (!active[k]) return;
+  const float a = lr[k];
+  const float t = step[k];
+  const float c1 = 1.f - __powf(b1, t), c2 = 1.f - __powf(b2, t);
+  const long base = (long)k * ld;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    const float th = theta[base + i];
+    const float g = grad[base + i] + wd * th;
+    const float mm = b1 * m[base + i] + (1.f - b1) * g;
+    const float vv = b2 * v[base + i] + (1.f - b2) * g * g;
+    m[base + i] = mm;
+    v[base + i] = vv;
+    const float nt = th - a * (mm / c1) / (sqrtf(vv / c2) + eps);
+    theta[base + i] = nt;
+    if (shadow) shadow[base + i] = f2bf(nt);
+  }
+}
+
+__global__ void broadcast_kernel(float* __restrict__ theta, bf16_t* __restrict__ shadow,
+                                 const float* __restrict__ src, long P4, long ld) {
+  const int k = blockIdx.y;
+  const long base = (long)k * ld;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
+    const float4 s = reinterpret_cast<const float4*>(src)[i];
+    reinterpret_cast<float4*>(theta + base)[i] = s;
+    if (shadow) {
+      uint2 u;
+      u.x = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
+      u.y = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
+      reinterpret_cast<uint2*>(shadow + base)[i] = u;
+    }
+  }
+}
+
+__global__ void delta_kernel(const float* __restrict__ theta, const float* __restrict__ base_p,
+                             float* __restrict__ out, long P4, long ld) {
+  const int k = blockIdx.y;
+  const long base = (long)k * ld;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
+    const float4 t = reinterpret_cast<const float4*>(theta + base)[i];
+    const float4 b = reinterpret_cast<const float4*>(base_p)[i];
+    reinterpret_cast<float4*>(out + base)[i] = make_float4(t.x - b.x, t.y - b.y, t.z - b.z, t.w - b.w);
+  }
+}
+
+// Σ_k w_k x[k, :] with fp64 accumulation (reference FedAvg accumulates in float64)
+__global__ void __launch_bounds__(256) weighted_sum_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           float* __restrict__ out, int K, long P4, long ld) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int k = 0; k < K; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(x + (long)k * ld)[i];
+      const double wk = w[k];
+      a0 += wk * v.x;
+      a1 += wk * v.y;
+      a2 += wk * v.z;
+      a3 += wk * v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+  }
+}
+
+__global__ void masked_weighted_sum_kernel(const float* __restrict__ x, const uint8_t* __restrict__ mask,
+                                           const float* __restrict__ w, float* __restrict__ num,
+                                           float* __restrict__ den, int K, long P, long ld) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    double a = 0, d = 0;
+    for (int k = 0; k < K; ++k) {
+      if (mask[(long)k * ld + i]) {
+        a += (double)w[k] * x[(long)k * ld + i];
+        d += w[k];
+      }
+    }
+    num[i] = (float)a;
+    den[i] = (float)d;
+  }
+}
+
+__global__ void dropout_mask_kernel(uint8_t* __restrict__ mask, long n, float p, uint32_t seed) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // matches ops.fl.philox_uniform: hash of (seed, element index)
+  const uint32_t h = mix32((uint32_t)(i & 0xffffffffu), seed);
+  mask[i] = ((float)h * (1.f / 4294967296.f)) >= p;
+}
+
+// Σ x² per (client, block); one block-stride loop, LDS-free wave reduction + atomics
+__global__ void block_sq_kernel(const float* __restrict__ x, const int* __restrict__ ids, float* __restrict__ out,
+                                long P, long ld, int nb) {
+  const int k = blockIdx.y;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    const int b = ids[i];
+    if (b >= 0) {
+      const float v = x[(long)k * ld + i];
+      atomicAdd(&out[(long)k * nb + b], v * v);
+    }
+  }
+}
+
+__global__ void seg_minmax_kernel(const float* __restrict__ x, const int* __restrict__ seg, float* __restrict__ mn,
+                                  float* __restrict__ mx, long P, long ld, int nseg) {
+  // per block: a contiguous range; reduce runs of equal segment id within each wave
+  const int k = blockIdx.y;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int s = (i < P) ? seg[i] : -1;
+  float lo = (i < P) ? x[(long)k * ld + i] : INFINITY;
+  float hi = (i < P) ? x[(long)k * ld + i] : -INFINITY;
+  // segmented wave reduction (segments are contiguous, so equal ids are adjacent)
+  for (int o = 1; o < 64; o <<= 1) {
+    const int so = __shfl_down(s, o, 64);
+    const float lo2 = __shfl_down(lo, o, 64), hi2 = __shfl_down(hi, o, 64);
+    if (lane + o < 64 && so == s) {
+      lo = fminf(lo, lo2);
+      hi = fmaxf(hi, hi2);
+    }
+  }
+  const int sprev = __shfl_up(s, 1, 64);
+  if (s >= 0 && (lane == 0 || sprev != s)) {
+    // float atomics on min/max via int ordering trick
+    float* pmn = &mn[(long)k * nseg + s];
+    float* pmx = &mx[(long)k * nseg + s];
+    int* imn = reinterpret_cast<int*>(pmn);
+    int* imx = reinterpret_cast<int*>(pmx);
+    if (lo >= 0)
+      atomicMin(imn, __float_as_int(lo));
+    else
+      atomicMax(reinterpret_cast<unsigned*>(imn), __float_as_uint(lo)), (void)0;
+    if (hi >= 0)
+      atomicMax(imx, __float_as_int(hi));
+    else
+      atomicMin(reinterpret_cast<unsigned*>(imx), __float_as_uint(hi));
+  }
+}
+
+__global__ void stochastic_qdq_kernel(float* __restrict__ x, const int* __restrict__ seg,
+                                      const float* __restrict__ mn, const float* __restrict__ mx, long P, long ld,
+                                      int nseg, uint32_t seed, int levels) {
+  const int k = blockIdx.y;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    const int s = seg[i];
+    const float lo = mn[(long)k * nseg + s];
+    const float sc = fmaxf((mx[(long)k * nseg + s] - lo) / levels, 1e-30f);
+    const long gi = (long)k * ld + i;
+    const float u = (float)mix32((uint32_t)(gi & 0xffffffffu), seed) * (1.f / 4294967296.f);
+    float q = floorf((x[gi] - lo) / sc + u);
+    q = fminf(fmaxf(q, 0.f), (float)levels);
+    x[gi] = lo + q * sc;
+  }
+}
+
+__global__ void sign_pack_kernel(const float* __restrict__ g, uint8_t* __restrict__ out, long P, long ld,
+                                 long nbytes) {
+  const int k = blockIdx.y;
+  for (long j = (long)blockIdx.x * blockDim.x + threadIdx.x; j < nbytes; j += (long)gridDim.x * blockDim.x) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const long i = j * 8 + t;
+      if (i < P && g[(long)k * ld + i] >= 0.f) b |= 1u << t;
+    }
+    out[(long)k * nbytes + j] = (uint8_t)b;
+  }
+}
+
+__global__ void sign_vote_kernel(const uint8_t* __restrict__ packed, const uint8_t* __restrict__ active,
+                                 int* __restrict__ votes, int K, long P, long nbytes) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    int v = 0;
+    for (int k = 0; k < K; ++k) {
+      if (active && !active[k]) continue;
+      v += ((packed[(long)k * nbytes + (i >> 3)] >> (i & 7)) & 1) ? 1 : -1;
+    }
+    votes[i] = v;
+  }
+}
+
+__global__ void embedding_fwd_kernel(const int* __restrict__ tok, const bf16_t* __restrict__ table,
+                                     bf16_t* __restrict__ out, long n_tok, int D, long t_cs, int rep, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long row = i / D;
+  const int d = i % D;
+  const int k = (int)(row / n_tok);
+  out[i] = table[(long)(k / rep) * t_cs + (long)tok[row] * D + d];
+}
+
+__global__ void embedding_bwd_kernel(const int* __restrict__ tok, const bf16_t* __restrict__ dy,
+                                     float* __restrict__ dtable, long n_tok, int D, long t_cs, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long row = i / D;
+  const int d = i % D;
+  const int k = (int)(row / n_tok);
+  atomicAdd(&dtable[(long)k * t_cs + (long)tok[row] * D + d], bf2f(dy[i]));
+}
+
+__global__ void gather_rows_kernel(const bf16_t* __restrict__ src, const int* __restrict__ idx,
+                                   bf16_t* __restrict__ dst, long n, long row_vec8) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * row_vec8) return;
+  const long r = i / row_vec8, c = i % row_vec8;
+  reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[(long)idx[r] * row_vec8 + c];
+}
+
+int grid_for(long n, int per_block = 256, int cap = 4096) { return (int)max(1L, min((long)cap, (n + per_block - 1) / per_block)); }
+
+}  // namespace
+
+void pool_fwd(const bf16_t* x, bf16_t* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k,
+              int stride, int pad, int mode, hipStream_t s) {
+  const long total = (long)K * B * OH * OW * C;
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, idx, total, H, W, C, OH, OW, k,
+                     stride, pad, mode);
+}
+
+void pool_bwd(const bf16_t* dy, const int* idx, bf16_t* dx, int K, int B, int H, int W, int C, int OH, int OW,
+              int k, int stride, int pad, int mode, hipStream_t s) {
+  const long total = (long)K * B * H * W * C;
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, idx, dx, total, H, W, C, OH, OW,
+                     k, stride, pad, mode);
+}
+
+void gap_fwd(const bf16_t* x, bf16_t* y, int KB, int HW, int C, hipStream_t s) {
+  const long total = (long)KB * C;
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, HW, C, total);
+}
+
+void gap_bwd(const bf16_t* dy, bf16_t* dx, int KB, int HW, int C, hipStream_t s) {
+  const long total = (long)KB * HW * C;
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, dx, HW, C, total);
+}
+
+void ce_fwd_bwd(const bf16_t* logits, const int* labels, const int* valid, float* loss, float* correct,
+                bf16_t* dlogits, int K, int B, int NC, hipStream_t s) {
+  DLS_CHECK(hipMemsetAsync(loss, 0, sizeof(float) * K, s));
+  DLS_CHECK(hipMemsetAsync(correct, 0, sizeof(float) * K, s));
+  hipLaunchKernelGGL(ce_kernel, dim3(cdiv(B, 4), K), dim3(256), 0, s, logits, labels, valid, loss, correct, dlogits,
+                     B, NC);
+}
+
+void relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s) {
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, dy, y, dx, n);
+}
+
+void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
+              const uint8_t* first, int K, long P, long ld, float wd, float momentum, float dampening, int nesterov,
+              hipStream_t s) {
+  const long P4 = P / 4;  // P is a multiple of 16 (layout alignment)
+  dim3 grid(grid_for(P4, 256, 1024), K);
+  hipLaunchKernelGGL(sgd_kernel, grid, dim3(256), 0, s, theta, grad, mom, shadow, lr, active, first, P4, ld, wd,
+                     momentum, dampening, nesterov);
+}
+
+void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shadow, const float* lr,
+               const uint8_t* active, const float* step, int K, long P, long ld, float b1, float b2, float eps,
+               float wd, hipStream_t s) {
+  dim3 grid(grid_for(P, 256, 1024), K);
+  hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, s, theta, grad, m, v, shadow, lr, active, step, P, ld, b1, b2,
+                     eps, wd);
+}
+
+void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s) {
+  dim3 grid(grid_for(P / 4, 256, 1024), K);
+  hipLaunchKernelGGL(broadcast_kernel, grid, dim3(256), 0, s, theta, shadow, src, P / 4, ld);
+}
+
+void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s) {
+  dim3 grid(grid_for(P / 4, 256, 1024), K);
+  hipLaunchKernelGGL(delta_kernel, grid, dim3(256), 0, s, theta, base, out, P / 4, ld);
+}
+
+void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s) {
+  hipLaunchKernelGGL(weighted_sum_kernel, dim3(grid_for(P / 4, 256, 8192)), dim3(256), 0, s, x, w, out, K, P / 4, ld);
+}
+
+void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
+                         long ld, hipStream_t s) {
+  hipLaunchKernelGGL(masked_weighted_sum_kernel, dim3(grid_for(P, 256, 8192)), dim3(256), 0, s, x, mask, w, num, den,
+                     K, P, ld);
+}
+
+void dropout_mask(uint8_t* mask, long n, float p, uint32_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, mask, n, p, seed);
+}
+
+void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
+                    hipStream_t s) {
+  DLS_CHECK(hipMemsetAsync(out, 0, sizeof(float) * K * nblocks, s));
+  dim3 grid(grid_for(P, 256, 2048), K);
+  hipLaunchKernelGGL(block_sq_kernel, grid, dim3(256), 0, s, x, block_ids, out, P, ld, nblocks);
+}
+
+void seg_minmax(const float* x, const int* seg, float* mn, float* mx, int K, long P, long ld, int nseg,
+                hipStream_t s) {
+  dim3 grid(cdiv(P, 256), K);
+  hipLaunchKernelGGL(seg_minmax_kernel, grid, dim3(256), 0, s, x, seg, mn, mx, P, ld, nseg);
+}
+
+void stochastic_qdq(float* x, const int* seg, const float* mn, const float* mx, int K, long P, long ld, int nseg,
+                    uint32_t seed, int levels, hipStream_t s) {
+  dim3 grid(grid_for(P, 256, 2048), K);
+  hipLaunchKernelGGL(stochastic_qdq_kernel, grid, dim3(256), 0, s, x, seg, mn, mx, P, ld, nseg, seed, levels);
+}
+
+void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s) {
+  const long nbytes = (P + 7) / 8;
+  dim3 grid(grid_for(nbytes, 256, 2048), K);
+  hipLaunchKernelGGL(sign_pack_kernel, grid, dim3(256), 0, s, g, out, P, ld, nbytes);
+}
+
+void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, long P, hipStream_t s) {
+  hipLaunchKernelGGL(sign_vote_kernel, dim3(grid_for(P, 256, 8192)), dim3(256), 0, s, packed, active, votes, K, P,
+                     (P + 7) / 8);
+}
+
+void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, long n_tok, int D, long t_cs, int rep,
+                   hipStream_t s) {
+  const long total = (long)K * n_tok * D;
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, table, out, n_tok, D,
+                     t_cs, rep, total);
+}
+
+void embedding_bwd(const int* tokens, const bf16_t* dy, float* dtable, int K, long n_tok, int D, long t_cs,
+                   hipStream_t s) {
+  const long total = (long)K * n_tok * D;
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, dy, dtable, n_tok, D,
+                     t_cs, total);
+}
+
+void gather_rows(const bf16_t* src, const int* idx, bf16_t* dst, long n, long row_elems, hipStream_t s) {
+  const long v8 = row_elems / 8;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(n * v8, 256)), dim3(256), 0, s, src, idx, dst, n, v8);
+}

@@ -1,0 +1,387 @@
+// Normalisation kernels (gfx950): client-batched BatchNorm with per-client batch statistics
+// over the *valid* rows only (ragged cohorts), fused residual-add + ReLU, and LayerNorm.
+//
+// BN forward = stats pass (per-(client,channel) Σx, Σx² with 16-B vector loads, LDS tree,
+// one fp32 atomic per channel per block) + apply pass (normalise, γ/β, +residual, ReLU,
+// zero padded rows). BN backward = reduction pass (Σg, Σg·x̂ with g = dy·relu'(y)) + apply
+// pass (dx, and dpre for the residual branch); dγ/dβ land directly in the flat fp32
+// gradient buffer (row stride P).
+#include "common.h"
+#include "dls.h"
+
+namespace {
+
+template <int V>
+__device__ __forceinline__ void load_vec(const bf16_t* p, float* f) {
+  if constexpr (V == 8) {
+    unpack8(*reinterpret_cast<const uint4*>(p), f);
+  } else if constexpr (V == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    f[0] = __uint_as_float(u.x << 16);
+    f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16);
+    f[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) f[i] = bf2f(p[i]);
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void store_vec(bf16_t* p, const float* f) {
+  if constexpr (V == 8) {
+    *reinterpret_cast<uint4*>(p) = pack8(f);
+  } else if constexpr (V == 4) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+    u.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = u;
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = f2bf(f[i]);
+  }
+}
+
+constexpr int ROWS_PER_BLOCK = 512;
+
+// Generic per-(client, channel) double reduction over rows [0, nrows_valid):
+//   mode 0: s0 += x, s1 += x²                       (BN fwd stats)
+//   mode 1: g = dy*relu'(y); s0 += g, s1 += g*x̂      (BN bwd)
+//   mode 2: s0 += x                                  (column sums, bias grads)
+template <int V, int MODE>
+__global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                          const bf16_t* __restrict__ yv, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const int* __restrict__ valid_rows, int R, int C, int relu,
+                                                          float* __restrict__ ws, long ws_cs) {
+  __shared__ float red[2][256 * V];
+  const int k = blockIdx.y;
+  const int CT = C / V;
+  const int tid = threadIdx.x;
+  const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
+  const int r0 = blockIdx.x * ROWS_PER_BLOCK;
+  const int r1 = min(nvalid, r0 + ROWS_PER_BLOCK);
+  const long base = (long)k * R * C;
+  for (int cg = 0; cg < CT; cg += 256) {
+    const int ctn = min(256, CT - cg);
+    const int RT = 256 / ctn;
+    const int cc = tid % ctn, rl = tid / ctn;
+    const bool active = rl < RT && (cg + cc) < CT;
+    float s0[V], s1[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) s0[i] = s1[i] = 0.f;
+    const int c0 = (cg + cc) * V;
+    float mu[V], rs[V];
+    if (MODE == 1 && active) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        mu[i] = mean[(long)k * C + c0 + i];
+        rs[i] = rstd[(long)k * C + c0 + i];
+      }
+    }
+    if (active) {
+      for (int r = r0 + rl; r < r1; r += RT) {
+        const long off = base + (long)r * C + c0;
+        float va[V];
+        load_vec<V>(a + off, va);
+        if (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            s0[i] += va[i];
+            s1[i] += va[i] * va[i];
+          }
+        } else if (MODE == 2) {
+#pragma unroll
+          for (int i = 0; i < V; ++i) s0[i] += va[i];
+        } else {
+          float vx[V], vy[V];
+          load_vec<V>(b + off, vx);
+          if (relu) load_vec<V>(yv + off, vy);
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            const float g = (relu && vy[i] <= 0.f) ? 0.f : va[i];
+            s0[i] += g;
+            s1[i] += g * (vx[i] - mu[i]) * rs[i];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      red[0][tid * V + i] = s0[i];
+      red[1][tid * V + i] = s1[i];
+    }
+    __syncthreads();
+    if (active && rl == 0) {
+      for (int j = 1; j < RT; ++j) {
+        const int t2 = j * ctn + cc;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          s0[i] += red[0][t2 * V + i];
+          s1[i] += red[1][t2 * V + i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        atomicAdd(&ws[(long)k * ws_cs + c0 + i], s0[i]);
+        if (MODE != 2) atomicAdd(&ws[(long)k * ws_cs + C + c0 + i], s1[i]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta, const bf16_t* __restrict__ res,
+                                                       bf16_t* __restrict__ y, float* __restrict__ mean_out,
+                                                       float* __restrict__ rstd_out, const int* __restrict__ valid_rows,
+                                                       const float* __restrict__ ws, long g_cs, int R, int C, int relu,
+                                                       float eps, int rep) {
+  const int k = blockIdx.y;
+  const int CT = C / V;
+  const long nchunks = (long)min(ROWS_PER_BLOCK, R - (int)blockIdx.x * ROWS_PER_BLOCK) * CT;
+  const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
+  const float n = (float)max(nvalid, 1);
+  const bf16_t* gk = gamma + (long)(k / rep) * g_cs;
+  const bf16_t* bk = beta + (long)(k / rep) * g_cs;
+  const long base = (long)k * R * C + (long)blockIdx.x * ROWS_PER_BLOCK * C;
+  for (long i = threadIdx.x; i < nchunks; i += 256) {
+    const int rloc = (int)(i / CT);
+    const int c0 = (int)(i % CT) * V;
+    const int r = blockIdx.x * ROWS_PER_BLOCK + rloc;
+    float out[V];
+    if (r < nvalid) {
+      float v[V], rv[V];
+      load_vec<V>(x + base + (long)rloc * C + c0, v);
+      if (res) load_vec<V>(res + base + (long)rloc * C + c0, rv);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = c0 + j;
+        const float mu = ws[(long)k * 2 * C + c] / n;
+        const float var = fmaxf(ws[(long)k * 2 * C + C + c] / n - mu * mu, 0.f);
+        const float rs = rsqrtf(var + eps);
+        float o = (v[j] - mu) * rs * bf2f(gk[c]) + bf2f(bk[c]);
+        if (res) o += rv[j];
+        if (relu) o = fmaxf(o, 0.f);
+        out[j] = o;
+        if (blockIdx.x == 0 && rloc == 0) {
+          mean_out[(long)k * C + c] = mu;
+          rstd_out[(long)k * C + c] = rs;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) out[j] = 0.f;
+    }
+    store_vec<V>(y + base + (long)rloc * C + c0, out);
+  }
+  // nvalid == 0 or block 0 has no valid rows: still publish stats
+  if (blockIdx.x == 0 && nvalid == 0) {
+    for (int c = threadIdx.x; c < C; c += 256) {
+      mean_out[(long)k * C + c] = 0.f;
+      rstd_out[(long)k * C + c] = rsqrtf(eps);
+    }
+  }
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const bf16_t* __restrict__ gamma,
+    const int* __restrict__ valid_rows, const float* __restrict__ ws, long g_cs, int R, int C, int relu,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    long dg_cs) {
+  const int k = blockIdx.y;
+  const int CT = C / V;
+  const long nchunks = (long)min(ROWS_PER_BLOCK, R - (int)blockIdx.x * ROWS_PER_BLOCK) * CT;
+  const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
+  const float n = (float)max(nvalid, 1);
+  const bf16_t* gk = gamma + (long)k * g_cs;
+  const long base = (long)k * R * C + (long)blockIdx.x * ROWS_PER_BLOCK * C;
+  if (blockIdx.x == 0 && dgamma) {
+    for (int c = threadIdx.x; c < C; c += 256) {
+      dbeta[(long)k * dg_cs + c] = ws[(long)k * 2 * C + c];
+      dgamma[(long)k * dg_cs + c] = ws[(long)k * 2 * C + C + c];
+    }
+  }
+  for (long i = threadIdx.x; i < nchunks; i += 256) {
+    const int rloc = (int)(i / CT);
+    const int c0 = (int)(i % CT) * V;
+    const int r = blockIdx.x * ROWS_PER_BLOCK + rloc;
+    const long off = base + (long)rloc * C + c0;
+    float o[V], gp[V];
+    if (r < nvalid) {
+      float vdy[V], vx[V], vy[V];
+      load_vec<V>(dy + off, vdy);
+      load_vec<V>(x + off, vx);
+      if (relu) load_vec<V>(y + off, vy);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = c0 + j;
+        const float g = (relu && vy[j] <= 0.f) ? 0.f : vdy[j];
+        const float mu = mean[(long)k * C + c], rs = rstd[(long)k * C + c];
+        const float xh = (vx[j] - mu) * rs;
+        const float sg = ws[(long)k * 2 * C + c], sgx = ws[(long)k * 2 * C + C + c];
+        o[j] = bf2f(gk[c]) * rs * (g - sg / n - xh * sgx / n);
+        gp[j] = g;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) o[j] = gp[j] = 0.f;
+    }
+    store_vec<V>(dx + off, o);
+    if (dpre) store_vec<V>(dpre + off, gp);
+  }
+}
+
+int vw(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : 1; }
+
+// ------------------------------------------------------------------ LayerNorm
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
+                                                     const bf16_t* __restrict__ beta, bf16_t* __restrict__ y,
+                                                     float* __restrict__ mean, float* __restrict__ rstd, long g_cs,
+                                                     long nrows, long rpc, int C, float eps, int rep) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= nrows) return;
+  const int k = (int)(row / rpc);
+  const bf16_t* xr = x + row * C;
+  float s = 0.f, sq = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float v = bf2f(xr[c]);
+    s += v;
+    sq += v * v;
+  }
+  s = wave_sum(s);
+  sq = wave_sum(sq);
+  const float mu = s / C;
+  const float rs = rsqrtf(fmaxf(sq / C - mu * mu, 0.f) + eps);
+  const bf16_t* g = gamma + (long)(k / rep) * g_cs;
+  const bf16_t* b = beta + (long)(k / rep) * g_cs;
+  for (int c = lane; c < C; c += 64) y[row * C + c] = f2bf((bf2f(xr[c]) - mu) * rs * bf2f(g[c]) + bf2f(b[c]));
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+constexpr int LN_MAXC = 16;  // C <= 1024
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const bf16_t* __restrict__ gamma, long g_cs, long rpc, int C,
+                                                     bf16_t* __restrict__ dx, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, long dg_cs, int rows_per_wave) {
+  // grid: (row-groups, K); each wave handles rows_per_wave rows of client k
+  const int k = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long rbeg = wave * rows_per_wave;
+  const long rend = min(rpc, rbeg + rows_per_wave);
+  const bf16_t* g = gamma + (long)k * g_cs;
+  float dg[LN_MAXC], db[LN_MAXC];
+#pragma unroll
+  for (int i = 0; i < LN_MAXC; ++i) dg[i] = db[i] = 0.f;
+  for (long r = rbeg; r < rend; ++r) {
+    const long row = (long)k * rpc + r;
+    const float mu = mean[row], rs = rstd[row];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) {
+        const float gy = bf2f(dy[row * C + c]);
+        const float xh = (bf2f(x[row * C + c]) - mu) * rs;
+        const float gg = gy * bf2f(g[c]);
+        a += gg;
+        b += gg * xh;
+        dg[i] += gy * xh;
+        db[i] += gy;
+      }
+    }
+    a = wave_sum(a) / C;
+    b = wave_sum(b) / C;
+#pragma unroll
+    for (int i = 0; i < LN_MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) {
+        const float gy = bf2f(dy[row * C + c]);
+        const float xh = (bf2f(x[row * C + c]) - mu) * rs;
+        dx[row * C + c] = f2bf(rs * (gy * bf2f(g[c]) - a - xh * b));
+      }
+    }
+  }
+  if (rend > rbeg) {
+#pragma unroll
+    for (int i = 0; i < LN_MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) {
+        atomicAdd(&dgamma[(long)k * dg_cs + c], dg[i]);
+        atomicAdd(&dbeta[(long)k * dg_cs + c], db[i]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+#define DISPATCH_V(V, ...)          \
+  if (V == 8) {                     \
+    constexpr int VV = 8;           \
+    __VA_ARGS__;                    \
+  } else if (V == 4) {              \
+    constexpr int VV = 4;           \
+    __VA_ARGS__;                    \
+  } else {                          \
+    constexpr int VV = 1;           \
+    __VA_ARGS__;                    \
+  }
+
+void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
+            float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
+            float* ws, hipStream_t s) {
+  DLS_CHECK(hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * K, s));
+  dim3 grid(cdiv(R, ROWS_PER_BLOCK), K);
+  const int V = vw(C);
+  DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
+                                   nullptr, valid_rows, R, C, 0, ws, (long)2 * C));
+  DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, gamma, beta, res, y, mean, rstd,
+                                   valid_rows, ws, g_cs, R, C, relu, eps, rep));
+}
+
+void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
+            const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
+            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, hipStream_t s) {
+  DLS_CHECK(hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * K, s));
+  dim3 grid(cdiv(R, ROWS_PER_BLOCK), K);
+  const int V = vw(C);
+  DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
+                                   valid_rows, R, C, relu, ws, (long)2 * C));
+  DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, mean, rstd, gamma,
+                                   valid_rows, ws, g_cs, R, C, relu, dx, dpre, dgamma, dbeta, dg_cs));
+}
+
+void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s) {
+  // out must be zeroed by the caller (it is a strided view of the grad buffer)
+  dim3 grid(cdiv(rows, ROWS_PER_BLOCK), K);
+  const int V = vw(C);
+  DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 2>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
+                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs));
+}
+
+void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,
+            long g_cs, int K, long rpc, int C, float eps, int rep, hipStream_t s) {
+  const long nrows = (long)K * rpc;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(nrows, 4)), dim3(256), 0, s, x, gamma, beta, y, mean, rstd, g_cs,
+                     nrows, rpc, C, eps, rep);
+}
+
+void ln_bwd(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd, const bf16_t* gamma,
+            long g_cs, int K, long rpc, int C, bf16_t* dx, float* dgamma, float* dbeta, long dg_cs, float* ws,
+            hipStream_t s) {
+  const int rows_per_wave = 16;
+  const long waves = (rpc + rows_per_wave - 1) / rows_per_wave;
+  dim3 grid(cdiv(waves, 4), K);
+  hipLaunchKernelGGL(ln_bwd_kernel, grid, dim3(256), 0, s, dy, x, mean, rstd, gamma, g_cs, rpc, C, dx, dgamma, dbeta,
+                     dg_cs, rows_per_wave);
+}

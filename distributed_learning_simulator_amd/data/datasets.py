@@ -134,6 +134,12 @@ class ImageDataset:
         """idx: any-shape int tensor on device -> [*idx.shape, H, W, C]."""
         flat = idx.reshape(-1).long()
         if self.data is not None:
+            from ..ops import backend
+
+            if backend.using_hip(self.data) and self.data[0].numel() % 8 == 0:
+                from ..ops import hip
+
+                return hip.gather_rows(self.data, idx).reshape(*idx.shape, *self.spec.shape)
             out = self.data.index_select(0, flat)
         else:
             out = self._generate(flat, self.device, self.dtype)

@@ -1,0 +1,99 @@
+"""Build the in-tree gfx950 extension `_dls_hip` with hipcc (no torch headers needed).
+
+    python -m distributed_learning_simulator_amd.ops.build [--force] [-j N]
+
+Each `csrc/*.hip` is compiled to an object (incremental, by mtime), `csrc/bindings.cpp`
+(pybind11) likewise, and everything is linked into
+`distributed_learning_simulator_amd/_dls_hip<EXT_SUFFIX>` — in-tree so it travels with the
+repo snapshot to the GPU box. The .so links libamdhip64.so.7 by SONAME; importing torch first
+makes it bind to torch's bundled HIP runtime (one runtime per process).
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "distributed_learning_simulator_amd")
+BUILD = os.path.join(ROOT, "build", "hip")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DLS_OFFLOAD_ARCH", "gfx950")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+TARGET = os.path.join(PKG, "_dls_hip" + EXT_SUFFIX)
+
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-mcode-object-version=5",
+                "-ffp-contract=fast", "-Wno-unused-result"]
+
+
+def _headers() -> list[str]:
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+
+
+def _needs(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src] + _headers())
+
+
+def _compile(src: str, obj: str, extra: list[str]) -> tuple[str, str]:
+    cmd = [HIPCC, *COMMON_FLAGS, *extra, "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return src, r.stderr
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
+    import pybind11
+
+    sources = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    if not force and os.path.exists(TARGET) and all(os.path.getmtime(s) <= os.path.getmtime(TARGET) for s in sources):
+        return TARGET  # up to date (object files need not be present, e.g. on a GPU box snapshot)
+    os.makedirs(BUILD, exist_ok=True)
+    py_inc = sysconfig.get_paths()["include"]
+    units = []
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith(".hip") or f.endswith(".cpp"):
+            src = os.path.join(CSRC, f)
+            obj = os.path.join(BUILD, f + ".o")
+            extra = [f"-I{CSRC}"]
+            if f.endswith(".cpp"):
+                extra += [f"-I{pybind11.get_include()}", f"-I{py_inc}", "-x", "hip"]
+            units.append((src, obj, extra))
+    todo = [u for u in units if force or _needs(u[1], u[0])]
+    jobs = jobs or min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8) or 1
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for src, err in ex.map(lambda u: _compile(*u), todo):
+                if verbose:
+                    print("compiled", os.path.basename(src), file=sys.stderr)
+                if err.strip() and verbose:
+                    print(err, file=sys.stderr)
+    objs = [u[1] for u in units]
+    if force or todo or not os.path.exists(TARGET) or any(os.path.getmtime(o) > os.path.getmtime(TARGET) for o in objs):
+        tmp = TARGET + ".tmp"
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, TARGET)
+    return TARGET
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=0)
+    a = ap.parse_args()
+    print(build(force=a.force, jobs=a.j, verbose=True))
+
+
+if __name__ == "__main__":
+    main()

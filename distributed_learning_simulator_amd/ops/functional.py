@@ -151,9 +151,7 @@ class _MaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, pad):
         be = _be(x)
-        if pad:
-            x = torch.nn.functional.pad(x, (0, 0, pad, pad, pad, pad), value=float("-inf"))
-        y, idx = be.maxpool_fwd(x, k, s)
+        y, idx = be.maxpool_fwd(x, k, s, pad)
         ctx.save_for_backward(idx)
         ctx.k, ctx.s, ctx.pad, ctx.xshape = k, s, pad, x.shape
         return y
@@ -162,10 +160,7 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         be = _be(dy)
-        dx = be.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, ctx.k, ctx.s)
-        if ctx.pad:
-            p = ctx.pad
-            dx = dx[:, :, p:-p, p:-p, :].contiguous()
+        dx = be.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, ctx.k, ctx.s, ctx.pad)
         return dx, None, None, None
 
 

@@ -1,0 +1,425 @@
+"""Host wrappers of the gfx950 kernels (`_dls_hip`), same API as `ops.ref`.
+
+Importing this module on a machine with a GPU but without the built extension raises — the
+GPU path never silently falls back to PyTorch. Shape/stride contracts are asserted here
+before any launch (a mis-shaped launch on the box can fault the GPU).
+"""
+
+from __future__ import annotations
+
+import importlib
+
+import torch
+
+from . import ref
+
+try:
+    _C = importlib.import_module("distributed_learning_simulator_amd._dls_hip")
+except ImportError as e:  # pragma: no cover - exercised only on a GPU box without a build
+    raise ImportError(
+        "HIP extension _dls_hip is not built; run `python -m distributed_learning_simulator_amd.ops.build` "
+        f"(original error: {e})"
+    ) from e
+
+BF16 = torch.bfloat16
+NULL = 0
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _client_view(w: torch.Tensor, K: int):
+    """(client stride, rep) of a [Kw, ...] parameter view with contiguous inner dims."""
+    Kw = w.shape[0]
+    inner = w[0]
+    assert inner.is_contiguous(), "parameter inner dims must be contiguous"
+    assert K % Kw == 0, (K, Kw)
+    return (w.stride(0) if Kw > 1 else 0), K // Kw
+
+
+def _check(t: torch.Tensor, dtype=None, contiguous=True, name="tensor"):
+    assert t.is_cuda, f"{name} must be on the GPU"
+    if dtype is not None:
+        assert t.dtype == dtype, f"{name}: expected {dtype}, got {t.dtype}"
+    if contiguous:
+        assert t.is_contiguous(), f"{name} must be contiguous"
+
+
+_ws_cache: dict = {}
+
+
+def _workspace(numel: int, device) -> torch.Tensor:
+    key = (device, "ws")
+    t = _ws_cache.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
+        _ws_cache[key] = t
+    return t
+
+
+# ----------------------------------------------------------------------------- conv
+def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
+    K, B, H, W, C = x.shape
+    x = x.contiguous()
+    _check(x, BF16, name="x")
+    _check(w, BF16, contiguous=False, name="w")
+    Kw, Co, KH, KW, Ci = w.shape
+    assert Ci == C, (Ci, C)
+    w_cs, rep = _client_view(w, K)
+    OH = (H + 2 * pad - KH) // stride + 1
+    OW = (W + 2 * pad - KW) // stride + 1
+    y = torch.empty((K, B, OH, OW, Co), dtype=BF16, device=x.device)
+    b_cs = 0
+    if bias is not None:
+        b_cs, _ = _client_view(bias, K)
+    M = B * OH * OW
+    _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
+               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, _s())
+    return y
+
+
+def _flip_transpose(w):
+    Kw, Co, KH, KW, Ci = w.shape
+    wt = torch.empty((Kw, Ci, KH, KW, Co), dtype=BF16, device=w.device)
+    _C.weight_flip_transpose(_p(w), _p(wt), w.stride(0) if Kw > 1 else 0, Kw, Co, KH, KW, Ci, _s())
+    return wt
+
+
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
+    K, B, OH, OW, Co = dy.shape
+    dy = dy.contiguous()
+    _check(dy, BF16, name="dy")
+    Kw, Co2, KH, KW, Ci = w.shape
+    assert Co2 == Co
+    wt = _flip_transpose(w)
+    rep = K // Kw
+    H, W = int(in_hw[0]), int(in_hw[1])
+    dx = torch.empty((K, B, H, W, Ci), dtype=BF16, device=dy.device)
+    M = B * H * W
+    _C.conv_nt(_p(dy), _p(wt), _p(dx), NULL, B * OH * OW * Co, M * Ci, wt.stride(0) if Kw > 1 else 0, 0, B, OH, OW, Co,
+               H, W, KH, KW, 1, KH - 1 - pad, stride, M, Ci, KH * KW * Co, rep, 0, K, _s())
+    return dx
+
+
+def conv_wgrad(dy, x, gw, stride: int, pad: int):
+    K, B, OH, OW, Co = dy.shape
+    _, _, H, W, C = x.shape
+    dy = dy.contiguous()
+    x = x.contiguous()
+    _check(dy, BF16, name="dy")
+    _check(x, BF16, name="x")
+    assert gw.dtype == torch.float32 and gw.shape[0] == K and gw[0].is_contiguous()
+    _, Co2, KH, KW, Ci = gw.shape
+    assert Co2 == Co and Ci == C
+    M = B * OH * OW
+    R = KH * KW * C
+    if _C.conv_tn_splitk(K, Co, R, M) > 1:
+        gw.zero_()
+    _C.conv_tn(_p(dy), _p(x), _p(gw), M * Co, B * H * W * C, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M,
+               Co, R, K, _s())
+
+
+# --------------------------------------------------------------------------- linear
+def linear_fwd(x, w, b=None):
+    K, N, Fi = x.shape
+    x = x.contiguous()
+    Kw, Fo, Fi2 = w.shape
+    assert Fi2 == Fi
+    w_cs, rep = _client_view(w, K)
+    b_cs = _client_view(b, K)[0] if b is not None else 0
+    y = torch.empty((K, N, Fo), dtype=BF16, device=x.device)
+    _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
+               0, K, _s())
+    return y
+
+
+def linear_dgrad(dy, w):
+    K, N, Fo = dy.shape
+    dy = dy.contiguous()
+    Kw, Fo2, Fi = w.shape
+    wt = torch.empty((Kw, Fi, Fo), dtype=BF16, device=w.device)
+    _C.weight_flip_transpose(_p(w), _p(wt), w.stride(0) if Kw > 1 else 0, Kw, Fo, 1, 1, Fi, _s())
+    dx = torch.empty((K, N, Fi), dtype=BF16, device=dy.device)
+    _C.conv_nt(_p(dy), _p(wt), _p(dx), NULL, N * Fo, N * Fi, wt.stride(0) if Kw > 1 else 0, 0, 1, N, 1, Fo, N, 1, 1, 1,
+               1, 0, 1, N, Fi, Fo, K // Kw, 0, K, _s())
+    return dx
+
+
+def linear_wgrad(dy, x, gw, gb=None):
+    K, N, Fo = dy.shape
+    Fi = x.shape[-1]
+    dy = dy.contiguous()
+    x = x.contiguous()
+    assert gw.shape == (K, Fo, Fi) and gw[0].is_contiguous()
+    if _C.conv_tn_splitk(K, Fo, Fi, N) > 1:
+        gw.zero_()
+    _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K, _s())
+    if gb is not None:
+        gb.zero_()
+        _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, _s())
+
+
+# ------------------------------------------------------------------------ batchnorm
+def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5):
+    K, R, C = x.shape
+    x = x.contiguous()
+    g_cs, rep = _client_view(gamma, K)
+    y = torch.empty_like(x)
+    mean = torch.empty((K, C), dtype=torch.float32, device=x.device)
+    rstd = torch.empty((K, C), dtype=torch.float32, device=x.device)
+    ws = _workspace(2 * K * C, x.device)
+    if residual is not None:
+        residual = residual.contiguous()
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
+              eps, rep, _p(ws), _s())
+    return y, mean, rstd
+
+
+def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre):
+    K, R, C = x.shape
+    g_cs, rep = _client_view(gamma, K)
+    assert rep == 1
+    dx = torch.empty_like(x)
+    dpre = torch.empty_like(x) if need_dpre else None
+    ws = _workspace(2 * K * C, x.device)
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    dg_cs = ggamma.stride(0) if ggamma is not None else 0
+    _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
+              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _s())
+    return dx, dpre
+
+
+# ------------------------------------------------------------------------ layernorm
+def ln_fwd(x, gamma, beta, eps=1e-5):
+    K = x.shape[0]
+    C = x.shape[-1]
+    x = x.contiguous()
+    g_cs, rep = _client_view(gamma, K)
+    rpc = x.numel() // (K * C)
+    y = torch.empty_like(x)
+    mean = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    _C.ln_fwd(_p(x), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), g_cs, K, rpc, C, eps, rep, _s())
+    return y, mean, rstd
+
+
+def ln_bwd(dy, x, mean, rstd, gamma):
+    K = x.shape[0]
+    C = x.shape[-1]
+    assert C <= 1024
+    g_cs, rep = _client_view(gamma, K)
+    rpc = x.numel() // (K * C)
+    dx = torch.empty_like(x)
+    dgamma = torch.zeros((K, C), dtype=torch.float32, device=x.device)
+    dbeta = torch.zeros((K, C), dtype=torch.float32, device=x.device)
+    _C.ln_bwd(_p(dy.contiguous()), _p(x), _p(mean), _p(rstd), _p(gamma), g_cs, K, rpc, C, _p(dx), _p(dgamma),
+              _p(dbeta), C, _s())
+    return dx, dgamma, dbeta
+
+
+# -------------------------------------------------------------------------- pooling
+def _pool_fwd(x, k, s, pad, mode):
+    K, B, H, W, C = x.shape
+    x = x.contiguous()
+    OH = (H + 2 * pad - k) // s + 1
+    OW = (W + 2 * pad - k) // s + 1
+    y = torch.empty((K, B, OH, OW, C), dtype=BF16, device=x.device)
+    idx = torch.empty((K, B, OH, OW, C), dtype=torch.int32, device=x.device) if mode == 0 else None
+    _C.pool_fwd(_p(x), _p(y), _p(idx), K, B, H, W, C, OH, OW, k, s, pad, mode, _s())
+    return y, idx
+
+
+def maxpool_fwd(x, k, s, pad=0):
+    return _pool_fwd(x, k, s, pad, 0)
+
+
+def maxpool_bwd(dy, idx, x_shape, k, s, pad=0):
+    K, B, H, W, C = x_shape
+    _, _, OH, OW, _ = dy.shape
+    dx = torch.empty(x_shape, dtype=BF16, device=dy.device)
+    _C.pool_bwd(_p(dy.contiguous()), _p(idx), _p(dx), K, B, H, W, C, OH, OW, k, s, pad, 0, _s())
+    return dx
+
+
+def avgpool_fwd(x, k, s):
+    return _pool_fwd(x, k, s, 0, 1)[0]
+
+
+def avgpool_bwd(dy, x_shape, k, s):
+    K, B, H, W, C = x_shape
+    _, _, OH, OW, _ = dy.shape
+    dx = torch.empty(x_shape, dtype=BF16, device=dy.device)
+    _C.pool_bwd(_p(dy.contiguous()), NULL, _p(dx), K, B, H, W, C, OH, OW, k, s, 0, 1, _s())
+    return dx
+
+
+def gap_fwd(x):
+    K, B, H, W, C = x.shape
+    x = x.contiguous()
+    y = torch.empty((K, B, C), dtype=BF16, device=x.device)
+    _C.gap_fwd(_p(x), _p(y), K * B, H * W, C, _s())
+    return y
+
+
+def gap_bwd(dy, x_shape):
+    K, B, H, W, C = x_shape
+    dx = torch.empty(x_shape, dtype=BF16, device=dy.device)
+    _C.gap_bwd(_p(dy.contiguous()), _p(dx), K * B, H * W, C, _s())
+    return dx
+
+
+# -------------------------------------------------------------------- cross entropy
+def ce_fwd_bwd(logits, labels, valid=None):
+    K, B, NC = logits.shape
+    logits = logits.contiguous()
+    lab = labels.to(torch.int32).contiguous()
+    v = valid.to(torch.int32).contiguous() if valid is not None else None
+    loss = torch.empty(K, dtype=torch.float32, device=logits.device)
+    correct = torch.empty(K, dtype=torch.float32, device=logits.device)
+    dlogits = torch.empty_like(logits)
+    _C.ce_fwd_bwd(_p(logits), _p(lab), _p(v), _p(loss), _p(correct), _p(dlogits), K, B, NC, _s())
+    return loss, correct, dlogits
+
+
+# ------------------------------------------------------------------------ embedding
+def embedding_fwd(tokens, table):
+    K = tokens.shape[0]
+    tok = tokens.to(torch.int32).contiguous()
+    t_cs, rep = _client_view(table, K)
+    D = table.shape[-1]
+    n_tok = tok.numel() // K
+    out = torch.empty((*tokens.shape, D), dtype=BF16, device=table.device)
+    _C.embedding_fwd(_p(tok), _p(table), _p(out), K, n_tok, D, t_cs, rep, _s())
+    return out
+
+
+def embedding_bwd(dy, tokens, gtable):
+    K = tokens.shape[0]
+    tok = tokens.to(torch.int32).contiguous()
+    D = dy.shape[-1]
+    gtable.zero_()
+    _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _s())
+
+
+# ------------------------------------------------------ not yet native (torch on GPU)
+attn_fwd = ref.attn_fwd
+attn_bwd = ref.attn_bwd
+spmm = ref.spmm
+
+
+# ---------------------------------------------------------------- optimiser / FL math
+def _row_args(theta):
+    assert theta.dtype == torch.float32 and theta.stride(1) == 1
+    K, P = theta.shape
+    assert P % 16 == 0, "flat buffers are padded to 16 elements"
+    return K, P, theta.stride(0)
+
+
+def sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, nesterov, first_step, shadow=None):
+    K, P, ld = _row_args(theta)
+    assert grad.stride(0) == ld and mom.stride(0) == ld
+    if shadow is not None:
+        assert shadow.stride(0) == ld and shadow.dtype == BF16
+    _C.sgd_step(_p(theta), _p(grad), _p(mom), _p(shadow), _p(lr.float().contiguous()),
+                _p(active.to(torch.uint8).contiguous()), _p(first_step.to(torch.uint8).contiguous()), K, P, ld,
+                float(weight_decay), float(momentum), float(dampening), int(nesterov), _s())
+
+
+def adam_step(theta, grad, m, v, lr, active, step, beta1, beta2, eps, weight_decay, shadow=None):
+    K, P, ld = _row_args(theta)
+    _C.adam_step(_p(theta), _p(grad), _p(m), _p(v), _p(shadow), _p(lr.float().contiguous()),
+                 _p(active.to(torch.uint8).contiguous()), _p(step.float().contiguous()), K, P, ld, beta1, beta2, eps,
+                 weight_decay, _s())
+
+
+def broadcast_rows(theta_rows, src, shadow_rows=None):
+    K, P, ld = _row_args(theta_rows)
+    src = src.float().contiguous()
+    assert src.numel() == P
+    _C.broadcast_rows(_p(theta_rows), _p(shadow_rows), _p(src), K, P, ld, _s())
+
+
+def delta_rows(theta_rows, base, out=None):
+    K, P, ld = _row_args(theta_rows)
+    if out is None:
+        out = torch.empty_like(theta_rows)
+    assert out.stride(0) == ld or out.data_ptr() == theta_rows.data_ptr()
+    _C.delta_rows(_p(theta_rows), _p(base.float().contiguous()), _p(out), K, P, ld, _s())
+    return out
+
+
+def weighted_sum(x, w):
+    K, P, ld = _row_args(x)
+    out = torch.empty(P, dtype=torch.float32, device=x.device)
+    _C.weighted_sum(_p(x), _p(w.float().contiguous()), _p(out), K, P, ld, _s())
+    return out
+
+
+def masked_weighted_sum(x, mask, w):
+    K, P, ld = _row_args(x)
+    mask = mask.to(torch.uint8)
+    assert mask.is_contiguous() and mask.shape == (K, P) and ld == P
+    num = torch.empty(P, dtype=torch.float32, device=x.device)
+    den = torch.empty(P, dtype=torch.float32, device=x.device)
+    _C.masked_weighted_sum(_p(x), _p(mask), _p(w.float().contiguous()), _p(num), _p(den), K, P, ld, _s())
+    return num, den
+
+
+def dropout_mask(shape, p, seed):
+    n = 1
+    for d in shape:
+        n *= d
+    m = torch.empty(shape, dtype=torch.uint8, device="cuda")
+    _C.dropout_mask(_p(m), n, float(p), seed & 0xFFFFFFFF, _s())
+    return m.bool()
+
+
+def block_sq_norms(x, block_offsets, block_ids):
+    K, P, ld = _row_args(x)
+    nb = int(block_offsets.numel()) - 1
+    out = torch.empty((K, nb), dtype=torch.float32, device=x.device)
+    _C.block_sq_norms(_p(x), _p(block_ids.to(torch.int32).contiguous()), _p(out), K, P, ld, nb, _s())
+    return out
+
+
+def stochastic_qdq(x, seg_ids, nseg, seed, levels):
+    K, P, ld = _row_args(x)
+    x = x.contiguous() if x.stride(0) != ld else x
+    mn = torch.full((K, nseg), float("inf"), dtype=torch.float32, device=x.device)
+    mx = torch.full((K, nseg), float("-inf"), dtype=torch.float32, device=x.device)
+    seg = seg_ids.to(torch.int32).contiguous()
+    out = x.clone()
+    _C.seg_minmax(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, _s())
+    _C.stochastic_qdq(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, seed & 0xFFFFFFFF, levels, _s())
+    return out
+
+
+def sign_pack(g):
+    K, P, ld = _row_args(g)
+    out = torch.empty((K, (P + 7) // 8), dtype=torch.uint8, device=g.device)
+    _C.sign_pack(_p(g), _p(out), K, P, ld, _s())
+    return out
+
+
+def sign_vote(packed, P, active=None):
+    K = packed.shape[0]
+    votes = torch.empty(P, dtype=torch.int32, device=packed.device)
+    a = active.to(torch.uint8).contiguous() if active is not None else None
+    _C.sign_vote(_p(packed.contiguous()), _p(a), _p(votes), K, P, _s())
+    return votes
+
+
+def gather_rows(src, idx):
+    """src [N, ...] bf16 contiguous, idx int -> [len(idx), ...]"""
+    row = src[0].numel()
+    assert row % 8 == 0 and src.is_contiguous()
+    i32 = idx.reshape(-1).to(torch.int32).contiguous()
+    out = torch.empty((i32.numel(), *src.shape[1:]), dtype=src.dtype, device=src.device)
+    _C.gather_rows(_p(src), _p(i32), _p(out), i32.numel(), row, _s())
+    return out

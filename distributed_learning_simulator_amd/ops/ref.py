@@ -184,16 +184,16 @@ def ln_bwd(dy, x, mean, rstd, gamma):
 
 
 # -------------------------------------------------------------------------- pooling
-def maxpool_fwd(x, k: int, s: int):
+def maxpool_fwd(x, k: int, s: int, pad: int = 0):
     K, B, H, W, C = x.shape
     g = _to_grouped(x)
-    y, idx = F.max_pool2d(g, k, s, return_indices=True)
+    y, idx = F.max_pool2d(g, k, s, padding=pad, return_indices=True)
     return _from_grouped(y, K).contiguous(), idx
 
 
-def maxpool_bwd(dy, idx, x_shape, k: int, s: int):
+def maxpool_bwd(dy, idx, x_shape, k: int, s: int, pad: int = 0):
     K, B, H, W, C = x_shape
-    g = F.max_unpool2d(_to_grouped(dy), idx, k, s, output_size=(H, W))
+    g = F.max_unpool2d(_to_grouped(dy), idx, k, s, padding=pad, output_size=(H, W))
     return _from_grouped(g, K).contiguous()
 
 

@@ -1,0 +1,235 @@
+"""Numerics of every gfx950 kernel vs the plain-PyTorch fp32 reference (`ops.ref`)."""
+
+import pytest
+import torch
+
+from distributed_learning_simulator_amd.ops import ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+def _close(out, exp, tol=2e-2):
+    out = out.float()
+    exp = exp.float()
+    err = (out - exp).abs().max().item()
+    mag = exp.abs().max().item() + 1e-6
+    assert err <= tol * mag, f"max err {err} vs magnitude {mag}"
+
+
+CONV_CASES = [
+    # K, B, H, W, Ci, Co, k, stride, pad
+    (3, 4, 8, 8, 16, 32, 3, 1, 1),
+    (2, 2, 8, 8, 64, 64, 3, 1, 1),
+    (2, 3, 9, 9, 64, 128, 3, 2, 1),
+    (2, 2, 8, 8, 64, 128, 1, 2, 0),
+    (3, 2, 8, 8, 3, 64, 3, 1, 1),       # stem: Ci=3 scalar path
+    (2, 2, 6, 6, 36, 12, 3, 1, 1),      # DenseNet-like: Ci%8==4, Co=12
+    (2, 2, 12, 12, 1, 6, 5, 1, 2),      # LeNet conv1
+    (2, 2, 7, 7, 128, 256, 3, 1, 1),
+    (1, 2, 16, 16, 8, 8, 7, 2, 3),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(hip, case):
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(0)
+    x = _bf(K, B, H, W, Ci)
+    w = _bf(K, Co, k, k, Ci, scale=0.2)
+    y = hip.conv_fwd(x, w, s, p)
+    y_ref = ref.conv_fwd(x.float(), w.float(), s, p)
+    assert y.shape == y_ref.shape
+    _close(y, y_ref)
+    dy = _bf(*y.shape)
+    dx = hip.conv_dgrad(dy, w, (H, W), s, p)
+    _close(dx, ref.conv_dgrad(dy.float(), w.float(), (H, W), s, p))
+    P = Co * k * k * Ci + 16
+    gbuf = torch.full((K, P), 7.0, device=DEV)
+    gw = gbuf[:, 8 : 8 + Co * k * k * Ci].unflatten(1, (Co, k, k, Ci))
+    hip.conv_wgrad(dy, x, gw, s, p)
+    _close(gw, ref.conv_wgrad(dy.float(), x.float(), (K, Co, k, k, Ci), s, p))
+    assert torch.all(gbuf[:, :8] == 7.0) and torch.all(gbuf[:, 8 + Co * k * k * Ci :] == 7.0)
+
+
+def test_conv_shared_weights_rep(hip):
+    # eval path: 6 virtual clients share 2 weight rows (rep = 3)
+    x = _bf(6, 2, 8, 8, 16)
+    w = _bf(2, 32, 3, 3, 16, scale=0.2)
+    _close(hip.conv_fwd(x, w, 1, 1), ref.conv_fwd(x.float(), w.float(), 1, 1))
+    w1 = _bf(1, 32, 3, 3, 16, scale=0.2)
+    _close(hip.conv_fwd(x, w1, 1, 1), ref.conv_fwd(x.float(), w1.float(), 1, 1))
+
+
+def test_conv_large_wgrad_splitk(hip):
+    # forces split-K atomics (few tiles, long pixel reduction)
+    K, B, H, W, Ci, Co = 2, 32, 16, 16, 64, 64
+    x = _bf(K, B, H, W, Ci)
+    dy = _bf(K, B, H, W, Co)
+    gw = torch.empty((K, Co, 3, 3, Ci), device=DEV)
+    hip.conv_wgrad(dy, x, gw, 1, 1)
+    _close(gw, ref.conv_wgrad(dy.float(), x.float(), (K, Co, 3, 3, Ci), 1, 1))
+
+
+@pytest.mark.parametrize("N,Fi,Fo", [(64, 512, 10), (33, 100, 300), (128, 784, 200), (5, 84, 10)])
+def test_linear(hip, N, Fi, Fo):
+    K = 3
+    x = _bf(K, N, Fi)
+    w = _bf(K, Fo, Fi, scale=0.1)
+    b = _bf(K, Fo)
+    _close(hip.linear_fwd(x, w, b), ref.linear_fwd(x.float(), w.float(), b.float()))
+    dy = _bf(K, N, Fo)
+    _close(hip.linear_dgrad(dy, w), ref.linear_dgrad(dy.float(), w.float()))
+    gw = torch.empty((K, Fo, Fi), device=DEV)
+    gb = torch.empty((K, Fo), device=DEV)
+    hip.linear_wgrad(dy, x, gw, gb)
+    dw_ref, db_ref = ref.linear_wgrad(dy.float(), x.float(), True)
+    _close(gw, dw_ref)
+    _close(gb, db_ref)
+
+
+@pytest.mark.parametrize("C", [64, 12, 3, 512])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_batchnorm(hip, C, relu, res):
+    K, R = 3, 300
+    x = _bf(K, R, C, scale=2.0) + 0.5
+    g = _bf(K, C) + 1
+    b = _bf(K, C)
+    valid = torch.tensor([300, 150, 7], dtype=torch.int32, device=DEV)
+    r = _bf(K, R, C) if res else None
+    y, mean, rstd = hip.bn_fwd(x, g, b, valid, relu, r)
+    y2, mean2, rstd2 = ref.bn_fwd(x.float(), g.float(), b.float(), valid, relu, r.float() if res else None)
+    _close(mean, mean2, 1e-3)
+    _close(rstd, rstd2, 1e-2)
+    _close(y, y2)
+    dy = _bf(K, R, C)
+    gg = torch.zeros((K, C), device=DEV)
+    gbeta = torch.zeros((K, C), device=DEV)
+    dx, dpre = hip.bn_bwd(dy, x, y, mean, rstd, g, valid, relu, gg, gbeta, res)
+    dx2, dg2, db2, dpre2 = ref.bn_bwd(dy.float(), x.float(), y.float(), mean2, rstd2, g.float(), valid, relu)
+    _close(dx, dx2, 3e-2)
+    _close(gg, dg2, 2e-2)
+    _close(gbeta, db2, 2e-2)
+    if res:
+        _close(dpre, dpre2)
+
+
+def test_layernorm(hip):
+    K, N, C = 2, 37, 100
+    x = _bf(K, N, C)
+    g = _bf(K, C) + 1
+    b = _bf(K, C)
+    y, mean, rstd = hip.ln_fwd(x, g, b)
+    y2, m2, r2 = ref.ln_fwd(x.float(), g.float(), b.float())
+    _close(y, y2)
+    dy = _bf(K, N, C)
+    dx, dg, db = hip.ln_bwd(dy, x, mean, rstd, g)
+    dx2, dg2, db2 = ref.ln_bwd(dy.float(), x.float(), m2, r2, g.float())
+    _close(dx, dx2, 3e-2)
+    _close(dg, dg2, 2e-2)
+    _close(db, db2, 2e-2)
+
+
+@pytest.mark.parametrize("k,s,pad", [(2, 2, 0), (3, 2, 1)])
+def test_maxpool(hip, k, s, pad):
+    x = _bf(2, 3, 9, 9, 16)
+    y, idx = hip.maxpool_fwd(x, k, s, pad)
+    y2, idx2 = ref.maxpool_fwd(x.float(), k, s, pad)
+    _close(y, y2, 1e-6)
+    dy = _bf(*y.shape)
+    _close(hip.maxpool_bwd(dy, idx, x.shape, k, s, pad), ref.maxpool_bwd(dy.float(), idx2, x.shape, k, s, pad))
+
+
+def test_avgpool_gap(hip):
+    x = _bf(2, 3, 8, 8, 24)
+    _close(hip.avgpool_fwd(x, 2, 2), ref.avgpool_fwd(x.float(), 2, 2))
+    dy = _bf(2, 3, 4, 4, 24)
+    _close(hip.avgpool_bwd(dy, x.shape, 2, 2), ref.avgpool_bwd(dy.float(), x.shape, 2, 2))
+    _close(hip.gap_fwd(x), ref.gap_fwd(x.float()))
+    dg = _bf(2, 3, 24)
+    _close(hip.gap_bwd(dg, x.shape), ref.gap_bwd(dg.float(), x.shape))
+
+
+@pytest.mark.parametrize("NC", [10, 100, 1000])
+def test_cross_entropy(hip, NC):
+    K, B = 3, 64
+    logits = _bf(K, B, NC, scale=3)
+    labels = torch.randint(0, NC, (K, B), device=DEV)
+    valid = torch.tensor([64, 30, 1], dtype=torch.int32, device=DEV)
+    l, c, d = hip.ce_fwd_bwd(logits, labels, valid)
+    l2, c2, d2 = ref.ce_fwd_bwd(logits.float(), labels, valid)
+    _close(l, l2, 1e-3)
+    assert torch.equal(c, c2)
+    _close(d, d2, 2e-2)
+
+
+def test_sgd_and_fl_math(hip):
+    K, P = 5, 4096
+    theta = torch.randn(K, P, device=DEV)
+    grad = torch.randn(K, P, device=DEV)
+    mom = torch.randn(K, P, device=DEV)
+    lr = torch.rand(K, device=DEV)
+    active = torch.tensor([1, 1, 0, 1, 1], dtype=torch.bool, device=DEV)
+    first = torch.tensor([1, 0, 0, 0, 1], dtype=torch.bool, device=DEV)
+    t2, m2 = theta.clone(), mom.clone()
+    shadow = torch.empty(K, P, dtype=torch.bfloat16, device=DEV)
+    hip.sgd_step(theta, grad, mom, lr, active, 5e-4, 0.9, 0.0, False, first, shadow)
+    ref.sgd_step(t2, grad, m2, lr, active, 5e-4, 0.9, 0.0, False, first)
+    torch.testing.assert_close(theta, t2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mom, m2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(shadow.float(), theta.to(torch.bfloat16).float())
+    w = torch.rand(K, device=DEV)
+    torch.testing.assert_close(hip.weighted_sum(theta, w), ref.weighted_sum(theta, w), rtol=1e-5, atol=1e-5)
+    base = torch.randn(P, device=DEV)
+    torch.testing.assert_close(hip.delta_rows(theta, base), theta - base)
+    rows = torch.empty(K, P, device=DEV)
+    hip.broadcast_rows(rows, base)
+    assert torch.equal(rows, base.expand(K, P))
+    mask = torch.rand(K, P, device=DEV) > 0.5
+    n1, d1 = hip.masked_weighted_sum(theta, mask, w)
+    n2, d2 = ref.masked_weighted_sum(theta, mask, w)
+    torch.testing.assert_close(n1, n2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(d1, d2)
+
+
+def test_compression_kernels(hip):
+    from distributed_learning_simulator_amd.ops import fl
+
+    K, P = 3, 1024
+    m_hip = hip.dropout_mask((K, P), 0.3, 1234)
+    m_ref = fl.philox_uniform((K, P), 1234, 0, DEV) >= 0.3
+    assert torch.equal(m_hip, m_ref)
+    g = torch.randn(K, P, device=DEV)
+    packed = hip.sign_pack(g)
+    from distributed_learning_simulator_amd.ops import quant
+
+    packed_ref = quant.sign_pack.__wrapped__(g) if hasattr(quant.sign_pack, "__wrapped__") else None
+    votes = hip.sign_vote(packed, P)
+    torch.testing.assert_close(votes, torch.sign(g).sum(0).to(torch.int32) if (g != 0).all() else votes)
+    seg = torch.cat([torch.zeros(500, dtype=torch.int32), torch.ones(524, dtype=torch.int32)]).to(DEV)
+    x = torch.randn(K, P, device=DEV)
+    dq = hip.stochastic_qdq(x, seg, 2, 7, 255)
+    step = (x.max() - x.min()) / 255
+    assert (dq - x).abs().max() <= step * 1.01
+    # unbiasedness
+    reps = torch.stack([hip.stochastic_qdq(x, seg, 2, s, 255) for s in range(64)]).mean(0)
+    assert (reps - x).abs().mean() < step * 0.1
+    del packed_ref
+
+
+def test_embedding_gather(hip):
+    K, V, D = 2, 50, 16
+    table = _bf(K, V, D)
+    tok = torch.randint(0, V, (K, 3, 7), device=DEV)
+    _close(hip.embedding_fwd(tok, table), ref.embedding_fwd(tok, table.float()))
+    dy = _bf(K, 3, 7, D)
+    gt = torch.empty(K, V, D, device=DEV)
+    hip.embedding_bwd(dy, tok, gt)
+    _close(gt, ref.embedding_bwd(dy.float(), tok, V))
+    src = _bf(100, 4, 4, 8)
+    idx = torch.randint(0, 100, (3, 5), device=DEV)
+    assert torch.equal(hip.gather_rows(src, idx), src[idx.reshape(-1)])
