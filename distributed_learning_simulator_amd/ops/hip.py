@@ -7,6 +7,7 @@ before any launch (a mis-shaped launch on the box can fault the GPU).
 
 from __future__ import annotations
 
+import collections
 import importlib
 
 import torch
@@ -29,8 +30,19 @@ def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+_keepalive: collections.deque = collections.deque(maxlen=48)  # > pointer args of any one launch
+
+
 def _p(t) -> int:
-    return 0 if t is None else t.data_ptr()
+    """Device pointer of t. The tensor is kept referenced until well after the launch that
+    consumes the pointer: an inline temporary (`_p(x.to(...))`) would otherwise be freed
+    while the argument list is still being built and a second temporary in the same call
+    could be allocated at the same address. After the launch, the caching allocator's
+    stream ordering makes reuse safe."""
+    if t is None:
+        return 0
+    _keepalive.append(t)
+    return t.data_ptr()
 
 
 def _client_view(w: torch.Tensor, K: int):

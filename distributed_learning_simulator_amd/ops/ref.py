@@ -192,9 +192,13 @@ def maxpool_fwd(x, k: int, s: int, pad: int = 0):
 
 
 def maxpool_bwd(dy, idx, x_shape, k: int, s: int, pad: int = 0):
+    # scatter-ADD (overlapping windows, e.g. 3x3/s2, route several grads to one input;
+    # max_unpool2d would overwrite instead of accumulate)
     K, B, H, W, C = x_shape
-    g = F.max_unpool2d(_to_grouped(dy), idx, k, s, padding=pad, output_size=(H, W))
-    return _from_grouped(g, K).contiguous()
+    g = _to_grouped(dy).float()
+    out = torch.zeros((B, K * C, H * W), dtype=torch.float32, device=dy.device)
+    out.scatter_add_(2, idx.flatten(2), g.flatten(2))
+    return _from_grouped(out.view(B, K * C, H, W), K).to(dy.dtype).contiguous()
 
 
 def avgpool_fwd(x, k: int, s: int):

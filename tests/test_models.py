@@ -1,0 +1,91 @@
+"""Model zoo: parameter counts pinned to the architectures the reference configs name, and
+cohort forward/backward on the CPU oracle path (gradients written into the flat buffer must
+match plain-PyTorch autograd of an equivalent per-client computation)."""
+
+import pytest
+import torch
+
+from distributed_learning_simulator_amd.data.datasets import get_spec
+from distributed_learning_simulator_amd.engine.params import BoundParams
+from distributed_learning_simulator_amd.models.layers import RunCtx
+from distributed_learning_simulator_amd.models.zoo import build_model
+from distributed_learning_simulator_amd.ops import functional as Fn
+
+
+@pytest.mark.parametrize("model,dataset,count", [
+    ("LeNet5", "MNIST", 61706),
+    ("ResNet18", "CIFAR10", 11173962),
+    ("Resnet50", "ImageNet", 25557032),
+    ("densenet40", "CIFAR10", 1059298),
+    ("densenet40", "CIFAR100", 1100428),
+])
+def test_param_counts(model, dataset, count):
+    assert build_model(model, get_spec(dataset)).num_params == count
+
+
+def test_transformer_layer_count():
+    m = build_model("TransformerClassificationModel", get_spec("imdb"),
+                    {"d_model": 100, "nhead": 5, "num_encoder_layer": 2})
+    # embedding 20000x100 + 2 x 452,548 (d=100, ff=2048) + classifier 202
+    assert m.num_params == 20000 * 100 + 2 * 452548 + 202
+
+
+def _run(model, x, labels, K, theta):
+    layout = model.layout
+    grad = torch.zeros_like(theta)
+    params = BoundParams(layout, theta, grad)
+    ctx = RunCtx(params, torch.full((K,), labels.shape[1], dtype=torch.int32))
+    logits = model.forward(x, ctx)
+    loss, correct = Fn.cross_entropy(logits, labels, ctx.valid)
+    loss.sum().backward()
+    return loss.detach(), grad
+
+
+@pytest.mark.parametrize("name,ds", [("LeNet5", "MNIST"), ("ResNet18", "CIFAR10"), ("densenet40", "CIFAR10")])
+def test_cohort_clients_are_independent(name, ds):
+    """Client k's loss/grad in a cohort of 2 equals running it alone (no cross-talk)."""
+    torch.manual_seed(0)
+    spec = get_spec(ds)
+    model = build_model(name, spec)
+    P = model.layout.padded_size
+    g = torch.Generator().manual_seed(1)
+    theta = torch.stack([model.layout.init_flat(g), model.layout.init_flat(g)])
+    H, W, C = spec.shape
+    x = torch.randn(2, 4, H, W, C)
+    y = torch.randint(0, spec.num_classes, (2, 4))
+    loss2, grad2 = _run(model, x, y, 2, theta.clone())
+    loss1, grad1 = _run(model, x[1:], y[1:], 1, theta[1:].clone())
+    torch.testing.assert_close(loss2[1:], loss1, rtol=1e-4, atol=1e-5)
+    # grouped conv with K=2 vs K=1 runs different CPU conv algorithms: fp32 reassociation
+    scale = grad1.abs().max().item()
+    # (BN over 4-image batches amplifies it); cross-talk would be O(1)
+    assert (grad2[1:] - grad1).abs().max().item() <= 1e-2 * scale
+    assert grad2.abs().sum() > 0
+
+
+def test_grad_matches_torch_autograd_lenet():
+    """Flat-buffer gradients == torch.autograd of the same math on leaf tensors."""
+    spec = get_spec("MNIST")
+    model = build_model("LeNet5", spec)
+    layout = model.layout
+    theta = layout.init_flat(torch.Generator().manual_seed(3)).unsqueeze(0)
+    x = torch.randn(1, 6, 28, 28, 1)
+    y = torch.randint(0, 10, (1, 6))
+    _, grad = _run(model, x, y, 1, theta.clone())
+    t = {k: v.clone().requires_grad_() for k, v in layout.unflatten(theta[0]).items()}
+    import torch.nn.functional as F
+
+    def conv(inp, w, b, pad):
+        return F.conv2d(inp, w.permute(0, 3, 1, 2), b, padding=pad)
+
+    h = x[0].permute(0, 3, 1, 2)
+    h = F.max_pool2d(F.relu(conv(h, t["conv1.weight"], t["conv1.bias"], 2)), 2)
+    h = F.max_pool2d(F.relu(conv(h, t["conv2.weight"], t["conv2.bias"], 0)), 2)
+    h = h.permute(0, 2, 3, 1).reshape(6, -1)
+    h = F.relu(F.linear(h, t["fc1.weight"], t["fc1.bias"]))
+    h = F.relu(F.linear(h, t["fc2.weight"], t["fc2.bias"]))
+    out = F.linear(h, t["fc3.weight"], t["fc3.bias"])
+    F.cross_entropy(out, y[0]).backward()
+    got = layout.unflatten(grad[0])
+    for k, v in t.items():
+        torch.testing.assert_close(got[k], v.grad, rtol=1e-4, atol=1e-6)
