@@ -302,16 +302,35 @@ __global__ void dropout_mask_kernel(uint8_t* __restrict__ mask, long n, float p,
   mask[i] = ((float)h * (1.f / 4294967296.f)) >= p;
 }
 
-// Σ x² per (client, block); one block-stride loop, LDS-free wave reduction + atomics
-__global__ void block_sq_kernel(const float* __restrict__ x, const int* __restrict__ ids, float* __restrict__ out,
-                                long P, long ld, int nb) {
+// Σ x² per (client, block). Every tensor starts 16-element aligned in the flat layout and
+// inter-tensor padding is zero, so a lane's 16-element chunk belongs to the block of its first
+// element. Lanes hold consecutive chunks → segmented wave reduction → one atomic per run.
+__global__ void __launch_bounds__(256) block_sq_kernel(const float* __restrict__ x, const int* __restrict__ ids,
+                                                       float* __restrict__ out, long P, long ld, int nb) {
   const int k = blockIdx.y;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
-    const int b = ids[i];
-    if (b >= 0) {
-      const float v = x[(long)k * ld + i];
-      atomicAdd(&out[(long)k * nb + b], v * v);
+  const int lane = threadIdx.x & 63;
+  const long nchunk = P / 16;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long c0 = (long)blockIdx.x * blockDim.x; c0 < nchunk; c0 += stride) {
+    const long c = c0 + threadIdx.x;
+    int b = -1;
+    float s = 0.f;
+    if (c < nchunk) {
+      b = ids[c * 16];
+      const float4* p = reinterpret_cast<const float4*>(x + (long)k * ld + c * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 v = p[j];
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
     }
+    for (int o = 1; o < 64; o <<= 1) {
+      const int bo = __shfl_down(b, o, 64);
+      const float so = __shfl_down(s, o, 64);
+      if (lane + o < 64 && bo == b) s += so;
+    }
+    const int bprev = __shfl_up(b, 1, 64);
+    if (b >= 0 && (lane == 0 || bprev != b)) atomicAdd(&out[(long)k * nb + b], s);
   }
 }
 
@@ -505,7 +524,7 @@ void dropout_mask(uint8_t* mask, long n, float p, uint32_t seed, hipStream_t s) 
 void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
                     hipStream_t s) {
   DLS_CHECK(hipMemsetAsync(out, 0, sizeof(float) * K * nblocks, s));
-  dim3 grid(grid_for(P, 256, 2048), K);
+  dim3 grid(grid_for(P / 16, 256, 1024), K);
   hipLaunchKernelGGL(block_sq_kernel, grid, dim3(256), 0, s, x, block_ids, out, P, ld, nblocks);
 }
 

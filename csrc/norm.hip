@@ -131,107 +131,147 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
   }
 }
 
-template <int V>
-__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
-                                                       const bf16_t* __restrict__ beta, const bf16_t* __restrict__ res,
-                                                       bf16_t* __restrict__ y, float* __restrict__ mean_out,
-                                                       float* __restrict__ rstd_out, const int* __restrict__ valid_rows,
-                                                       const float* __restrict__ ws, long g_cs, int R, int C, int relu,
-                                                       float eps, int rep) {
-  const int k = blockIdx.y;
-  const int CT = C / V;
-  const long nchunks = (long)min(ROWS_PER_BLOCK, R - (int)blockIdx.x * ROWS_PER_BLOCK) * CT;
+// Per-(client, channel) coefficients from the reduced sums (one tiny launch), so the apply
+// passes are a pure fused multiply-add stream with no per-element division or rsqrt.
+//  fwd:  coef = {scale = γ·rstd, shift = β − mean·scale};  also publishes mean / rstd
+//  bwd:  dx = a·g + d + e·x  with a = γ·rstd, e = −a·rstd·Σgx̂/n, d = −a·Σg/n − e·mean;
+//        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
+__global__ void bn_coef_kernel(const float* __restrict__ ws, const bf16_t* __restrict__ gamma,
+                               const bf16_t* __restrict__ beta, const int* __restrict__ valid_rows,
+                               const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                               float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef,
+                               float* __restrict__ dgamma, float* __restrict__ dbeta, long dg_cs, long g_cs, int K,
+                               int R, int C, float eps, int rep, int bwd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= K * C) return;
+  const int k = i / C, c = i % C;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const float n = (float)max(nvalid, 1);
-  const bf16_t* gk = gamma + (long)(k / rep) * g_cs;
-  const bf16_t* bk = beta + (long)(k / rep) * g_cs;
-  const long base = (long)k * R * C + (long)blockIdx.x * ROWS_PER_BLOCK * C;
-  for (long i = threadIdx.x; i < nchunks; i += 256) {
-    const int rloc = (int)(i / CT);
-    const int c0 = (int)(i % CT) * V;
-    const int r = blockIdx.x * ROWS_PER_BLOCK + rloc;
-    float out[V];
-    if (r < nvalid) {
-      float v[V], rv[V];
-      load_vec<V>(x + base + (long)rloc * C + c0, v);
-      if (res) load_vec<V>(res + base + (long)rloc * C + c0, rv);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int c = c0 + j;
-        const float mu = ws[(long)k * 2 * C + c] / n;
-        const float var = fmaxf(ws[(long)k * 2 * C + C + c] / n - mu * mu, 0.f);
-        const float rs = rsqrtf(var + eps);
-        float o = (v[j] - mu) * rs * bf2f(gk[c]) + bf2f(bk[c]);
-        if (res) o += rv[j];
-        if (relu) o = fmaxf(o, 0.f);
-        out[j] = o;
-        if (blockIdx.x == 0 && rloc == 0) {
-          mean_out[(long)k * C + c] = mu;
-          rstd_out[(long)k * C + c] = rs;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; ++j) out[j] = 0.f;
+  const float s0 = ws[(long)k * 2 * C + c], s1 = ws[(long)k * 2 * C + C + c];
+  const float g = bf2f(gamma[(long)(k / rep) * g_cs + c]);
+  if (!bwd) {
+    const float mu = s0 / n;
+    const float var = fmaxf(s1 / n - mu * mu, 0.f);
+    const float rs = rsqrtf(var + eps);
+    const float sc = g * rs;
+    mean_out[i] = mu;
+    rstd_out[i] = rs;
+    coef[2 * i] = sc;
+    coef[2 * i + 1] = bf2f(beta[(long)(k / rep) * g_cs + c]) - mu * sc;
+  } else {
+    const float mu = mean_in[i], rs = rstd_in[i];
+    const float a = g * rs;
+    const float e = -a * rs * s1 / n;
+    const float d = -a * s0 / n - e * mu;
+    coef[3 * i] = a;
+    coef[3 * i + 1] = d;
+    coef[3 * i + 2] = e;
+    if (dgamma) {
+      dbeta[(long)k * dg_cs + c] = s0;
+      dgamma[(long)k * dg_cs + c] = s1;
     }
-    store_vec<V>(y + base + (long)rloc * C + c0, out);
   }
-  // nvalid == 0 or block 0 has no valid rows: still publish stats
-  if (blockIdx.x == 0 && nvalid == 0) {
-    for (int c = threadIdx.x; c < C; c += 256) {
-      mean_out[(long)k * C + c] = 0.f;
-      rstd_out[(long)k * C + c] = rsqrtf(eps);
+}
+
+// thread owns one V-channel chunk and strides over rows; grid (row-blocks, K)
+template <int V>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                       bf16_t* __restrict__ y, const int* __restrict__ valid_rows,
+                                                       const float* __restrict__ coef, int R, int C, int relu) {
+  const int k = blockIdx.y;
+  const int CT = C / V;
+  const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
+  const int r0 = blockIdx.x * ROWS_PER_BLOCK, r1 = min(R, r0 + ROWS_PER_BLOCK);
+  const long base = (long)k * R * C;
+  for (int cg = 0; cg < CT; cg += 256) {
+    const int ctn = min(256, CT - cg);
+    const int RT = 256 / ctn;
+    const int cc = threadIdx.x % ctn, rl = threadIdx.x / ctn;
+    if (rl >= RT) continue;
+    const int c0 = (cg + cc) * V;
+    float sc[V], sh[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      sc[j] = coef[2 * ((long)k * C + c0 + j)];
+      sh[j] = coef[2 * ((long)k * C + c0 + j) + 1];
+    }
+    for (int r = r0 + rl; r < r1; r += RT) {
+      const long off = base + (long)r * C + c0;
+      float out[V];
+      if (r < nvalid) {
+        float v[V];
+        load_vec<V>(x + off, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) out[j] = fmaf(v[j], sc[j], sh[j]);
+        if (res) {
+          float rv[V];
+          load_vec<V>(res + off, rv);
+#pragma unroll
+          for (int j = 0; j < V; ++j) out[j] += rv[j];
+        }
+        if (relu) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) out[j] = fmaxf(out[j], 0.f);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) out[j] = 0.f;
+      }
+      store_vec<V>(y + off, out);
     }
   }
 }
 
 template <int V>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ rstd, const bf16_t* __restrict__ gamma,
-    const int* __restrict__ valid_rows, const float* __restrict__ ws, long g_cs, int R, int C, int relu,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    long dg_cs) {
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                           const bf16_t* __restrict__ y,
+                                                           const int* __restrict__ valid_rows,
+                                                           const float* __restrict__ coef, int R, int C, int relu,
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre) {
   const int k = blockIdx.y;
   const int CT = C / V;
-  const long nchunks = (long)min(ROWS_PER_BLOCK, R - (int)blockIdx.x * ROWS_PER_BLOCK) * CT;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
-  const float n = (float)max(nvalid, 1);
-  const bf16_t* gk = gamma + (long)k * g_cs;
-  const long base = (long)k * R * C + (long)blockIdx.x * ROWS_PER_BLOCK * C;
-  if (blockIdx.x == 0 && dgamma) {
-    for (int c = threadIdx.x; c < C; c += 256) {
-      dbeta[(long)k * dg_cs + c] = ws[(long)k * 2 * C + c];
-      dgamma[(long)k * dg_cs + c] = ws[(long)k * 2 * C + C + c];
-    }
-  }
-  for (long i = threadIdx.x; i < nchunks; i += 256) {
-    const int rloc = (int)(i / CT);
-    const int c0 = (int)(i % CT) * V;
-    const int r = blockIdx.x * ROWS_PER_BLOCK + rloc;
-    const long off = base + (long)rloc * C + c0;
-    float o[V], gp[V];
-    if (r < nvalid) {
-      float vdy[V], vx[V], vy[V];
-      load_vec<V>(dy + off, vdy);
-      load_vec<V>(x + off, vx);
-      if (relu) load_vec<V>(y + off, vy);
+  const int r0 = blockIdx.x * ROWS_PER_BLOCK, r1 = min(R, r0 + ROWS_PER_BLOCK);
+  const long base = (long)k * R * C;
+  for (int cg = 0; cg < CT; cg += 256) {
+    const int ctn = min(256, CT - cg);
+    const int RT = 256 / ctn;
+    const int cc = threadIdx.x % ctn, rl = threadIdx.x / ctn;
+    if (rl >= RT) continue;
+    const int c0 = (cg + cc) * V;
+    float ca[V], cd[V], ce[V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        const int c = c0 + j;
-        const float g = (relu && vy[j] <= 0.f) ? 0.f : vdy[j];
-        const float mu = mean[(long)k * C + c], rs = rstd[(long)k * C + c];
-        const float xh = (vx[j] - mu) * rs;
-        const float sg = ws[(long)k * 2 * C + c], sgx = ws[(long)k * 2 * C + C + c];
-        o[j] = bf2f(gk[c]) * rs * (g - sg / n - xh * sgx / n);
-        gp[j] = g;
+    for (int j = 0; j < V; ++j) {
+      const long q = 3 * ((long)k * C + c0 + j);
+      ca[j] = coef[q];
+      cd[j] = coef[q + 1];
+      ce[j] = coef[q + 2];
+    }
+    for (int r = r0 + rl; r < r1; r += RT) {
+      const long off = base + (long)r * C + c0;
+      float o[V], gp[V];
+      if (r < nvalid) {
+        float vdy[V], vx[V];
+        load_vec<V>(dy + off, vdy);
+        load_vec<V>(x + off, vx);
+        if (relu) {
+          float vy[V];
+          load_vec<V>(y + off, vy);
+#pragma unroll
+          for (int j = 0; j < V; ++j) vdy[j] = vy[j] > 0.f ? vdy[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          gp[j] = vdy[j];
+          o[j] = fmaf(ca[j], vdy[j], fmaf(ce[j], vx[j], cd[j]));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = gp[j] = 0.f;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; ++j) o[j] = gp[j] = 0.f;
+      store_vec<V>(dx + off, o);
+      if (dpre) store_vec<V>(dpre + off, gp);
     }
-    store_vec<V>(dx + off, o);
-    if (dpre) store_vec<V>(dpre + off, gp);
   }
 }
 
@@ -340,25 +380,32 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
             float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
             float* ws, hipStream_t s) {
+  // ws layout: [K][2C] sums, then [K][2C] coefficients
+  float* coef = ws + (long)2 * C * K;
   DLS_CHECK(hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * K, s));
   dim3 grid(cdiv(R, ROWS_PER_BLOCK), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
                                    nullptr, valid_rows, R, C, 0, ws, (long)2 * C));
-  DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, gamma, beta, res, y, mean, rstd,
-                                   valid_rows, ws, g_cs, R, C, relu, eps, rep));
+  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, ws, gamma, beta, valid_rows,
+                     nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+  DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, res, y, valid_rows, coef, R, C,
+                                   relu));
 }
 
 void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
             const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
             bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, hipStream_t s) {
+  float* coef = ws + (long)2 * C * K;
   DLS_CHECK(hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * K, s));
   dim3 grid(cdiv(R, ROWS_PER_BLOCK), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
                                    valid_rows, R, C, relu, ws, (long)2 * C));
-  DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, mean, rstd, gamma,
-                                   valid_rows, ws, g_cs, R, C, relu, dx, dpre, dgamma, dbeta, dg_cs));
+  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, ws, gamma, nullptr, valid_rows,
+                     mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
+  DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, valid_rows, coef, R, C,
+                                   relu, dx, dpre));
 }
 
 void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s) {

@@ -1,0 +1,177 @@
+"""Shapley-value methods: GTG-Shapley (`GTG_shapley_value`), multi-round SV
+(`multiround_shapley_value`) and the config-only `Hierarchical_shapley_value`.
+
+Reference `method/shapley_value/*`: ShapleyValueAlgorithm(FedAVGAlgorithm) with
+accumulate=False (`shapley_value_algorithm.py:11-92`); subset utility = Test accuracy of the
+dataset-size-weighted FedAvg of the subset's round-t models (`:67-76`); optional
+`choose_best_subset`; `shapley_values.json` at exit; servers need the round-0 performance
+(`shapley_value_server.py:4-7`).
+
+MI355X-native: client models stay on device; each rank all-gathers the round's client rows
+once (RCCL), every subset model is one fused weighted row-sum, and batches of subset models
+are evaluated as one client-batched forward over the rank's test shard.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+
+from ...algorithm.fed_avg_algorithm import FedAVGAlgorithm
+from ...message import FlatParameterMessage
+from ...ops import fl
+from ...server.aggregation_server import AggregationServer
+from ...utils.logging import get_logger
+from ...worker.aggregation_worker import AggregationWorker
+from ..algorithm_factory import CentralizedAlgorithmFactory
+from .estimators import GTGShapleyValue, HierarchicalShapleyValue, MultiRoundShapleyValue
+
+
+class ShapleyValueAlgorithm(FedAVGAlgorithm):
+    sv_algorithm_cls = GTGShapleyValue
+    metric_type = "accuracy"
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.accumulate = False
+        self.sv_algorithm = None
+        self.shapley_values: dict = {}
+        self.shapley_values_S: dict = {}
+        self._rows: dict[int, torch.Tensor] = {}
+        self._sizes: dict[int, float] = {}
+
+    @property
+    def choose_best_subset(self) -> bool:
+        return bool(self.config.algorithm_kwargs.get("choose_best_subset", False))
+
+    def _process(self, msg, old_parameter) -> None:
+        sizes = msg.dataset_sizes.tolist()
+        for i, c in enumerate(msg.client_ids):
+            row = msg.data[i]
+            self._rows[c] = (row + old_parameter) if msg.kind == "delta" else row.clone()
+            self._sizes[c] = float(sizes[i])
+
+    def _gather_all(self):
+        comm = self.comm
+        ids = sorted(self._rows)
+        if comm.world == 1:
+            return ids, torch.stack([self._rows[c] for c in ids]) if ids else None, [self._sizes[c] for c in ids]
+        meta = comm.all_gather_object((ids, [self._sizes[c] for c in ids]))
+        maxn = max(len(m[0]) for m in meta)
+        P = self.layout.padded_size
+        local = torch.zeros((max(maxn, 1), P), dtype=torch.float32, device=self.device)
+        for i, c in enumerate(ids):
+            local[i] = self._rows[c]
+        parts = comm.all_gather(local)
+        rows, all_ids, all_sizes = {}, [], {}
+        for (pids, psizes), t in zip(meta, parts):
+            for i, c in enumerate(pids):
+                rows[c] = t[i]
+                all_sizes[c] = psizes[i]
+        all_ids = sorted(rows)
+        return all_ids, torch.stack([rows[c] for c in all_ids]), [all_sizes[c] for c in all_ids]
+
+    def _subset_models(self, subsets, ids, rows, sizes) -> torch.Tensor:
+        pos = {c: i for i, c in enumerate(ids)}
+        out = torch.empty((len(subsets), rows.shape[1]), dtype=torch.float32, device=rows.device)
+        for j, s in enumerate(subsets):
+            w = torch.zeros(len(ids), dtype=torch.float32)
+            tot = sum(sizes[pos[c]] for c in s)
+            for c in s:
+                w[pos[c]] = sizes[pos[c]] / tot
+            out[j] = fl.weighted_sum(rows, w.to(rows.device))
+        return out
+
+    def aggregate_worker_data(self, old_parameter: torch.Tensor) -> FlatParameterMessage:
+        server = self.server
+        rnd = server.round_number
+        ids, rows, sizes = self._gather_all()
+        if rows is None:
+            return super().aggregate_worker_data(old_parameter)
+        last = server.performance_stat.get(rnd - 1, server.performance_stat.get(max(server.performance_stat, default=0), {}))
+        last_metric = last.get(f"test_{self.metric_type}", 0.0)
+        kw = dict(self.config.algorithm_kwargs.get("sv_kwargs", {}))
+        if self.sv_algorithm_cls is HierarchicalShapleyValue:
+            kw.setdefault("part_number", self.config.algorithm_kwargs.get("part_number", 2))
+        if self.sv_algorithm is None:
+            self.sv_algorithm = self.sv_algorithm_cls(players=ids, last_round_metric=last_metric, seed=self.config.seed, **kw)
+        else:
+            self.sv_algorithm.reset_players(ids, last_metric)
+        chunk = int(self.config.algorithm_kwargs.get("sv_eval_batch", 32))
+
+        def batch_metric(subsets):
+            vals = []
+            for s0 in range(0, len(subsets), chunk):
+                models = self._subset_models(subsets[s0 : s0 + chunk], ids, rows, sizes)
+                _, acc = server.get_metrics_many(models)
+                vals.extend(acc if self.metric_type == "accuracy" else _)
+            return vals
+
+        self.sv_algorithm.set_batch_metric_function(batch_metric)
+        self.sv_algorithm.compute(round_number=rnd)
+        self.shapley_values[rnd] = dict(self.sv_algorithm.shapley_values)
+        self.shapley_values_S[rnd] = dict(self.sv_algorithm.shapley_values_S)
+        chosen = ids
+        if self.choose_best_subset and self.shapley_values_S[rnd]:
+            chosen = sorted(self.shapley_values_S[rnd])
+            get_logger().warning("use subset %s", chosen)
+        sel = [ids.index(c) for c in chosen]
+        w = torch.tensor([sizes[i] for i in sel], dtype=torch.float32, device=rows.device)
+        new = fl.weighted_sum(rows[sel].contiguous(), w / w.sum())
+        self._rows.clear()
+        msg = FlatParameterMessage(parameter=new, layout=self.layout, other_data=dict(self._other_data),
+                                   end_training=bool(self._end_training))
+        self._reset_acc()
+        return msg
+
+    def clear_worker_data(self) -> None:
+        super().clear_worker_data()
+        self._rows.clear()
+        self._sizes.clear()
+
+    def exit(self) -> None:
+        if self.server is None or not self.server.session.is_main:
+            return
+        os.makedirs(self.config.save_dir, exist_ok=True)
+        with open(os.path.join(self.config.save_dir, "shapley_values.json"), "wt", encoding="utf8") as f:
+            json.dump(self.shapley_values, f)
+        if self.choose_best_subset:
+            with open(os.path.join(self.config.save_dir, "shapley_values_S.json"), "wt", encoding="utf8") as f:
+                json.dump(self.shapley_values_S, f)
+
+
+class GTGShapleyValueAlgorithm(ShapleyValueAlgorithm):
+    sv_algorithm_cls = GTGShapleyValue
+
+
+class MultiRoundShapleyValueAlgorithm(ShapleyValueAlgorithm):
+    sv_algorithm_cls = MultiRoundShapleyValue
+
+
+class HierarchicalShapleyValueAlgorithm(ShapleyValueAlgorithm):
+    sv_algorithm_cls = HierarchicalShapleyValue
+
+
+class ShapleyValueServer(AggregationServer):
+    def __init__(self, config, endpoint, algorithm=None, session=None, **kwargs):
+        super().__init__(config, endpoint, algorithm=algorithm, session=session, **kwargs)
+        self.need_init_performance = True
+
+
+class GTGShapleyValueServer(ShapleyValueServer):
+    pass
+
+
+class MultiRoundShapleyValueServer(ShapleyValueServer):
+    pass
+
+
+for _name, _algo, _server in (
+    ("GTG_shapley_value", GTGShapleyValueAlgorithm, GTGShapleyValueServer),
+    ("multiround_shapley_value", MultiRoundShapleyValueAlgorithm, MultiRoundShapleyValueServer),
+    ("Hierarchical_shapley_value", HierarchicalShapleyValueAlgorithm, ShapleyValueServer),
+):
+    CentralizedAlgorithmFactory.register_algorithm(
+        algorithm_name=_name, client_cls=AggregationWorker, server_cls=_server, algorithm_cls=_algo)

@@ -37,6 +37,7 @@ class AggregationServer(Server):
         self.early_stop = bool(config.algorithm_kwargs.get("early_stop", False))
         self.global_parameter: torch.Tensor | None = None
         self.selected: list[int] = []
+        self.last_result = None
 
     @property
     def round_number(self) -> int:
@@ -100,6 +101,7 @@ class AggregationServer(Server):
         """Broadcast to the next round's selected workers (M5/M1); `None` to the rest (M2,
         0 bytes). Returns (parameters as the clients receive them, downlink bytes)."""
         self._before_send_result(result)
+        self.last_result = result
         if result.end_training:
             self._ended = True
         self.selected = self._select_workers_next(result)
@@ -131,28 +133,29 @@ class AggregationServer(Server):
         round_stat = {f"test_{k}": v for k, v in metric.items()}
         key = self._get_stat_key() if key is None else key
         self._stat[key] = round_stat
+        self.last_recorded = (key, round_stat)
         get_logger().info("round: %s, test accuracy %.4f loss %.4f", key, metric["accuracy"], metric["loss"])
         if self.session.is_main:
             os.makedirs(self.save_dir, exist_ok=True)
             with open(os.path.join(self.save_dir, "round_record.json"), "wt", encoding="utf8") as f:
                 json.dump(self._stat, f)
-        if metric["accuracy"] > self._max_acc and key != 0:
-            prev = self._max_acc
-            self._max_acc_before = prev
+        if key == 0:
+            return
+        # plateau bookkeeping against the best accuracy *before* this round (fixes B7)
+        if metric["accuracy"] > self._max_acc + 0.001:
+            self._plateau = 0
+        else:
+            self._plateau += 1
+            get_logger().info("plateau is %s (best %.4f, current %.4f)", self._plateau, self._max_acc,
+                              metric["accuracy"])
+        if metric["accuracy"] > self._max_acc:
             self._max_acc = metric["accuracy"]
             if self.config.save_models and self.session.is_main:
                 self._save_model(parameter, os.path.join(self.save_dir, "best_global_model.pk"))
 
     def _convergent(self) -> bool:
-        """Plateau ≥5 rounds within 0.001 of the best accuracy *before* this round (B7)."""
-        cur = self._stat[self._get_stat_key()]["test_accuracy"]
-        best_before = getattr(self, "_best_before", 0.0)
-        if cur > best_before + 0.001:
-            self._best_before = max(best_before, cur)
-            self._plateau = 0
-            return False
-        self._plateau += 1
-        get_logger().warning("plateau is %s (best %.4f, current %.4f)", self._plateau, best_before, cur)
+        """≥5 consecutive evaluations without beating the best by 0.001
+        (reference `aggregation_server.py:166-184`)."""
         return self._plateau >= 5
 
     def _save_model(self, parameter: torch.Tensor, path: str) -> None:

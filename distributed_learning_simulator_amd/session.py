@@ -116,6 +116,7 @@ class Session:
         init = server._before_start()
         theta_recv, down = server.send_result(init)
         self.bytes_down_total += down
+        server.last_recorded = None  # the round-0 (init) stat is not a round row
         if hasattr(server, "run_rounds"):  # methods with their own round structure
             server.run_rounds(self, theta_recv)
         else:
@@ -173,7 +174,11 @@ class Session:
         wall = time.perf_counter() - t0
         self.bytes_up_total += up
         self.bytes_down_total += down
-        stat = self.server.performance_stat.get(r, {})
+        rec = getattr(self.server, "last_recorded", None)
+        stat = {}
+        if rec is not None:
+            r, stat = rec
+            self.server.last_recorded = None
         row = {"round": r, "wall_s": wall, "rounds_per_s": 1.0 / max(wall, 1e-9), "selected_clients": len(selected),
                "comm_bytes_up": up, "comm_bytes_down": down, "comm_bytes_total": up + down,
                "gpus": self.comm.world, **stat, **extra}
