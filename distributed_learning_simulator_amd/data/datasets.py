@@ -87,7 +87,7 @@ class ImageDataset:
     Labels are a seeded balanced permutation. `gather(idx)` returns [.., H, W, C]."""
 
     def __init__(self, spec: DatasetSpec, split: str, seed: int, device, dtype,
-                 materialize_limit: int = 2_000_000_000, noise: float = 1.0):
+                 materialize_limit: int = 2_000_000_000, noise: float = 1.0, signal: float = 0.35):
         self.spec = spec
         self.split = split
         self.device = device
@@ -101,7 +101,8 @@ class ImageDataset:
         gp = torch.Generator().manual_seed(seed * 7919 + 17)  # prototypes shared by splits
         low = torch.randn(spec.num_classes, C, max(H // 4, 2), max(W // 4, 2), generator=gp)
         proto = torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
-        self.prototypes = proto.permute(0, 2, 3, 1).contiguous()  # [classes, H, W, C]
+        # weak class signal under unit noise: learnable, but not in a single step
+        self.prototypes = (proto * signal).permute(0, 2, 3, 1).contiguous()  # [classes, H, W, C]
         self.salt = seed * 2654435761 + (0 if split == "train" else 97)
         self.materialized = n * H * W * C <= materialize_limit
         self.labels_dev = self.labels.to(device)
@@ -201,8 +202,9 @@ def create_dataset_collection(name: str, dataset_kwargs: dict | None, seed: int,
     kw = dict(dataset_kwargs or {})
     if spec.kind == "image":
         noise = float(kw.get("noise", 1.0))
-        return DatasetCollection(spec, ImageDataset(spec, "train", seed, device, dtype, noise=noise),
-                                 ImageDataset(spec, "test", seed, device, dtype, noise=noise))
+        signal = float(kw.get("signal", 0.35))
+        return DatasetCollection(spec, ImageDataset(spec, "train", seed, device, dtype, noise=noise, signal=signal),
+                                 ImageDataset(spec, "test", seed, device, dtype, noise=noise, signal=signal))
     if spec.kind == "text":
         return DatasetCollection(spec, TextDataset(spec, "train", seed, device), TextDataset(spec, "test", seed, device))
     if spec.kind == "graph":

@@ -130,11 +130,13 @@ class CohortTrainer:
     # ------------------------------------------------------------------ schedule
     def build_schedule(self, shards: list[torch.Tensor], epochs: int, seed: int,
                        epoch_offset: int = 0, total_epochs: int | None = None,
-                       lr_override: float | None = None, first_epoch_resets: bool = True) -> RoundSchedule:
+                       lr_override: float | None = None, first_epoch_resets: bool = True,
+                       min_steps_per_epoch: int = 1) -> RoundSchedule:
         B = self.hyper.batch_size
         K = len(shards)
         total_epochs = total_epochs or epochs
-        per_epoch_steps = [max(1, max((s.numel() + B - 1) // B for s in shards)) for _ in range(epochs)]
+        per_epoch_steps = [max(min_steps_per_epoch, max((s.numel() + B - 1) // B for s in shards))
+                           for _ in range(epochs)]
         S = sum(per_epoch_steps)
         idx = torch.zeros((S, K, B), dtype=torch.int32)
         counts = torch.zeros((S, K), dtype=torch.int32)
@@ -171,9 +173,13 @@ class CohortTrainer:
                              epoch_end, S, K)
 
     # --------------------------------------------------------------------- train
-    def forward_loss(self, K: int, x, labels, valid):
+    def forward_loss(self, K: int, x, labels, valid, shared: bool = False, grad_rows=None):
+        """shared=True: all K clients use parameter row 0 (synchronous-gradient methods such as
+        sign-SGD, where every client holds the same model); per-client gradients still land in
+        separate rows of `grad_rows` (default grad[:K])."""
         b = self.buffers
-        params = BoundParams(self.layout, b.compute[:K], b.grad[:K])
+        grad = grad_rows if grad_rows is not None else b.grad[:K]
+        params = BoundParams(self.layout, b.compute[:1] if shared else b.compute[:K], grad, K=K)
         ctx = RunCtx(params, valid, training=True)
         logits = self.model.forward(x, ctx)
         loss, correct = Fn.cross_entropy(logits, labels, valid)

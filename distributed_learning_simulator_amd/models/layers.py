@@ -117,27 +117,9 @@ class Conv2d(Module):
 
     def forward(self, x, ctx):
         P = ctx.P
-        y = Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad)
-        if self.b:
-            # bias only appears in LeNet; fold through a broadcast add (autograd handles db)
-            y = _BiasAdd.apply(y, ctx.token, P.w(self.b), P.g(self.b))
-        return y
-
-
-class _BiasAdd(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, y, token, b, gb):
-        ctx.gb = gb
-        K = y.shape[0]
-        shape = (b.shape[0],) + (1,) * (y.dim() - 2) + (b.shape[-1],)
-        return y + b.reshape(shape).to(y.dtype)
-
-    @staticmethod
-    def backward(ctx, dy):
-        if ctx.gb is not None:
-            red = tuple(range(1, dy.dim() - 1))
-            ctx.gb.copy_(dy.float().sum(dim=red))
-        return dy, None, None, None
+        b = P.w(self.b) if self.b else None
+        gb = P.g(self.b) if self.b else None
+        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb)
 
 
 class BatchNorm(Module):

@@ -22,11 +22,11 @@ def _be(t):
 # --------------------------------------------------------------------------- conv2d
 class _Conv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, token, w, gw, stride, pad):
+    def forward(ctx, x, token, w, gw, stride, pad, b, gb):
         be = _be(x)
-        y = be.conv_fwd(x, w, stride, pad)
+        y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.save_for_backward(x, w)
-        ctx.gw, ctx.stride, ctx.pad = gw, stride, pad
+        ctx.gw, ctx.gb, ctx.stride, ctx.pad = gw, gb, stride, pad
         return y
 
     @staticmethod
@@ -40,13 +40,17 @@ class _Conv(torch.autograd.Function):
         if ctx.gw is not None:
             if be is ref:
                 ctx.gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (x.shape[0],) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
+                if ctx.gb is not None:
+                    ctx.gb.copy_(dy.float().sum(dim=(1, 2, 3)))
             else:
                 be.conv_wgrad(dy, x, ctx.gw, ctx.stride, ctx.pad)
-        return dx, None, None, None, None, None
+                if ctx.gb is not None:
+                    be.bias_grad(dy, ctx.gb)
+        return dx, None, None, None, None, None, None, None
 
 
-def conv2d(x, token, w, gw, stride=1, pad=0):
-    return _Conv.apply(x, token, w, gw, stride, pad)
+def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None):
+    return _Conv.apply(x, token, w, gw, stride, pad, b, gb)
 
 
 # --------------------------------------------------------------------------- linear

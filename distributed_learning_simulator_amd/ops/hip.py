@@ -136,6 +136,15 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int):
                Co, R, K, _s())
 
 
+def bias_grad(dy, gb):
+    """gb[k, c] = Σ_{b,h,w} dy[k, b, h, w, c] (conv bias gradient)."""
+    K = dy.shape[0]
+    C = dy.shape[-1]
+    rows = dy.numel() // (K * C)
+    gb.zero_()
+    _C.col_sum(_p(dy.contiguous()), _p(gb), gb.stride(0), K, rows, C, _s())
+
+
 # --------------------------------------------------------------------------- linear
 def linear_fwd(x, w, b=None):
     K, N, Fi = x.shape
@@ -196,7 +205,8 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5)
 def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre):
     K, R, C = x.shape
     g_cs, rep = _client_view(gamma, K)
-    assert rep == 1
+    # the kernels index γ by client k with stride g_cs: shared (Kw=1 → stride 0) or per client
+    assert rep == 1 or gamma.shape[0] == 1, "bn_bwd supports per-client or fully shared γ"
     dx = torch.empty_like(x)
     dpre = torch.empty_like(x) if need_dpre else None
     ws = _workspace(5 * K * C, x.device)

@@ -44,10 +44,11 @@ def _w_grouped(w: torch.Tensor) -> torch.Tensor:
     return w.permute(0, 1, 4, 2, 3).reshape(K * Co, Ci, kh, kw)
 
 
-def conv_fwd(x, w, stride: int, pad: int):
+def conv_fwd(x, w, stride: int, pad: int, bias=None):
     K = x.shape[0]
     w = _match(w, K)
-    y = F.conv2d(_to_grouped(x), _w_grouped(w), stride=stride, padding=pad, groups=K)
+    b = _match(bias, K).reshape(-1).to(x.dtype) if bias is not None else None
+    y = F.conv2d(_to_grouped(x), _w_grouped(w).to(x.dtype), b, stride=stride, padding=pad, groups=K)
     return _from_grouped(y, K).contiguous()
 
 

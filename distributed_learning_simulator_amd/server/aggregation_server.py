@@ -122,7 +122,8 @@ class AggregationServer(Server):
     def _after_send_result(self, result: Message) -> None:
         if isinstance(result, FlatParameterMessage) and not result.in_round:
             self._round_number += 1
-        self._algorithm.clear_worker_data()
+        if self._algorithm is not None:
+            self._algorithm.clear_worker_data()
 
     def _stopped(self) -> bool:
         return self._ended or self._round_number > self.config.round
