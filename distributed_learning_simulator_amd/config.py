@@ -52,7 +52,7 @@ class DistributedTrainingConfig:
     # --- trainer / model / data keys (external Config in the reference) ---
     dataset_name: str = ""
     model_name: str = ""
-    optimizer_name: str = "SGD"
+    optimizer_name: str = ""  # "" => SGD (Adam for graph datasets; parity unpinned)
     learning_rate: float = 0.01
     learning_rate_scheduler_name: str | None = None
     epoch: int = 1

@@ -301,18 +301,47 @@ class TransformerClassifier(Module):
 
 # ---------------------------------------------------------------------------- GCN
 class GCNConv(Module):
+    """PyG `GCNConv`: out = Â (X Wᵀ) + b (bias after propagation); params `lin.weight`, `bias`."""
+
     kind = "GCNConv"
 
     def __init__(self, fin, fout):
         super().__init__()
-        self.child("lin", Linear(fin, fout, bias=True))
+        self.fout = fout
+        self.child("lin", Linear(fin, fout, bias=False))
 
-    def forward(self, x, ctx, graph):
-        # Â (X W) + b  — bias added after propagation like PyG; here lin's bias before
-        # propagation is equivalent up to Â's row sums (=1 for the sym-normalised Â with
-        # self loops only approximately); we keep PyG's order explicitly.
-        h = self.lin.forward(x, ctx)
-        return Fn.spmm(h, graph)
+    def register(self, layout):
+        super().register(layout)
+        self.b = layout.add(f"{self.name}.bias", (self.fout,), "zeros", 1, self.name).name
+
+    def own_params(self):
+        return [self.b]
+
+    def forward(self, x, ctx, edges, K):
+        from ..data.graph import propagate
+
+        P = ctx.P
+        if x.dim() == 2:  # shared node features
+            h = Fn.linear_shared_input(x, ctx.token, P.w(self.lin.w), P.g(self.lin.w))
+        else:
+            h = self.lin.forward(x, ctx)
+        h = propagate(h, edges)
+        return _AddBias.apply(h, ctx.token, P.w(self.b), P.g(self.b))
+
+
+class _AddBias(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, token, b, gb):
+        ctx.gb = gb
+        K = h.shape[0]
+        bb = b if b.shape[0] == K else b.repeat_interleave(K // b.shape[0], 0)
+        return h + bb[:, None, :].to(h.dtype)
+
+    @staticmethod
+    def backward(ctx, dh):
+        if ctx.gb is not None:
+            ctx.gb.copy_(dh.float().sum(1))
+        return dh, None, None, None
 
 
 class GCNNet(Module):
@@ -324,12 +353,20 @@ class GCNNet(Module):
         self.convs = [self.child(f"conv{i + 1}", GCNConv(dims[i], dims[i + 1])) for i in range(layers)]
 
     def forward(self, batch, ctx):
-        x, graph = batch
+        from ..data.graph import substitute_halo
+
+        h = batch.x
+        K = ctx.P.K
         for i, c in enumerate(self.convs):
-            x = c.forward(x, ctx, graph)
+            if i > 0 and batch.views is not None and batch.views.share_feature:
+                h = substitute_halo(h, batch.views, batch.comm)
+            h = c.forward(h, ctx, batch.l0 if i == 0 else batch.l1, K)
             if i + 1 < len(self.convs):
-                x = torch.relu(x)
-        return x
+                h = torch.relu(h)
+        if batch.seeds is None:
+            return h
+        idx = batch.seeds.long().unsqueeze(-1).expand(-1, -1, h.shape[-1])
+        return torch.gather(h, 1, idx)
 
 
 # --------------------------------------------------------------------------- build

@@ -88,6 +88,41 @@ def linear(x, token, w, b, gw, gb):
     return y.reshape(*shp[:-1], y.shape[-1])
 
 
+class _LinearSharedInput(torch.autograd.Function):
+    """y[k] = x W_kᵀ for ONE input x [N, Fi] shared by K weight rows: a single GEMM against the
+    concatenated weights [K·Fo, Fi] (GCN first layer: node features are common to all clients)."""
+
+    @staticmethod
+    def forward(ctx, x, token, w, gw):
+        be = _be(x)
+        K, Fo, Fi = w.shape
+        wcat = w.reshape(1, K * Fo, Fi).contiguous()
+        y = be.linear_fwd(x.unsqueeze(0).contiguous(), wcat, None)  # [1, N, K*Fo]
+        ctx.save_for_backward(x)
+        ctx.gw, ctx.K, ctx.Fo = gw, K, Fo
+        return y[0].view(-1, K, Fo).permute(1, 0, 2).contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        if ctx.gw is not None:
+            be = _be(dy)
+            K, Fo = ctx.K, ctx.Fo
+            dyc = dy.permute(1, 0, 2).reshape(1, -1, K * Fo).contiguous()
+            Fi = x.shape[-1]
+            if be is ref:
+                dw, _ = ref.linear_wgrad(dyc.float(), x.unsqueeze(0).float(), False)
+            else:
+                dw = torch.empty((1, K * Fo, Fi), dtype=torch.float32, device=dy.device)
+                be.linear_wgrad(dyc, x.unsqueeze(0).contiguous(), dw, None)
+            ctx.gw.copy_(dw.view(K, Fo, Fi))
+        return None, None, None, None
+
+
+def linear_shared_input(x, token, w, gw):
+    return _LinearSharedInput.apply(x, token, w, gw)
+
+
 # ------------------------------------------------------------------------ batchnorm
 class _BN(torch.autograd.Function):
     @staticmethod

@@ -57,7 +57,7 @@ class Session:
         self.dc = create_dataset_collection(cfg.dataset_name, cfg.dataset_kwargs, cfg.seed, self.device,
                                             self.compute_dtype)
         if practitioners is None:
-            labels = self.dc.train.labels if self.dc.spec.kind != "graph" else self.dc.graph.labels_cpu
+            labels = self.dc.train.labels  # (graph: labels of the training nodes)
             practitioners = create_practitioners(cfg, labels)
         else:
             # reference algorithm_factory.py:15-23: worker ids = rank of practitioner id
@@ -72,6 +72,10 @@ class Session:
         n_sel = min(n_sel, cfg.worker_number)
         per_rank = math.ceil(n_sel / self.comm.world)
         capacity = max(1, min(per_rank, cfg.cohort_size) if cfg.cohort_size else per_rank)
+        if self.dc.spec.kind == "graph":
+            capacity = per_rank  # halo exchange needs every client of the rank resident at once
+        if not cfg.optimizer_name:
+            cfg.optimizer_name = "Adam" if self.dc.spec.kind == "graph" else "SGD"
         self.hyper = HyperParameter.from_config(cfg)
         self.trainer = CohortTrainer(self.model, self.dc, self.hyper, self.device, self.compute_dtype, capacity)
         algo = cfg.distributed_algorithm
