@@ -101,16 +101,19 @@ PYBIND11_MODULE(_dls_hip, m) {
     masked_weighted_sum(P<const float>(x), P<const uint8_t>(mask), P<const float>(w), P<float>(num), P<float>(den), K, Pn,
                         ld, S(s));
   });
-  m.def("dropout_mask", [](ptr mask, long n, float p, uint32_t seed, ptr s) { dropout_mask(P<uint8_t>(mask), n, p, seed, S(s)); });
+  m.def("dropout_mask", [](ptr mask, int K, long Pn, float p, ptr seeds, ptr s) {
+    dropout_mask(P<uint8_t>(mask), K, Pn, p, P<const uint32_t>(seeds), S(s));
+  });
   m.def("block_sq_norms", [](ptr x, ptr ids, ptr out, int K, long Pn, long ld, int nb, ptr s) {
     block_sq_norms(P<const float>(x), P<const int>(ids), P<float>(out), K, Pn, ld, nb, S(s));
   });
   m.def("seg_minmax", [](ptr x, ptr seg, ptr mn, ptr mx, int K, long Pn, long ld, int nseg, ptr s) {
     seg_minmax(P<const float>(x), P<const int>(seg), P<float>(mn), P<float>(mx), K, Pn, ld, nseg, S(s));
   });
-  m.def("stochastic_qdq", [](ptr x, ptr seg, ptr mn, ptr mx, int K, long Pn, long ld, int nseg, uint32_t seed,
+  m.def("stochastic_qdq", [](ptr x, ptr seg, ptr mn, ptr mx, int K, long Pn, long ld, int nseg, ptr seeds,
                              int levels, ptr s) {
-    stochastic_qdq(P<float>(x), P<const int>(seg), P<const float>(mn), P<const float>(mx), K, Pn, ld, nseg, seed, levels,
+    stochastic_qdq(P<float>(x), P<const int>(seg), P<const float>(mn), P<const float>(mx), K, Pn, ld, nseg,
+                   P<const uint32_t>(seeds), levels,
                    S(s));
   });
   m.def("sign_pack", [](ptr g, ptr out, int K, long Pn, long ld, ptr s) { sign_pack(P<const float>(g), P<uint8_t>(out), K, Pn, ld, S(s)); });

@@ -72,13 +72,13 @@ void delta_rows(const float* theta, const float* base, float* out, int K, long P
 void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s);
 void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
                          long ld, hipStream_t s);
-void dropout_mask(uint8_t* mask, long n, float p, uint32_t seed, hipStream_t s);
+void dropout_mask(uint8_t* mask, int K, long P, float p, const uint32_t* seeds, hipStream_t s);
 void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
                     hipStream_t s);
 void seg_minmax(const float* x, const int* seg, float* mn, float* mx, int K, long P, long ld, int nseg,
                 hipStream_t s);
 void stochastic_qdq(float* x, const int* seg, const float* mn, const float* mx, int K, long P, long ld, int nseg,
-                    uint32_t seed, int levels, hipStream_t s);
+                    const uint32_t* seeds, int levels, hipStream_t s);
 void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s);
 void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, long P, hipStream_t s);
 void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, long n_tok, int D, long t_cs,

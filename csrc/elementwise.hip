@@ -294,11 +294,14 @@ __global__ void masked_weighted_sum_kernel(const float* __restrict__ x, const ui
   }
 }
 
-__global__ void dropout_mask_kernel(uint8_t* __restrict__ mask, long n, float p, uint32_t seed) {
+// Per-row seeds are derived from the CLIENT id (not its row position), so masks / rounding
+// noise are identical whatever rank or wave hosts the client (matches ops.fl.uniform_rows).
+__global__ void dropout_mask_kernel(uint8_t* __restrict__ mask, long P, float p, const uint32_t* __restrict__ seeds,
+                                    long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  // matches ops.fl.philox_uniform: hash of (seed, element index)
-  const uint32_t h = mix32((uint32_t)(i & 0xffffffffu), seed);
+  const long k = i / P, e = i - k * P;
+  const uint32_t h = mix32((uint32_t)(e & 0xffffffffu), seeds[k]);
   mask[i] = ((float)h * (1.f / 4294967296.f)) >= p;
 }
 
@@ -372,14 +375,15 @@ __global__ void seg_minmax_kernel(const float* __restrict__ x, const int* __rest
 
 __global__ void stochastic_qdq_kernel(float* __restrict__ x, const int* __restrict__ seg,
                                       const float* __restrict__ mn, const float* __restrict__ mx, long P, long ld,
-                                      int nseg, uint32_t seed, int levels) {
+                                      int nseg, const uint32_t* __restrict__ seeds, int levels) {
   const int k = blockIdx.y;
+  const uint32_t seed = seeds[k];
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
     const int s = seg[i];
     const float lo = mn[(long)k * nseg + s];
     const float sc = fmaxf((mx[(long)k * nseg + s] - lo) / levels, 1e-30f);
     const long gi = (long)k * ld + i;
-    const float u = (float)mix32((uint32_t)(gi & 0xffffffffu), seed) * (1.f / 4294967296.f);
+    const float u = (float)mix32((uint32_t)(i & 0xffffffffu), seed) * (1.f / 4294967296.f);
     float q = floorf((x[gi] - lo) / sc + u);
     q = fminf(fmaxf(q, 0.f), (float)levels);
     x[gi] = lo + q * sc;
@@ -517,8 +521,9 @@ void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, fl
                      K, P, ld);
 }
 
-void dropout_mask(uint8_t* mask, long n, float p, uint32_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(dropout_mask_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, mask, n, p, seed);
+void dropout_mask(uint8_t* mask, int K, long P, float p, const uint32_t* seeds, hipStream_t s) {
+  const long n = (long)K * P;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, mask, P, p, seeds, n);
 }
 
 void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
@@ -535,7 +540,7 @@ void seg_minmax(const float* x, const int* seg, float* mn, float* mx, int K, lon
 }
 
 void stochastic_qdq(float* x, const int* seg, const float* mn, const float* mx, int K, long P, long ld, int nseg,
-                    uint32_t seed, int levels, hipStream_t s) {
+                    const uint32_t* seed, int levels, hipStream_t s) {
   dim3 grid(grid_for(P, 256, 2048), K);
   hipLaunchKernelGGL(stochastic_qdq_kernel, grid, dim3(256), 0, s, x, seg, mn, mx, P, ld, nseg, seed, levels);
 }

@@ -131,7 +131,9 @@ class CohortTrainer:
     def build_schedule(self, shards: list[torch.Tensor], epochs: int, seed: int,
                        epoch_offset: int = 0, total_epochs: int | None = None,
                        lr_override: float | None = None, first_epoch_resets: bool = True,
-                       min_steps_per_epoch: int = 1) -> RoundSchedule:
+                       min_steps_per_epoch: int = 1, client_ids: list[int] | None = None) -> RoundSchedule:
+        """Per-client shuffles are keyed by (seed, CLIENT id, epoch) so a client sees the same
+        batches whichever rank/wave/row hosts it."""
         B = self.hyper.batch_size
         K = len(shards)
         total_epochs = total_epochs or epochs
@@ -150,7 +152,8 @@ class CohortTrainer:
                 n = shard.numel()
                 if n == 0:
                     continue
-                g = torch.Generator().manual_seed((seed * 1_000_003 + k * 7919 + e * 104729) & 0x7FFFFFFF)
+                key = client_ids[k] if client_ids is not None else k
+                g = torch.Generator().manual_seed((seed * 1_000_003 + key * 7919 + e * 104729) & 0x7FFFFFFF)
                 perm = shard[torch.randperm(n, generator=g)]
                 nb = (n + B - 1) // B
                 padded = torch.cat([perm, perm[:1].expand(nb * B - n)]) if nb * B > n else perm

@@ -31,8 +31,8 @@ class FedDropoutAvgWorker(AggregationWorker):
     def _get_sent_data(self, wave, theta_g, stats) -> CohortMessage:
         msg = super()._get_sent_data(wave, theta_g, stats)
         K, P = msg.data.shape
-        seed = (self.config.seed * 1_000_003 + self._round_num * 7919 + wave[0]) & 0x7FFFFFFF
-        mask = fl.dropout_mask((K, P), self._dropout_rate, seed, msg.data.device)
+        seed = (self.config.seed * 1_000_003 + self._round_num * 7919) & 0x7FFFFFFF
+        mask = fl.dropout_mask((K, P), self._dropout_rate, fl.row_seeds(seed, list(wave)), msg.data.device)
         mask &= self.session.layout.valid_mask(msg.data.device).unsqueeze(0)
         msg.data.mul_(mask)
         msg.mask = mask

@@ -85,7 +85,7 @@ class GraphWorker(AggregationWorker):
         self.trainer.hyper.batch_size = B
         try:
             return self.trainer.build_schedule(shards, self.local_epochs(),
-                                               seed=self.config.seed * 100_003 + round_num * 1009 + wave[0],
+                                               seed=self.config.seed * 100_003 + round_num * 1009, client_ids=list(wave),
                                                min_steps_per_epoch=self._batch_number)
         finally:
             self.trainer.hyper.batch_size = saved

@@ -61,7 +61,7 @@ class FedOBDWorker(AggregationWorker):
         if self.phase != Phase.STAGE_TWO:
             return super().build_schedule(round_num, wave)
         return self.trainer.build_schedule(
-            self.shards(wave), 1, seed=self.config.seed * 100_003 + round_num * 1009 + self._stage2_epoch * 31 + wave[0],
+            self.shards(wave), 1, seed=self.config.seed * 100_003 + round_num * 1009 + self._stage2_epoch * 31, client_ids=list(wave),
             epoch_offset=self._stage2_epoch - 1, total_epochs=self._second_phase_epoch)
 
     def _get_sent_data(self, wave, theta_g, stats) -> CohortMessage:

@@ -56,7 +56,7 @@ class SignSGDWorker(AggregationWorker):
         steps_per_epoch = max(1, max((n + B - 1) // B for n in all_sizes))
         shards = self.shards(local) if local else []
         sched = tr.build_schedule(shards, self.local_epochs(), seed=self.config.seed * 100_003 + round_num,
-                                  min_steps_per_epoch=steps_per_epoch) if local else None
+                                  min_steps_per_epoch=steps_per_epoch, client_ids=local) if local else None
         epochs = self.local_epochs()
         S = steps_per_epoch * epochs
         stats = TrainStats(epochs, max(len(local), 1), tr.device)

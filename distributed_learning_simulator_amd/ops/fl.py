@@ -80,7 +80,7 @@ def philox_uniform(shape, seed: int, offset: int, device) -> torch.Tensor:
 
 def _mix(x: torch.Tensor, seed: int) -> torch.Tensor:
     m = 0xFFFFFFFF
-    x = (x ^ (seed * 0x9E3779B9)) & m
+    x = (x ^ ((seed * 0x9E3779B9) & m)) & m
     x = x ^ (x >> 16)
     x = (x * 0x7FEB352D) & m
     x = x ^ (x >> 15)
@@ -89,12 +89,31 @@ def _mix(x: torch.Tensor, seed: int) -> torch.Tensor:
     return x
 
 
-def dropout_mask(shape, p: float, seed: int, device) -> torch.Tensor:
-    """Bernoulli(1-p) keep-mask [K,P] keyed by (seed, element)."""
+def row_seeds(seed: int, keys: list[int]) -> list[int]:
+    """Per-row 32-bit seeds derived from (seed, CLIENT id): masks and rounding noise do not
+    depend on which rank / wave / row hosts a client, so 1-GPU and N-GPU runs agree."""
+    out = []
+    for k in keys:
+        h = (seed * 0x9E3779B1 + (k + 1) * 0x85EBCA77 + 0x27D4EB2F) & 0xFFFFFFFF
+        h ^= h >> 15
+        h = (h * 0x2C1B3C6D) & 0xFFFFFFFF
+        h ^= h >> 12
+        out.append(h)
+    return out
+
+
+def uniform_rows(seeds: list[int], P: int, device) -> torch.Tensor:
+    """[K, P] uniforms u[k, i] = hash(i, seeds[k]) (identical to the kernels' mix32)."""
+    idx = torch.arange(P, device=device, dtype=torch.int64)
+    return torch.stack([(_mix(idx, s).float() * (1.0 / 4294967296.0)) for s in seeds])
+
+
+def dropout_mask(shape, p: float, seeds: list[int], device) -> torch.Tensor:
+    """Bernoulli(1-p) keep-mask [K,P]; row k keyed by seeds[k]."""
     be = backend.get(torch.empty(0, device=device))
     if be is ref:
-        return philox_uniform(shape, seed, 0, device) >= p
-    return be.dropout_mask(shape, p, seed)
+        return uniform_rows(seeds, shape[1], device) >= p
+    return be.dropout_mask(shape, p, seeds)
 
 
 def block_sq_norms(x, block_offsets, block_ids):

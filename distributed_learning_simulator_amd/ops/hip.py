@@ -393,12 +393,16 @@ def masked_weighted_sum(x, mask, w):
     return num, den
 
 
-def dropout_mask(shape, p, seed):
-    n = 1
-    for d in shape:
-        n *= d
+def _seeds_dev(seeds) -> torch.Tensor:
+    return torch.tensor([s & 0xFFFFFFFF for s in seeds], dtype=torch.int64).to(torch.int32).to("cuda")
+
+
+def dropout_mask(shape, p, seeds):
+    K, P = shape
+    assert len(seeds) == K
     m = torch.empty(shape, dtype=torch.uint8, device="cuda")
-    _C.dropout_mask(_p(m), n, float(p), seed & 0xFFFFFFFF, _s())
+    sd = _seeds_dev(seeds)
+    _C.dropout_mask(_p(m), K, P, float(p), _p(sd), _s())
     return m.bool()
 
 
@@ -410,15 +414,17 @@ def block_sq_norms(x, block_offsets, block_ids):
     return out
 
 
-def stochastic_qdq(x, seg_ids, nseg, seed, levels):
+def stochastic_qdq(x, seg_ids, nseg, seeds, levels):
     K, P, ld = _row_args(x)
-    x = x.contiguous() if x.stride(0) != ld else x
+    assert len(seeds) == K
     mn = torch.full((K, nseg), float("inf"), dtype=torch.float32, device=x.device)
     mx = torch.full((K, nseg), float("-inf"), dtype=torch.float32, device=x.device)
     seg = seg_ids.to(torch.int32).contiguous()
-    out = x.clone()
+    out = x.contiguous().clone()
+    ld = out.stride(0)
+    sd = _seeds_dev(seeds)
     _C.seg_minmax(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, _s())
-    _C.stochastic_qdq(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, seed & 0xFFFFFFFF, levels, _s())
+    _C.stochastic_qdq(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, _p(sd), levels, _s())
     return out
 
 

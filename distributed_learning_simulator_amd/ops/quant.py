@@ -27,7 +27,7 @@ import math
 import torch
 
 from . import backend, ref
-from .fl import philox_uniform
+from .fl import uniform_rows
 
 
 def _seg_minmax(x: torch.Tensor, seg_ids: torch.Tensor, nseg: int):
@@ -40,20 +40,20 @@ def _seg_minmax(x: torch.Tensor, seg_ids: torch.Tensor, nseg: int):
     return mn, mx
 
 
-def stochastic_quantize(x: torch.Tensor, seg_ids: torch.Tensor, seg_sizes: torch.Tensor, seed: int,
+def stochastic_quantize(x: torch.Tensor, seg_ids: torch.Tensor, seg_sizes: torch.Tensor, seeds: list[int],
                         levels: int = 255):
-    """Returns (dequantised x [K,P], wire_bytes [K] int)."""
+    """Returns (dequantised x [K,P], wire_bytes [K] int). seeds: per-row (per-client) seeds."""
     be = backend.get(x)
     nseg = int(seg_sizes.numel())  # + 1 trailing slot for inter-tensor padding
     if be is not ref:
-        dq = be.stochastic_qdq(x, seg_ids, nseg + 1, seed, levels)
+        dq = be.stochastic_qdq(x, seg_ids, nseg + 1, seeds, levels)
     else:
         mn, mx = _seg_minmax(x, seg_ids, nseg + 1)
         scale = ((mx - mn) / levels).clamp(min=1e-30)
         sid = seg_ids.long()
         lo = mn[:, sid]
         sc = scale[:, sid]
-        u = philox_uniform(x.shape, seed, 0, x.device)
+        u = uniform_rows(seeds, x.shape[1], x.device)
         q = torch.floor((x.float() - lo) / sc + u).clamp(0, levels)
         dq = lo + q * sc
     P_valid = int(seg_sizes.sum().item())

@@ -20,7 +20,7 @@ from __future__ import annotations
 import torch
 
 from ..message import CohortMessage
-from ..ops import quant
+from ..ops import fl, quant
 from ..utils.logging import get_logger
 
 
@@ -120,7 +120,8 @@ class StochasticQuantClientEndpoint(QuantClientEndpoint):
     levels = 255
 
     def quantize(self, msg, seed):
-        dq, wire = quant.stochastic_quantize(msg.data, self.ctx.seg_ids, self.ctx.seg_sizes, seed, self.levels)
+        seeds = fl.row_seeds(seed, msg.client_ids)
+        dq, wire = quant.stochastic_quantize(msg.data, self.ctx.seg_ids, self.ctx.seg_sizes, seeds, self.levels)
         msg.data.copy_(dq)
         if msg.block_mask is not None:
             frac = self._dense_wire(msg)
@@ -135,7 +136,8 @@ class StochasticQuantServerEndpoint(QuantServerEndpoint):
     def encode_broadcast(self, params, seed):
         if not self.quant_broadcast:
             return params, self.ctx.dense_bytes
-        dq, wire = quant.stochastic_quantize(params.unsqueeze(0), self.ctx.seg_ids, self.ctx.seg_sizes, seed, self.levels)
+        dq, wire = quant.stochastic_quantize(params.unsqueeze(0), self.ctx.seg_ids, self.ctx.seg_sizes,
+                                             fl.row_seeds(seed, [-1]), self.levels)
         return dq[0], wire[0]
 
 

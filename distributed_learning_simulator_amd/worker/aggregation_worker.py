@@ -50,16 +50,16 @@ class AggregationWorker(Worker):
         stats = self.trainer.train(schedule, executor=self)
         self.log_train_stats(wave, stats, len(schedule.epoch_end) - 1)
         msg = self._get_sent_data(wave, theta_g, stats)
-        return self.endpoint.send(msg, seed=self.upload_seed(round_num, wave[0]))
+        return self.endpoint.send(msg, seed=self.upload_seed(round_num))
 
     def build_schedule(self, round_num: int, wave: list[int]):
         return self.trainer.build_schedule(
             self.shards(wave), self.local_epochs(),
-            seed=self.config.seed * 100_003 + round_num * 1009 + wave[0],
+            seed=self.config.seed * 100_003 + round_num * 1009, client_ids=list(wave),
         )
 
-    def upload_seed(self, round_num: int, first_client: int) -> int:
-        return (self.config.seed * 7_368_787 + round_num * 104_729 + first_client) & 0x7FFFFFFF
+    def upload_seed(self, round_num: int) -> int:
+        return (self.config.seed * 7_368_787 + round_num * 104_729) & 0x7FFFFFFF
 
     # -------------------------------------------------------------- hooks
     def _load_result_from_server(self, theta_g: torch.Tensor, K: int) -> None:
