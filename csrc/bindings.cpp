@@ -19,21 +19,37 @@ PYBIND11_MODULE(_dls_hip, m) {
 
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
-                      int relu, int K, ptr s) {
-    ConvNTParams p{P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), P<const bf16_t>(bias), x_cs, y_cs, w_cs, b_cs,
-                   B, H, W, C, OH, OW, KH, KW, stride, pad, dil, M, N, R, rep, relu};
-    conv_nt(p, K, S(s));
+                      int relu, int K, int b_kmajor, int variant, ptr s) {
+    ConvNTParams p{};
+    p.x = P<const bf16_t>(x);
+    p.w = P<const bf16_t>(w);
+    p.y = P<bf16_t>(y);
+    p.bias = P<const bf16_t>(bias);
+    p.x_cs = x_cs; p.y_cs = y_cs; p.w_cs = w_cs; p.b_cs = b_cs;
+    p.B = B; p.H = H; p.W = W; p.C = C; p.OH = OH; p.OW = OW; p.KH = KH; p.KW = KW;
+    p.stride = stride; p.pad = pad; p.dil = dil; p.M = M; p.N = N; p.R = R; p.rep = rep; p.relu = relu;
+    p.b_kmajor = b_kmajor;
+    conv_nt(p, K, variant, S(s));
   });
+  m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
+                         int W, int Ci, int KH, int KW, int stride, int pad, int variant, ptr s) {
+    conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
+               stride, pad, variant, S(s));
+  });
+  m.def("conv_nt_num_variants", &conv_nt_num_variants);
+  m.def("conv_nt_default_variant", &conv_nt_default_variant);
   m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,
                       int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, ptr s) {
-    ConvTNParams p{P<const bf16_t>(dy), P<const bf16_t>(x), P<float>(dw), dy_cs, x_cs, dw_cs, B, H, W, C, OH, OW, KH,
-                   KW, stride, pad, M, Co, R, 1, M};
+    ConvTNParams p{};
+    p.dy = P<const bf16_t>(dy);
+    p.x = P<const bf16_t>(x);
+    p.dw = P<float>(dw);
+    p.dy_cs = dy_cs; p.x_cs = x_cs; p.dw_cs = dw_cs;
+    p.B = B; p.H = H; p.W = W; p.C = C; p.OH = OH; p.OW = OW; p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad;
+    p.M = M; p.Co = Co; p.R = R; p.splitk = 1; p.m_per_split = M;
     conv_tn(p, K, S(s));
   });
   m.def("conv_tn_splitk", &conv_tn_splitk);
-  m.def("weight_flip_transpose", [](ptr w, ptr wt, long w_cs, int K, int Co, int KH, int KW, int Ci, ptr s) {
-    weight_flip_transpose(P<const bf16_t>(w), P<bf16_t>(wt), w_cs, K, Co, KH, KW, Ci, S(s));
-  });
 
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
                      int R, int C, int relu, float eps, int rep, ptr ws, ptr s) {

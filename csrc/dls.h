@@ -6,6 +6,26 @@
 
 typedef uint16_t bf16_t;
 
+// Division by a runtime-constant divisor without the ~40-instruction integer divide:
+// q = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31 (host precomputes mul/shift).
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  f.shift = s;
+  f.mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << s) - d)) / d + 1);
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+
 struct ConvNTParams {
   const bf16_t* x;  // A source image [K][B][H][W][C]
   const bf16_t* w;  // B rows [N][R] per weight row
@@ -14,9 +34,16 @@ struct ConvNTParams {
   long x_cs, y_cs, w_cs, b_cs;
   int B, H, W, C;
   int OH, OW, KH, KW, stride, pad, dil;
+  int pad_w;  // horizontal padding (conv_nt() sets pad_w = pad for plain launches)
   int M, N, R;
   int rep;
   int relu;
+  int b_kmajor;  // 1: B read from a forward conv weight [Co=C][wKH][wKW][Ci=N] (dgrad)
+  // dgrad tap mapping (b_kmajor): loop tap kh2 ∈ [0,KH) reads weight row kh = kh_off - kh_step·kh2
+  int wKH, wKW, kh_off, kh_step, kw_off, kw_step;
+  // output row remap (sub-pixel dgrad): GEMM row (b, oh, ow) → dx pixel (oh·out_s+out_ph, ow·out_s+out_pw)
+  int out_s, out_ph, out_pw, out_H, out_W;
+  FastDiv fd_ohw, fd_ow, fd_kwc, fd_c;  // filled by conv_nt()
 };
 
 struct ConvTNParams {
@@ -27,13 +54,19 @@ struct ConvTNParams {
   int B, H, W, C, OH, OW, KH, KW, stride, pad;
   int M, Co, R;
   int splitk, m_per_split;
+  FastDiv fd_ohw, fd_ow;  // filled by conv_tn()
 };
 
-void conv_nt(const ConvNTParams& p, int K, hipStream_t s);
+// variant < 0: shape heuristic; 0..conv_nt_num_variants()-1: explicit tile config (benchmarks)
+void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s);
+int conv_nt_num_variants();
+int conv_nt_default_variant(int M, int N, int R);
+// dX of a conv (any stride): stride-1 → one flipped-weight NT GEMM; stride s > 1 → s² parity
+// classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, long w_cs, int K, int rep, int B, int OH, int OW,
+                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, hipStream_t s);
 void conv_tn(ConvTNParams p, int K, hipStream_t s);
 int conv_tn_splitk(int K, int Co, int R, int M);
-void weight_flip_transpose(const bf16_t* w, bf16_t* wt, long w_cs, int K, int Co, int KH, int KW, int Ci,
-                           hipStream_t s);
 
 // ---------------------------------------------------------------- normalisation
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,

@@ -75,6 +75,11 @@ def _workspace(numel: int, device) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- conv
+# NT-GEMM tile configuration: -1 = per-shape heuristic (csrc/conv_nt.hip); the kernel
+# microbenchmark (bench/kernel_bench.py) sets explicit variant ids to sweep them.
+nt_variant = -1
+
+
 def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
     K, B, H, W, C = x.shape
     x = x.contiguous()
@@ -91,15 +96,8 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
         b_cs, _ = _client_view(bias, K)
     M = B * OH * OW
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
-               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, _s())
+               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_variant, _s())
     return y
-
-
-def _flip_transpose(w):
-    Kw, Co, KH, KW, Ci = w.shape
-    wt = torch.empty((Kw, Ci, KH, KW, Co), dtype=BF16, device=w.device)
-    _C.weight_flip_transpose(_p(w), _p(wt), w.stride(0) if Kw > 1 else 0, Kw, Co, KH, KW, Ci, _s())
-    return wt
 
 
 def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
@@ -108,13 +106,13 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
     _check(dy, BF16, name="dy")
     Kw, Co2, KH, KW, Ci = w.shape
     assert Co2 == Co
-    wt = _flip_transpose(w)
-    rep = K // Kw
+    w_cs, rep = _client_view(w, K)
     H, W = int(in_hw[0]), int(in_hw[1])
     dx = torch.empty((K, B, H, W, Ci), dtype=BF16, device=dy.device)
-    M = B * H * W
-    _C.conv_nt(_p(dy), _p(wt), _p(dx), NULL, B * OH * OW * Co, M * Ci, wt.stride(0) if Kw > 1 else 0, 0, B, OH, OW, Co,
-               H, W, KH, KW, 1, KH - 1 - pad, stride, M, Ci, KH * KW * Co, rep, 0, K, _s())
+    # B operand read straight from the forward weight (flip + transpose in the loader);
+    # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
+    _C.conv_dgrad(_p(dy), _p(w), _p(dx), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, nt_variant,
+                  _s())
     return dx
 
 
@@ -155,7 +153,7 @@ def linear_fwd(x, w, b=None):
     b_cs = _client_view(b, K)[0] if b is not None else 0
     y = torch.empty((K, N, Fo), dtype=BF16, device=x.device)
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               0, K, _s())
+               0, K, 0, nt_variant, _s())
     return y
 
 
@@ -163,11 +161,11 @@ def linear_dgrad(dy, w):
     K, N, Fo = dy.shape
     dy = dy.contiguous()
     Kw, Fo2, Fi = w.shape
-    wt = torch.empty((Kw, Fi, Fo), dtype=BF16, device=w.device)
-    _C.weight_flip_transpose(_p(w), _p(wt), w.stride(0) if Kw > 1 else 0, Kw, Fo, 1, 1, Fi, _s())
+    w_cs, rep = _client_view(w, K)
     dx = torch.empty((K, N, Fi), dtype=BF16, device=dy.device)
-    _C.conv_nt(_p(dy), _p(wt), _p(dx), NULL, N * Fo, N * Fi, wt.stride(0) if Kw > 1 else 0, 0, 1, N, 1, Fo, N, 1, 1, 1,
-               1, 0, 1, N, Fi, Fo, K // Kw, 0, K, _s())
+    # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
+    _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
+               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_variant, _s())
     return dx
 
 

