@@ -84,15 +84,21 @@ def _hash_u32(x: torch.Tensor) -> torch.Tensor:
 class ImageDataset:
     """Class-conditional images: x = prototype[y] (low-frequency pattern) + noise(index).
 
-    Labels are a seeded balanced permutation. `gather(idx)` returns [.., H, W, C]."""
+    Labels are a seeded balanced permutation. `gather(idx)` returns [.., H, W, Cs] where
+    Cs = `channels` ≥ C: conv-first models store RGB with zero channels up to 8 so the stem's
+    im2col gathers are 16-byte vectors (exact: the padded weight channels see only zeros)."""
 
     def __init__(self, spec: DatasetSpec, split: str, seed: int, device, dtype,
-                 materialize_limit: int = 2_000_000_000, noise: float = 1.0, signal: float = 0.35):
+                 materialize_limit: int = 2_000_000_000, noise: float = 1.0, signal: float = 0.35,
+                 channels: int | None = None):
         self.spec = spec
         self.split = split
         self.device = device
         self.dtype = dtype
         self.noise = noise
+        H0, W0, C0 = spec.shape
+        self.channels = max(int(channels or C0), C0)
+        self.shape = (H0, W0, self.channels)
         n = spec.n_train if split == "train" else spec.n_test
         self.n = n
         g = torch.Generator().manual_seed(seed * 1000003 + (0 if split == "train" else 1))
@@ -104,7 +110,7 @@ class ImageDataset:
         # weak class signal under unit noise: learnable, but not in a single step
         self.prototypes = (proto * signal).permute(0, 2, 3, 1).contiguous()  # [classes, H, W, C]
         self.salt = seed * 2654435761 + (0 if split == "train" else 97)
-        self.materialized = n * H * W * C <= materialize_limit
+        self.materialized = n * H * W * self.channels <= materialize_limit
         self.labels_dev = self.labels.to(device)
         self.proto_dev = self.prototypes.to(device, dtype)
         if self.materialized:
@@ -129,7 +135,10 @@ class ImageDataset:
         noise = u * math.sqrt(6.0) * self.noise
         lab = self.labels[idx.cpu()].long() if device.type == "cpu" else self.labels_dev[idx].long()
         proto = (self.prototypes if device.type == "cpu" else self.proto_dev.float())[lab]
-        return (proto + noise.view(-1, H, W, C)).to(dtype)
+        img = (proto + noise.view(-1, H, W, C)).to(dtype)
+        if self.channels > C:
+            img = torch.nn.functional.pad(img, (0, self.channels - C))
+        return img
 
     def gather(self, idx: torch.Tensor) -> torch.Tensor:
         """idx: any-shape int tensor on device -> [*idx.shape, H, W, C]."""
@@ -140,11 +149,11 @@ class ImageDataset:
             if backend.using_hip(self.data) and self.data[0].numel() % 8 == 0:
                 from ..ops import hip
 
-                return hip.gather_rows(self.data, idx).reshape(*idx.shape, *self.spec.shape)
+                return hip.gather_rows(self.data, idx).reshape(*idx.shape, *self.shape)
             out = self.data.index_select(0, flat)
         else:
             out = self._generate(flat, self.device, self.dtype)
-        return out.reshape(*idx.shape, *self.spec.shape)
+        return out.reshape(*idx.shape, *self.shape)
 
     def gather_labels(self, idx: torch.Tensor) -> torch.Tensor:
         return self.labels_dev.index_select(0, idx.reshape(-1).long()).reshape(idx.shape)
@@ -197,14 +206,17 @@ class DatasetCollection:
 
 
 def create_dataset_collection(name: str, dataset_kwargs: dict | None, seed: int, device,
-                              dtype=torch.float32) -> DatasetCollection:
+                              dtype=torch.float32, image_channels: int | None = None) -> DatasetCollection:
+    """`image_channels`: stored channel count for image sets (≥ the dataset's; zero-padded)."""
     spec = get_spec(name, dataset_kwargs)
     kw = dict(dataset_kwargs or {})
     if spec.kind == "image":
         noise = float(kw.get("noise", 1.0))
         signal = float(kw.get("signal", 0.35))
-        return DatasetCollection(spec, ImageDataset(spec, "train", seed, device, dtype, noise=noise, signal=signal),
-                                 ImageDataset(spec, "test", seed, device, dtype, noise=noise, signal=signal))
+        return DatasetCollection(spec, ImageDataset(spec, "train", seed, device, dtype, noise=noise, signal=signal,
+                                                    channels=image_channels),
+                                 ImageDataset(spec, "test", seed, device, dtype, noise=noise, signal=signal,
+                                              channels=image_channels))
     if spec.kind == "text":
         return DatasetCollection(spec, TextDataset(spec, "train", seed, device), TextDataset(spec, "test", seed, device))
     if spec.kind == "graph":

@@ -374,6 +374,18 @@ def count_params(model: CohortModel) -> int:
     return model.layout.num_params
 
 
+def stored_image_channels(name: str, dataset_spec) -> int | None:
+    """Channel count image data should be stored with for this model: conv-stem ResNet/DenseNet
+    consume RGB zero-padded to 8 channels (16-byte im2col gathers, exact); others the raw C."""
+    if dataset_spec.kind != "image":
+        return None
+    C = dataset_spec.shape[2]
+    n = name.lower().replace("_", "")
+    if (n.startswith("resnet") or n.startswith("densenet")) and C % 8:
+        return (C + 7) // 8 * 8
+    return C
+
+
 def build_model(name: str, dataset_spec, model_kwargs: dict | None = None) -> CohortModel:
     kw = dict(model_kwargs or {})
     n = name.lower().replace("_", "")

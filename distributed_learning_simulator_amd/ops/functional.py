@@ -21,12 +21,19 @@ def _be(t):
 
 # --------------------------------------------------------------------------- conv2d
 class _Conv(torch.autograd.Function):
+    """Conv2d over the client dim. If the input carries more channels than the weight (image
+    data stored zero-padded to 8 channels), the weight is zero-padded to match and only the
+    real channels' gradient is written back."""
+
     @staticmethod
     def forward(ctx, x, token, w, gw, stride, pad, b, gb):
         be = _be(x)
+        ci = w.shape[-1]
+        if x.shape[-1] > ci:
+            w = torch.nn.functional.pad(w, (0, x.shape[-1] - ci))
         y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.save_for_backward(x, w)
-        ctx.gw, ctx.gb, ctx.stride, ctx.pad = gw, gb, stride, pad
+        ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         return y
 
     @staticmethod
@@ -37,15 +44,22 @@ class _Conv(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad)
+            if dx.shape[-1] > ctx.ci:
+                dx = dx[..., : ctx.ci]
         if ctx.gw is not None:
+            padded = w.shape[-1] > ctx.ci
+            K = x.shape[0]
+            gw = torch.empty((K,) + tuple(w.shape[1:]), dtype=torch.float32, device=dy.device) if padded else ctx.gw
             if be is ref:
-                ctx.gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (x.shape[0],) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
+                gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (K,) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
                 if ctx.gb is not None:
                     ctx.gb.copy_(dy.float().sum(dim=(1, 2, 3)))
             else:
-                be.conv_wgrad(dy, x, ctx.gw, ctx.stride, ctx.pad)
+                be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad)
                 if ctx.gb is not None:
                     be.bias_grad(dy, ctx.gb)
+            if padded:
+                ctx.gw.copy_(gw[..., : ctx.ci])
         return dx, None, None, None, None, None, None, None
 
 

@@ -25,10 +25,10 @@ import time
 
 import torch
 
-from .data.datasets import create_dataset_collection
+from .data.datasets import create_dataset_collection, get_spec
 from .engine.trainer import CohortTrainer, HyperParameter
 from .method import CentralizedAlgorithmFactory
-from .models.zoo import build_model
+from .models.zoo import build_model, stored_image_channels
 from .parallel.comm import Comm, get_comm, init_distributed
 from .practitioner import create_practitioners
 from .utils.logging import get_logger
@@ -54,8 +54,10 @@ class Session:
         self.is_main = self.comm.rank == 0
         self.compute_dtype = resolve_dtype(cfg, self.device)
         torch.manual_seed(cfg.seed)
+        spec = get_spec(cfg.dataset_name, cfg.dataset_kwargs)
         self.dc = create_dataset_collection(cfg.dataset_name, cfg.dataset_kwargs, cfg.seed, self.device,
-                                            self.compute_dtype)
+                                            self.compute_dtype,
+                                            image_channels=stored_image_channels(cfg.model_name, spec))
         if practitioners is None:
             labels = self.dc.train.labels  # (graph: labels of the training nodes)
             practitioners = create_practitioners(cfg, labels)

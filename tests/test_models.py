@@ -89,3 +89,21 @@ def test_grad_matches_torch_autograd_lenet():
     got = layout.unflatten(grad[0])
     for k, v in t.items():
         torch.testing.assert_close(got[k], v.grad, rtol=1e-4, atol=1e-6)
+
+
+def test_zero_padded_input_channels_are_exact():
+    """RGB stored zero-padded to 8 channels (conv-first models, 16-byte stem gathers) gives the
+    same loss and weight gradients as the raw 3-channel input."""
+    from distributed_learning_simulator_amd.models.zoo import stored_image_channels
+
+    spec = get_spec("CIFAR10")
+    assert stored_image_channels("ResNet18", spec) == 8
+    assert stored_image_channels("LeNet5", get_spec("MNIST")) == 1
+    model = build_model("ResNet18", spec)
+    theta = model.layout.init_flat(torch.Generator().manual_seed(3))[None].clone()
+    x = torch.randn(1, 2, 32, 32, 3)
+    y = torch.randint(0, 10, (1, 2))
+    loss3, grad3 = _run(model, x, y, 1, theta.clone())
+    loss8, grad8 = _run(model, torch.nn.functional.pad(x, (0, 5)), y, 1, theta.clone())
+    torch.testing.assert_close(loss8, loss3, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(grad8, grad3, rtol=1e-4, atol=1e-6)
