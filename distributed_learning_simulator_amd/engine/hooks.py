@@ -21,6 +21,7 @@ class ExecutorHookPoint(Enum):
     AFTER_BATCH = auto()
     AFTER_EPOCH = auto()
     AFTER_EXECUTE = auto()
+    AFTER_LOAD_MODEL = auto()  # kwargs `theta` ([K,P] rows just loaded); analysis.module_diff
 
 
 class StopExecutingException(Exception):

@@ -114,12 +114,16 @@ class CohortTrainer:
         """Every resident client row k < K starts from θ_g (M1/M5 receive + load)."""
         shadow = self.buffers.shadow[:K] if self.buffers.shadow is not None else None
         fl.broadcast_rows(self.buffers.theta[:K], theta_g.to(self.device), shadow)
+        if self.hooks.has_hook(ExecutorHookPoint.AFTER_LOAD_MODEL):
+            self.hooks.exec(ExecutorHookPoint.AFTER_LOAD_MODEL, theta=self.buffers.theta[:K])
 
     def load_rows(self, theta_rows: torch.Tensor) -> None:
         K = theta_rows.shape[0]
         self.buffers.theta[:K].copy_(theta_rows)
         if self.buffers.shadow is not None:
             self.buffers.shadow[:K].copy_(theta_rows)
+        if self.hooks.has_hook(ExecutorHookPoint.AFTER_LOAD_MODEL):
+            self.hooks.exec(ExecutorHookPoint.AFTER_LOAD_MODEL, theta=self.buffers.theta[:K])
 
     def reset_optimizer(self, K: int) -> None:
         self.buffers.state1[:K].zero_()

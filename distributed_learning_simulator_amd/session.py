@@ -18,6 +18,7 @@ ranks → finalize → next round's broadcast is already resident. Metrics per r
 from __future__ import annotations
 
 import copy
+import dataclasses
 import json
 import math
 import os
@@ -135,6 +136,9 @@ class Session:
         get_logger().info("training use %s seconds", total)
         if self.is_main:
             os.makedirs(cfg.save_dir, exist_ok=True)
+            # reference dumps config.pkl (`server/server.py:57-60`); JSON here (analysis.session)
+            with open(os.path.join(cfg.save_dir, "config.json"), "wt", encoding="utf8") as f:
+                json.dump(dataclasses.asdict(cfg), f, default=str, indent=1)
             with open(os.path.join(cfg.save_dir, "metrics.jsonl"), "wt", encoding="utf8") as f:
                 for m in self.metrics:
                     f.write(json.dumps(m) + "\n")
