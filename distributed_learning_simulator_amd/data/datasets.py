@@ -199,10 +199,27 @@ class DatasetCollection:
     train: object
     test: object
     graph: object = None
+    # Validation phase carved out of the test split (`split_validation`); None = whole test set
+    test_indices: torch.Tensor | None = None
+    validation_indices: torch.Tensor | None = None
 
     @property
     def name(self):
         return self.spec.name
+
+    def split_validation(self, seed: int) -> None:
+        """Give the collection a Validation phase: a seeded half of the test split becomes
+        validation (dealt to clients for keep-best-model selection), the other half stays the
+        server's test set. Parity unpinned: the reference's external toolbox owns this split."""
+        if self.graph is not None or self.validation_indices is not None:
+            return
+        n = self.test.n
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(seed * 31 + 7))
+        self.validation_indices = perm[: n // 2].sort().values
+        self.test_indices = perm[n // 2 :].sort().values
+
+    def validation_labels(self) -> torch.Tensor:
+        return self.test.labels[self.validation_indices]
 
 
 def create_dataset_collection(name: str, dataset_kwargs: dict | None, seed: int, device,

@@ -192,6 +192,37 @@ class CohortTrainer:
         loss, correct = Fn.cross_entropy(logits, labels, valid)
         return loss, correct
 
+    @torch.no_grad()
+    def evaluate_clients(self, K: int, shards: list[torch.Tensor], dataset=None,
+                         batch_size: int | None = None) -> torch.Tensor:
+        """Accuracy of each resident client's CURRENT model (row k) on its own index shard of
+        `dataset` (default: the test split, where the Validation phase lives) — one batched
+        forward per batch position, client = leading dim, ragged shards via valid counts."""
+        ds = dataset or self.dc.test
+        B = batch_size or self.hyper.batch_size
+        sizes = [int(s.numel()) for s in shards]
+        nmax = max(sizes) if sizes else 0
+        correct = torch.zeros(K, dtype=torch.float32, device=self.device)
+        if nmax == 0:
+            return correct
+        idx = torch.zeros(K, nmax, dtype=torch.long)
+        for k, s in enumerate(shards):
+            if s.numel():
+                idx[k, : s.numel()] = s
+                idx[k, s.numel():] = s[0]
+        idx = idx.to(self.device)
+        size_t = torch.tensor(sizes, dtype=torch.int32, device=self.device)
+        params = BoundParams(self.layout, self.buffers.compute[:K], None, K=K)
+        for b0 in range(0, nmax, B):
+            b1 = min(nmax, b0 + B)
+            valid = (size_t - b0).clamp(0, b1 - b0).to(torch.int32)
+            x = ds.gather(idx[:, b0:b1])
+            y = ds.gather_labels(idx[:, b0:b1])
+            ctx = RunCtx(params, valid, training=False)
+            _, c = Fn.cross_entropy(self.model.forward(x, ctx), y, valid)
+            correct += c
+        return correct / size_t.clamp(min=1).float()
+
     def _gather(self, ds, idx):
         if self.model.input_kind == "graph":
             return self.graph.batch(idx)
@@ -248,22 +279,30 @@ class CohortTrainer:
     # ------------------------------------------------------------------ evaluate
     @torch.no_grad()
     def evaluate(self, theta_rows: torch.Tensor, dataset=None, batch_size: int | None = None,
-                 max_images: int = 8192, shard: tuple[int, int] = (0, 1)):
-        """Evaluate M models (theta_rows [M,P] fp32 or [P]) on `dataset` (default Test).
+                 max_images: int = 8192, shard: tuple[int, int] = (0, 1), indices: torch.Tensor | None = None):
+        """Evaluate M models (theta_rows [M,P] fp32 or [P]) on `dataset` (default: the Test
+        phase — `dc.test_indices` of the test split when a validation half was carved out).
         BN uses batch statistics of each eval batch (reference: running stats disabled).
         The test set is cut into batches; each batch is a virtual client, so one launch
         covers many batches (and many models). `shard=(rank, world)` evaluates only this
         rank's share of the batches. Returns (loss_sum [M], correct [M], n_total)."""
         if theta_rows.dim() == 1:
             theta_rows = theta_rows.unsqueeze(0)
-        ds = dataset or self.dc.test
+        if dataset is None:
+            ds = self.dc.test
+            if indices is None:
+                indices = self.dc.test_indices
+        else:
+            ds = dataset
         if self.model.input_kind == "graph":
             return self.graph.evaluate(self, theta_rows, shard)
         M = theta_rows.shape[0]
         B = batch_size or self.hyper.batch_size
-        n = ds.n
+        n = ds.n if indices is None else int(indices.numel())
         nb = (n + B - 1) // B
         flat = torch.arange(nb * B, device=self.device) % n
+        if indices is not None:
+            flat = indices.to(self.device)[flat]
         idx = flat.view(nb, B)
         counts = torch.full((nb,), B, dtype=torch.int32, device=self.device)
         counts[-1] = n - (nb - 1) * B

@@ -53,6 +53,7 @@ class FedOBDWorker(AggregationWorker):
         if self.phase == Phase.STAGE_ONE and last is not None and last.other_data.get("phase_two"):
             get_logger().warning("switch to phase 2")
             self.phase = Phase.STAGE_TWO
+            self.disable_choose_model_by_validation()  # reference fed_obd/worker.py:35
         if self.phase == Phase.STAGE_TWO:
             self._stage2_epoch += 1
         yield from super().run_round(round_num, theta_g, client_ids)

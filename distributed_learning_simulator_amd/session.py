@@ -32,6 +32,7 @@ from .method import CentralizedAlgorithmFactory
 from .models.zoo import build_model, stored_image_channels
 from .parallel.comm import Comm, get_comm, init_distributed
 from .practitioner import create_practitioners
+from .sampler import get_partition
 from .utils.logging import get_logger
 
 
@@ -68,6 +69,14 @@ class Session:
             for wid, p in enumerate(practitioners):
                 p.set_worker_id(wid)
             cfg.worker_number = len(practitioners)
+        if cfg.dataset_sampling == "iid" and self.dc.graph is None:
+            # Validation phase for keep-best-model selection (reference aggregation_worker.py:28-35)
+            self.dc.split_validation(cfg.seed)
+            vparts = get_partition("iid", self.dc.validation_labels(), len(practitioners), seed=cfg.seed + 1)
+            key = self.dc.spec.name + "/validation"
+            for p, part in zip(practitioners, vparts):
+                if not p.has_dataset(key):
+                    p.set_sampler(key, self.dc.validation_indices[part])
         self.practitioners = {p.worker_id: p for p in practitioners}
         self.model = build_model(cfg.model_name, self.dc.spec, cfg.model_kwargs)
         self.layout = self.model.layout

@@ -19,6 +19,7 @@ from typing import Iterator
 
 import torch
 
+from ..engine.hooks import ExecutorHookPoint
 from ..message import CohortMessage
 from ..ops import fl
 from .worker import Worker
@@ -31,6 +32,44 @@ class AggregationWorker(Worker):
         self._reuse_learning_rate = False
         self._keep_optimizer_state = False
         self._epochs = config.epoch
+        # IID sampling ⇒ upload the best-validation model of the round (reference
+        # `aggregation_worker.py:28-29,60-67,82-86`, KeepModelHook(keep_best_model=True))
+        self._choose_model_by_validation = False
+        self._best_theta: torch.Tensor | None = None
+        self._best_acc: torch.Tensor | None = None
+        if session is not None and config.dataset_sampling == "iid" and session.dc.validation_indices is not None:
+            self.enable_choose_model_by_validation()
+
+    # ------------------------------------------------- keep best by validation
+    def enable_choose_model_by_validation(self) -> None:
+        self._choose_model_by_validation = True
+
+    def disable_choose_model_by_validation(self) -> None:
+        self._choose_model_by_validation = False
+        self._best_theta = None
+        self._best_acc = None
+
+    def _validation_shards(self, wave: list[int]) -> list[torch.Tensor]:
+        key = self.session.dc.spec.name + "/validation"
+        return [self.session.practitioners[c].indices(key) for c in wave]
+
+    def _keep_best_hook(self, wave: list[int]):
+        K = len(wave)
+        shards = self._validation_shards(wave)
+        P = self.trainer.buffers.theta.shape[1]
+        if self._best_theta is None or self._best_theta.shape[0] < K:
+            self._best_theta = torch.empty((self.trainer.capacity, P), dtype=torch.float32,
+                                           device=self.trainer.buffers.theta.device)
+        self._best_acc = torch.full((K,), -1.0, device=self._best_theta.device)
+
+        def after_epoch(**_):
+            acc = self.trainer.evaluate_clients(K, shards)
+            better = acc > self._best_acc
+            self._best_acc = torch.where(better, acc, self._best_acc)
+            theta = self.trainer.buffers.theta[:K]
+            self._best_theta[:K].copy_(torch.where(better[:, None], theta, self._best_theta[:K]))
+
+        return after_epoch
 
     # ------------------------------------------------------------ round driver
     def local_epochs(self) -> int:
@@ -47,7 +86,13 @@ class AggregationWorker(Worker):
         K = len(wave)
         self._load_result_from_server(theta_g, K)
         schedule = self.build_schedule(round_num, wave)
-        stats = self.trainer.train(schedule, executor=self)
+        if self._choose_model_by_validation:
+            self.trainer.hooks.append_named_hook(ExecutorHookPoint.AFTER_EPOCH, "keep_model_hook",
+                                                 self._keep_best_hook(wave))
+        try:
+            stats = self.trainer.train(schedule, executor=self)
+        finally:
+            self.trainer.hooks.remove_named_hook("keep_model_hook")
         self.log_train_stats(wave, stats, len(schedule.epoch_end) - 1)
         msg = self._get_sent_data(wave, theta_g, stats)
         return self.endpoint.send(msg, seed=self.upload_seed(round_num))
@@ -72,6 +117,8 @@ class AggregationWorker(Worker):
     def _get_sent_data(self, wave: list[int], theta_g: torch.Tensor, stats) -> CohortMessage:
         K = len(wave)
         rows = self.trainer.buffers.theta[:K]
+        if self._choose_model_by_validation and self._best_acc is not None:
+            rows.copy_(self._best_theta[:K])  # "use best model"
         if self._send_parameter_diff:
             data = fl.delta_rows(rows, theta_g, out=rows)
             kind = "delta"

@@ -144,3 +144,42 @@ def test_sign_sgd_bytes(tmp_path):
     P = sess.layout.num_params
     steps = (sess.practitioners[0].dataset_size(sess.dc.spec.name) + 63) // 64
     assert result["metrics"][0]["comm_bytes_up"] == 3 * steps * ((P + 7) // 8)
+
+
+def test_iid_keeps_best_validation_model(tmp_path, monkeypatch):
+    """IID sampling ⇒ each client uploads its best-validation-accuracy model of the round
+    (reference aggregation_worker.py:28-29,82-86), not the last epoch's."""
+    group = "fed_avg"
+    args = ["--config-name", "fed_avg/mnist.yaml", f"++{group}.round=1", f"++{group}.epoch=2",
+            f"++{group}.worker_number=2", f"++{group}.dataset_kwargs.scale=0.04", f"++{group}.save_dir={tmp_path}",
+            f"++{group}.log_level=WARNING"]
+    cfg = load_config(args)
+    assert cfg.dataset_sampling == "iid"
+    sess = Session(cfg, comm=Comm())
+    assert sess.dc.validation_indices is not None
+    assert sess.worker._choose_model_by_validation
+    key = sess.dc.spec.name + "/validation"
+    val = [sess.practitioners[c].indices(key) for c in range(2)]
+    assert all(v.numel() > 0 for v in val) and not set(val[0].tolist()) & set(val[1].tolist())
+    assert not set(sess.dc.validation_indices.tolist()) & set(sess.dc.test_indices.tolist())
+    snaps = []
+    accs = iter([torch.tensor([0.5, 0.2]), torch.tensor([0.3, 0.4])])  # client 0 best @1, client 1 @2
+
+    def fake_eval(K, shards, dataset=None, batch_size=None):
+        snaps.append(sess.trainer.buffers.theta[:K].clone())
+        return next(accs)
+
+    monkeypatch.setattr(sess.trainer, "evaluate_clients", fake_eval)
+    sent = []
+    orig = sess.worker._get_sent_data
+
+    def spy(wave, theta_g, stats):
+        msg = orig(wave, theta_g, stats)
+        sent.append(msg.data.clone() + theta_g)
+        return msg
+
+    monkeypatch.setattr(sess.worker, "_get_sent_data", spy)
+    sess.run()
+    assert len(snaps) == 2
+    torch.testing.assert_close(sent[0][0], snaps[0][0])
+    torch.testing.assert_close(sent[0][1], snaps[1][1])
