@@ -1,0 +1,76 @@
+"""Static memory planner: how many clients a rank keeps resident at once (the cohort).
+
+Reference `executor.py:69-93` / `training.py:103` pack executors onto GPUs dynamically: the
+first executor in a process takes a cross-process lock, picks the GPU with enough free memory
+for its previous peak and releases the lock after the first batch. With all
+of a rank's clients advancing together, the equivalent decision is made once, up front:
+
+  per_client = optimizer/parameter state (θ, grad, momentum[, Adam v], bf16 shadow: P_pad each)
+             + activation peak of one client's training step (measured by a probe step)
+  capacity   = min(clients this rank hosts, ⌊budget / per_client⌋),  budget = fraction × free HBM
+
+Clients beyond the capacity are trained in successive waves through the same buffers.
+On MI355X (288 GB HBM3E) a ResNet-18/CIFAR client costs ≈0.2 GB, so 100 clients fit in one
+wave; ResNet-50/ImageNet at batch 128 costs ≈20 GB of activations and runs in waves.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..utils.logging import get_logger
+
+
+def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
+    P = layout.padded_size
+    n = 3 * 4 * P  # theta, grad, state1
+    if optimizer.lower() == "adam":
+        n += 4 * P
+    if compute_dtype != torch.float32:
+        n += torch.tensor([], dtype=compute_dtype).element_size() * P
+    return n
+
+
+def probe_activation_bytes(model, dc, hyper, device, compute_dtype) -> int:
+    """Peak extra device memory of ONE client's forward+backward at the configured batch
+    size (a real step through the cohort trainer with capacity 1)."""
+    from .trainer import CohortTrainer
+
+    if device.type != "cuda":
+        return 0
+    torch.cuda.synchronize(device)
+    trainer = CohortTrainer(model, dc, hyper, device, compute_dtype, 1)
+    base = torch.cuda.memory_allocated(device)
+    torch.cuda.reset_peak_memory_stats(device)
+    B = hyper.batch_size
+    n = dc.train.n if hasattr(dc.train, "n") else B
+    idx = (torch.arange(B, device=device) % max(n, 1)).view(1, B)
+    x = trainer._gather(dc.train, idx)
+    y = dc.train.gather_labels(idx)
+    valid = torch.full((1,), B, dtype=torch.int32, device=device)
+    loss, _ = trainer.forward_loss(1, x, y, valid)
+    loss.sum().backward()
+    torch.cuda.synchronize(device)
+    peak = torch.cuda.max_memory_allocated(device) - base
+    del trainer, x, y, loss
+    torch.cuda.empty_cache()
+    return int(peak)
+
+
+def plan_capacity(wanted: int, layout, model, dc, hyper, device, compute_dtype,
+                  fraction: float = 0.80, explicit: int = 0) -> int:
+    """Cohort size for this rank. `explicit` > 0 (config `cohort_size`) wins."""
+    if explicit:
+        return max(1, min(wanted, explicit))
+    if device.type != "cuda" or wanted <= 1:
+        return max(1, wanted)
+    state = state_bytes_per_client(layout, compute_dtype, hyper.optimizer_name)
+    act = probe_activation_bytes(model, dc, hyper, device, compute_dtype)
+    per_client = state + int(act * 1.15)  # allocator slack
+    free, _total = torch.cuda.mem_get_info(device)
+    cap = max(1, min(wanted, int(math.floor(fraction * free / max(per_client, 1)))))
+    get_logger().info("memory plan: %.1f MiB state + %.1f MiB activations per client, %.1f GiB free "
+                      "-> %d of %d clients resident per wave", state / 2**20, act / 2**20, free / 2**30, cap, wanted)
+    return cap

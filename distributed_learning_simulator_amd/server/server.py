@@ -15,25 +15,20 @@ import random
 
 import torch
 
+from ..executor import Executor
 from ..utils.logging import get_logger
 
 
-class Server:
+class Server(Executor):
     def __init__(self, config, endpoint, algorithm=None, session=None, **kwargs):
-        self.config = config
+        super().__init__(config, "server", session)
         self.endpoint = endpoint
-        self.session = session
         self._algorithm = algorithm
         self.worker_number = config.worker_number
-        self.name = "server"
 
     @property
     def algorithm(self):
         return self._algorithm
-
-    @property
-    def save_dir(self) -> str:
-        return os.path.join(self.config.save_dir, "server")
 
     # reference server.py:123-131
     def _select_workers(self) -> list[int]:

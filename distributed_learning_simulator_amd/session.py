@@ -27,6 +27,7 @@ import time
 import torch
 
 from .data.datasets import create_dataset_collection, get_spec
+from .engine.memory import plan_capacity
 from .engine.trainer import CohortTrainer, HyperParameter
 from .method import CentralizedAlgorithmFactory
 from .models.zoo import build_model, stored_image_channels
@@ -83,12 +84,14 @@ class Session:
         n_sel = int(cfg.algorithm_kwargs.get("random_client_number", cfg.worker_number) or cfg.worker_number)
         n_sel = min(n_sel, cfg.worker_number)
         per_rank = math.ceil(n_sel / self.comm.world)
-        capacity = max(1, min(per_rank, cfg.cohort_size) if cfg.cohort_size else per_rank)
-        if self.dc.spec.kind == "graph":
-            capacity = per_rank  # halo exchange needs every client of the rank resident at once
         if not cfg.optimizer_name:
             cfg.optimizer_name = "Adam" if self.dc.spec.kind == "graph" else "SGD"
         self.hyper = HyperParameter.from_config(cfg)
+        if self.dc.spec.kind == "graph":
+            capacity = per_rank  # halo exchange needs every client of the rank resident at once
+        else:
+            capacity = plan_capacity(per_rank, self.layout, self.model, self.dc, self.hyper, self.device,
+                                     self.compute_dtype, explicit=cfg.cohort_size)
         self.trainer = CohortTrainer(self.model, self.dc, self.hyper, self.device, self.compute_dtype, capacity)
         algo = cfg.distributed_algorithm
         self.server = CentralizedAlgorithmFactory.create_server(

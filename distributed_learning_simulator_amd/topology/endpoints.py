@@ -46,6 +46,8 @@ class ClientEndpoint:
         self.ctx = _Ctx(layout, device, seed)
 
     def _dense_wire(self, msg: CohortMessage) -> list[int]:
+        if "wire_bytes" in msg.extra:  # sender-side sparse encodings (error feedback top-k)
+            return list(msg.extra["wire_bytes"])
         if msg.block_mask is not None:
             sizes = msg.extra["block_param_sizes"]  # [nblocks] logical elements
             sel = (msg.block_mask.float() * sizes.float()[None, :]).sum(1)

@@ -1,0 +1,158 @@
+"""Synchronous per-optimizer-step gradient exchange (true data-parallel SGD across clients).
+
+Reference `worker/gradient_worker.py:13-131`: the worker replaces the optimizer step
+(OPTIMIZER_STEP hook), flattens its gradient (+ weight decay, `compute_gradient` `:13-26`),
+passes it through `_process_gradient` (identity; the override point for compressed
+schemes), sends `{dataset_size, gradient}`, receives the server's aggregated gradient and
+applies momentum/dampening/nesterov SGD itself (`:50-116`); per-epoch loss/accuracy go to
+`epoch_stat.json` (`:118-131`). The reference registers no server for it.
+
+Cohort form: every client of the job holds the SAME model (one shared parameter row), so a
+step is
+  for each wave of resident clients: forward/backward with the shared row, per-client
+      gradient rows g_k (+ wd·θ) → `_accumulate` into a step accumulator
+  one all-reduce of the accumulator over ranks (RCCL) → `_finalize` → aggregated gradient
+  fused SGD on the shared row (momentum state lives with the row).
+Default aggregation = dataset-size-weighted mean of the active clients' gradients (fp32 on
+the wire, P·4 B per client each way); `method.sign_sgd` overrides the three hooks with the
+1-bit pack / int32 majority vote.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import torch
+
+from ..engine.trainer import TrainStats
+from ..message import FlatParameterMessage
+from ..ops import fl
+from ..server.aggregation_server import AggregationServer
+from .aggregation_worker import AggregationWorker
+
+
+class GradientWorker(AggregationWorker):
+    def __init__(self, config, endpoint, session=None, **kwargs):
+        super().__init__(config, endpoint, session, **kwargs)
+        self.disable_choose_model_by_validation()
+        self.epoch_stat: dict = {}
+        opt = (session.trainer.hyper.optimizer_name if session is not None else config.optimizer_name) or "SGD"
+        assert opt.lower() == "sgd", "GradientWorker applies SGD itself (reference gradient_worker.py:32)"
+
+    # ------------------------------------------------------ aggregation hooks
+    def _new_accumulator(self, P: int, device) -> dict:
+        return {"sum": torch.zeros(P, dtype=torch.float32, device=device),
+                "weight": torch.zeros(1, dtype=torch.float32, device=device)}
+
+    def _process_gradient(self, g: torch.Tensor) -> torch.Tensor:
+        """Override point (reference `_process_gradient`): g [K,P] fp32 → wire payload."""
+        return g
+
+    def _accumulate(self, acc: dict, payload: torch.Tensor, active: torch.Tensor, weight: torch.Tensor) -> None:
+        w = weight * active.float()
+        acc["sum"] += fl.weighted_sum(payload, w)
+        acc["weight"] += w.sum()
+
+    def _reduce(self, acc: dict) -> None:
+        self.session.comm.all_reduce_many_([acc["sum"], acc["weight"]])
+
+    def _finalize(self, acc: dict) -> torch.Tensor:
+        return (acc["sum"] / acc["weight"].clamp(min=1e-12)).unsqueeze(0)
+
+    def _wire_bytes_per_client(self) -> int:
+        return self.trainer.layout.num_params * 4
+
+    # ----------------------------------------------------------------- round
+    def train_round_sync(self, round_num: int, theta_g: torch.Tensor, clients: list[int], on_epoch=None):
+        """All clients of the job train one round of `epoch` epochs with a gradient exchange
+        after every step. Returns (final θ, bytes up, bytes down)."""
+        tr = self.trainer
+        sess = self.session
+        P = tr.layout.padded_size
+        b = tr.buffers
+        tr.load_global(theta_g, 1)
+        tr.reset_optimizer(1)
+        local = sess.local_clients(clients)
+        cap = tr.capacity
+        name = sess.dc.spec.name
+        # every rank runs the same number of steps: schedule over the GLOBAL max shard
+        all_sizes = [sess.practitioners[c].dataset_size(name) for c in clients]
+        B = tr.hyper.batch_size
+        steps_per_epoch = max(1, max((n + B - 1) // B for n in all_sizes))
+        shards = self.shards(local) if local else []
+        sizes = self.dataset_sizes(local).to(tr.device) if local else None
+        sched = tr.build_schedule(shards, self.local_epochs(), seed=self.config.seed * 100_003 + round_num,
+                                  min_steps_per_epoch=steps_per_epoch, client_ids=local) if local else None
+        epochs = self.local_epochs()
+        S = steps_per_epoch * epochs
+        stats = TrainStats(epochs, max(len(local), 1), tr.device)
+        up = down = 0
+        wd = tr.hyper.weight_decay
+        theta0 = b.theta[:1]
+        nbytes = self._wire_bytes_per_client()
+        e = 0
+        for s in range(S):
+            acc = self._new_accumulator(P, tr.device)
+            if sched is not None and s < sched.steps:
+                for w0 in range(0, len(local), cap):
+                    w1 = min(len(local), w0 + cap)
+                    K = w1 - w0
+                    idx = sched.idx[s, w0:w1]
+                    valid = sched.counts[s, w0:w1]
+                    x = tr._gather(sess.dc.train, idx)
+                    y = sess.dc.train.gather_labels(idx)
+                    loss, correct = tr.forward_loss(K, x, y, valid, shared=True)
+                    loss.sum().backward()
+                    with torch.no_grad():
+                        g = b.grad[:K]
+                        if wd:  # compute_gradient (`gradient_worker.py:13-26`)
+                            g.add_(theta0, alpha=wd)
+                        self._accumulate(acc, self._process_gradient(g), sched.active[s, w0:w1], sizes[w0:w1])
+                        vf = valid.float()
+                        ee = min(e, epochs - 1)
+                        stats.loss_sum[ee, w0:w1] += loss.detach() * vf
+                        stats.correct[ee, w0:w1] += correct
+                        stats.samples[ee, w0:w1] += vf
+            self._reduce(acc)
+            with torch.no_grad():
+                grad = self._finalize(acc)
+                lr = torch.full((1,), tr.hyper.lr_at_epoch(e, epochs), device=tr.device)
+                one = torch.ones(1, dtype=torch.bool, device=tr.device)
+                first = torch.tensor([s == 0], device=tr.device)
+                fl.sgd_step(theta0, grad, b.state1[:1], lr, one, first, 0.0, tr.hyper.momentum,
+                            tr.hyper.dampening, tr.hyper.nesterov, b.shadow[:1] if b.shadow is not None else None)
+            up += len(clients) * nbytes  # every client sends its gradient each step (M9)
+            down += len(clients) * nbytes  # and receives the aggregate (M10)
+            if (s + 1) % steps_per_epoch == 0:
+                if on_epoch is not None:
+                    on_epoch(e, stats)
+                e += 1
+        self.last_stats = stats
+        return b.theta[0].clone(), up, down
+
+
+class GradientServer(AggregationServer):
+    """Drives synchronous-gradient rounds (the per-step exchange is an all-reduce inside
+    `GradientWorker.train_round_sync`); records `epoch_stat.json` like the reference worker."""
+
+    def run_rounds(self, session, theta_recv):
+        worker = session.worker
+        while not self._stopped():
+            r = self.round_number
+            t0 = time.perf_counter()
+            selected = list(self.selected)
+
+            def on_epoch(e, stats):
+                loss, acc = stats.epoch_metrics(e)
+                worker.epoch_stat[e + 1] = {"loss": float(loss.mean()), "accuracy": float(acc.mean())}
+
+            theta, up, down = worker.train_round_sync(r, theta_recv, selected, on_epoch)
+            result = FlatParameterMessage(parameter=theta, layout=session.layout)
+            theta_recv, _ = self.send_result(result)
+            session.record_round(r, t0, selected, up, down)
+        if session.is_main:
+            os.makedirs(worker.save_dir, exist_ok=True)
+            with open(os.path.join(worker.save_dir, "epoch_stat.json"), "wt", encoding="utf8") as f:
+                json.dump(worker.epoch_stat, f)

@@ -14,17 +14,16 @@ import os
 
 import torch
 
+from ..executor import Executor
 from ..utils.logging import get_logger
 
 
-class Worker:
+class Worker(Executor):
     def __init__(self, config, endpoint, session=None, **kwargs):
-        self.config = config
+        super().__init__(config, "worker cohort", session)
         self.endpoint = endpoint
-        self.session = session
         self._round_num = 0
         self._force_stop = False
-        self.name = "worker cohort"
 
     @property
     def trainer(self):

@@ -183,3 +183,52 @@ def test_iid_keeps_best_validation_model(tmp_path, monkeypatch):
     assert len(snaps) == 2
     torch.testing.assert_close(sent[0][0], snaps[0][0])
     torch.testing.assert_close(sent[0][1], snaps[1][1])
+
+
+def test_sync_sgd_gradient_worker(tmp_path):
+    """GradientWorker substrate (reference gradient_worker.py): dense weighted-mean gradient
+    all-reduce every step; wire = P·4 B per client per step each way."""
+    sess, result = _run("sign_sgd/cifar10.yaml", {"round": 1, "epoch": 1, "worker_number": 3, "model_name": "LeNet5",
+                                                  "distributed_algorithm": "sync_SGD", "learning_rate": 0.01,
+                                                  "dataset_kwargs.scale": 0.04, "log_level": "WARNING"}, tmp_path)
+    P = sess.layout.num_params
+    B = sess.trainer.hyper.batch_size
+    steps = max((sess.practitioners[c].dataset_size(sess.dc.spec.name) + B - 1) // B for c in range(3))
+    assert result["bytes_up"] == steps * 3 * P * 4
+    assert all(torch.isfinite(torch.tensor(v["test_loss"])) for v in result["performance"].values())
+
+
+def test_topk_error_feedback_worker(tmp_path):
+    from distributed_learning_simulator_amd.algorithm.fed_avg_algorithm import FedAVGAlgorithm
+    from distributed_learning_simulator_amd.method.algorithm_factory import CentralizedAlgorithmFactory
+    from distributed_learning_simulator_amd.server.aggregation_server import AggregationServer
+    from distributed_learning_simulator_amd.worker.error_feedback_worker import TopKErrorFeedbackWorker
+
+    if "test_topk_ef" not in CentralizedAlgorithmFactory.config:
+        CentralizedAlgorithmFactory.register_algorithm("test_topk_ef", TopKErrorFeedbackWorker, AggregationServer,
+                                                       algorithm_cls=FedAVGAlgorithm)
+    captured = []
+    orig = TopKErrorFeedbackWorker.sparsify
+
+    def spy(self, rows):
+        before = rows.clone()
+        out, nb = orig(self, rows)
+        captured.append((before, out))
+        return out, nb
+
+    TopKErrorFeedbackWorker.sparsify = spy
+    try:
+        sess, result = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 2,
+                                                   "distributed_algorithm": "test_topk_ef",
+                                                   "algorithm_kwargs.topk_ratio": 0.05,
+                                                   "dataset_kwargs.scale": 0.04, "log_level": "WARNING"}, tmp_path)
+    finally:
+        TopKErrorFeedbackWorker.sparsify = orig
+    P = sess.layout.num_params
+    k = int(P * 0.05)
+    assert result["bytes_up"] == 2 * 2 * k * 8
+    (b1, s1), (b2, s2) = captured
+    assert int((s1 != 0).sum(1).max()) <= k
+    # residual carried into round 2: what round 1 did not send
+    err = sess.worker._error
+    torch.testing.assert_close(err, b2 - s2)
