@@ -12,8 +12,8 @@
 // padded to (BK+8) bf16 ⇒ conflict-free ds_read_b128 fragment reads; incremental im2col
 // state (no integer division in the K loop); XCD-aware tile order.
 // DEPTH = 2 keeps two K tiles in flight in registers (loads for tile k+2 are issued before
-// computing tile k and written to LDS after computing tile k+1), hiding L2/HBM latency at
-// the 1–2 blocks/CU occupancy these tiles run at; one barrier per K tile.
+// computing tile k and written to LDS after computing tile k+1); measured slower than
+// DEPTH = 1 on every ResNet shape (≈190 VGPRs ⇒ 1 wave/SIMD), kept for the sweep only.
 #include "dls.h"
 #include "gemm_common.h"
 
@@ -270,6 +270,9 @@ bool launch_variant(int v, const ConvNTParams& p, int K, int va, int vb, bool bk
     case 5: return launch_cfg<64, 64, 64, 2, 2, 1, false>(p, K, va, vb, bkm, s);
     case 6: return launch_cfg<128, 128, 32, 2, 2, 1, true>(p, K, va, vb, bkm, s);
     case 7: return launch_cfg<128, 64, 32, 2, 1, 1, true>(p, K, va, vb, bkm, s);
+    case 8: return launch_cfg<256, 64, 64, 4, 1, 1, false>(p, K, va, vb, bkm, s);
+    case 9: return launch_cfg<256, 64, 32, 4, 1, 1, false>(p, K, va, vb, bkm, s);
+    case 10: return launch_cfg<256, 128, 32, 4, 2, 1, false>(p, K, va, vb, bkm, s);
     default: return false;
   }
 }
@@ -281,11 +284,13 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 
 }  // namespace
 
-int conv_nt_num_variants() { return 8; }
+int conv_nt_num_variants() { return 11; }
 
-int conv_nt_default_variant(int M, int N, int R) {
-  if (N <= 64) return 5;  // 64x64: 4 waves of 32x32, 2 blocks/CU (l1: 361 vs 306 TFLOP/s for 128x64)
-  return 0;
+int conv_nt_default_variant(int M, int N, int R, int b_kmajor) {
+  // measured (profiles/kernel_bench_resnet18_sweep.jsonl): forward wants 64-deep K tiles (B rows
+  // are 128-B lines), dgrad's k-major B streams full lines at any depth and prefers 256-row tiles
+  if (b_kmajor) return N <= 64 ? 9 : 10;  // 256x64 / 256x128 BK32: l3 dgrad 666 vs 571 TFLOP/s
+  return N <= 64 ? 5 : 0;                 // 64x64 (l1 361) / 128x128 BK64 (l3 607)
 }
 
 void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
@@ -308,9 +313,9 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   if (va == 8 && vb == 4) vb = 1;
   if (va == 4 && vb == 8) vb = 4;
   if (va == 1 && vb == 4) vb = 1;
-  if (variant < 0) variant = conv_nt_default_variant(p.M, p.N, p.R);
+  if (variant < 0) variant = conv_nt_default_variant(p.M, p.N, p.R, p.b_kmajor);
   // narrow / scalar-gather layers (stem, LeNet, tiny linears) keep the small-K-tile config
-  if ((va != 8 || vb != 8) && variant < 6) variant = (p.N <= 64) ? 7 : 6;
+  if ((va != 8 || vb != 8) && (variant < 6 || variant > 7)) variant = (p.N <= 64) ? 7 : 6;
   if (!launch_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt: bad variant %d\n", variant);
 }
 

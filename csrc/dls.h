@@ -60,7 +60,7 @@ struct ConvTNParams {
 // variant < 0: shape heuristic; 0..conv_nt_num_variants()-1: explicit tile config (benchmarks)
 void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s);
 int conv_nt_num_variants();
-int conv_nt_default_variant(int M, int N, int R);
+int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // dX of a conv (any stride): stride-1 → one flipped-weight NT GEMM; stride s > 1 → s² parity
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, long w_cs, int K, int rep, int B, int OH, int OW,

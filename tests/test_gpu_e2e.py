@@ -17,7 +17,7 @@ def _session(cfg_name, overrides, tmp_path):
     group = cfg_name.split("/")[0]
     args = ["--config-name", cfg_name] + [f"++{group}.{k}={v}" for k, v in overrides.items()]
     args.append(f"++{group}.save_dir={tmp_path}")
-    return Session(load_config(args), comm=Comm())
+    return Session(load_config(args), comm=Comm(device=torch.device("cuda", 0)))
 
 
 def test_fedavg_resnet18_on_gpu(hip, tmp_path):
@@ -35,5 +35,6 @@ def test_memory_probe_measures_activations(hip, tmp_path):
     sess = _session("fed_avg/cifar10.yaml", {"round": 1, "epoch": 1, "worker_number": 2, "model_name": "ResNet18",
                                              "dataset_kwargs.scale": 0.02, "log_level": "WARNING"}, tmp_path)
     act = probe_activation_bytes(sess.model, sess.dc, sess.hyper, sess.device, sess.compute_dtype)
+    print("probe bytes", act, "batch", sess.hyper.batch_size, "x", sess.dc.train.shape, sess.model.name)
     # ResNet-18/CIFAR, batch 64, bf16: tens of MiB of saved activations per client
     assert 8 * 2**20 < act < 2 * 2**30
