@@ -142,6 +142,22 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("embedding_bwd", [](ptr tok, ptr dy, ptr dtable, int K, long n_tok, int D, long t_cs, ptr s) {
     embedding_bwd(P<const int>(tok), P<const bf16_t>(dy), P<float>(dtable), K, n_tok, D, t_cs, S(s));
   });
+  m.def("attn_supported", &attn_supported);
+  m.def("attn_fwd", [](ptr q, ptr k, ptr v, ptr kv, ptr o, ptr lse, long KBH, int H, int L, int DH, ptr s) {
+    return attn_fwd(P<const bf16_t>(q), P<const bf16_t>(k), P<const bf16_t>(v), P<const int>(kv), P<bf16_t>(o),
+                    P<float>(lse), KBH, H, L, DH, S(s));
+  });
+  m.def("attn_bwd", [](ptr dout, ptr q, ptr k, ptr v, ptr o, ptr lse, ptr kv, ptr dq, ptr dk, ptr dv, ptr delta,
+                       long KBH, int H, int L, int DH, ptr s) {
+    return attn_bwd(P<const bf16_t>(dout), P<const bf16_t>(q), P<const bf16_t>(k), P<const bf16_t>(v),
+                    P<const bf16_t>(o), P<const float>(lse), P<const int>(kv), P<bf16_t>(dq), P<bf16_t>(dk),
+                    P<bf16_t>(dv), P<float>(delta), KBH, H, L, DH, S(s));
+  });
+  m.def("spmm", [](ptr rowptr, ptr col, ptr val, ptr x, ptr y, int K, int N, int Nx, int F, long x_cs, long y_cs,
+                   ptr s) {
+    spmm(P<const int>(rowptr), P<const int>(col), P<const float>(val), P<const bf16_t>(x), P<bf16_t>(y), K, N, Nx, F,
+         x_cs, y_cs, S(s));
+  });
   m.def("gather_rows", [](ptr src, ptr idx, ptr dst, long n, long row_elems, ptr s) {
     gather_rows(P<const bf16_t>(src), P<const int>(idx), P<bf16_t>(dst), n, row_elems, S(s));
   });

@@ -118,4 +118,13 @@ void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, l
                    int rep, hipStream_t s);
 void embedding_bwd(const int* tokens, const bf16_t* dy, float* dtable, int K, long n_tok, int D, long t_cs,
                    hipStream_t s);
+// --------------------------------------------------------------- attention / graph
+bool attn_supported(int L, int DH);
+bool attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const int* key_valid, bf16_t* o, float* lse, long KBH,
+              int H, int L, int DH, hipStream_t s);
+bool attn_bwd(const bf16_t* dout, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const float* lse,
+              const int* key_valid, bf16_t* dq, bf16_t* dk, bf16_t* dv, float* delta, long KBH, int H, int L, int DH,
+              hipStream_t s);
+void spmm(const int* rowptr, const int* col, const float* val, const bf16_t* x, bf16_t* y, int K, int N, int Nx, int F,
+          long x_cs, long y_cs, hipStream_t s);
 void gather_rows(const bf16_t* src, const int* idx, bf16_t* dst, long n, long row_elems, hipStream_t s);

@@ -40,6 +40,34 @@ class EdgeSet:
     K: int
     N: int
 
+    def csr(self) -> "CSRPair":
+        """CSR of Â (rows = dst, over K·N flat rows, or N when the graph is shared) and of Âᵀ
+        (for the backward), built once per edge set for the native SpMM kernel."""
+        cached = getattr(self, "_csr", None)
+        if cached is None:
+            rows = self.N * self.K
+            cached = CSRPair(*_to_csr(self.dst, self.src, self.val, rows), *_to_csr(self.src, self.dst, self.val, rows))
+            object.__setattr__(self, "_csr", cached)
+        return cached
+
+
+@dataclass
+class CSRPair:
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    val: torch.Tensor
+    rowptr_t: torch.Tensor
+    col_t: torch.Tensor
+    val_t: torch.Tensor
+
+
+def _to_csr(row: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_rows: int):
+    order = torch.argsort(row, stable=True)
+    counts = torch.bincount(row, minlength=n_rows)
+    rowptr = torch.zeros(n_rows + 1, dtype=torch.int32, device=row.device)
+    rowptr[1:] = counts.cumsum(0).to(torch.int32)
+    return rowptr, col[order].to(torch.int32), val[order].float()
+
 
 def gcn_norm(src: torch.Tensor, dst: torch.Tensor, n: int):
     """Self loops + symmetric normalisation (PyG `gcn_norm`); messages flow src -> dst."""
@@ -217,6 +245,15 @@ class ClientGraphViews:
 def propagate(h: torch.Tensor, es: EdgeSet) -> torch.Tensor:
     """out[k, i] = Σ_j Â_k[i, j] h[k, j]  (h [K, N, F]); differentiable gather + index_add."""
     K, N, F = h.shape
+    from ..ops import backend
+
+    if backend.using_hip(h):  # native CSR SpMM (csrc/attention.hip: spmm_kernel)
+        from ..ops import functional as Fn
+
+        csr = es.csr()
+        if es.K == 1:  # one graph shared by the K models
+            return Fn.spmm(h, csr)
+        return Fn.spmm(h.reshape(1, K * N, F), csr).view(K, N, F)
     if es.K == 1 and K > 1:  # one graph shared by K models (evaluation): fold K into features
         flat = h.permute(1, 0, 2).reshape(N, K * F)
         msg = flat.index_select(0, es.src) * es.val.to(h.dtype)[:, None]

@@ -34,29 +34,39 @@ def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
 
 
 def probe_activation_bytes(model, dc, hyper, device, compute_dtype) -> int:
-    """Peak extra device memory of ONE client's forward+backward at the configured batch
-    size (a real step through the cohort trainer with capacity 1)."""
+    """Activation memory of ONE client's training step at the configured batch size: the
+    bytes autograd keeps for the backward (every distinct tensor saved by the forward, counted
+    through `saved_tensors_hooks`, so the figure does not depend on allocator state), plus the
+    largest single saved tensor twice over for the backward's transient gradients."""
     from .trainer import CohortTrainer
 
     if device.type != "cuda":
         return 0
-    torch.cuda.synchronize(device)
     trainer = CohortTrainer(model, dc, hyper, device, compute_dtype, 1)
-    base = torch.cuda.memory_allocated(device)
-    torch.cuda.reset_peak_memory_stats(device)
     B = hyper.batch_size
     n = dc.train.n if hasattr(dc.train, "n") else B
     idx = (torch.arange(B, device=device) % max(n, 1)).view(1, B)
     x = trainer._gather(dc.train, idx)
     y = dc.train.gather_labels(idx)
     valid = torch.full((1,), B, dtype=torch.int32, device=device)
-    loss, _ = trainer.forward_loss(1, x, y, valid)
+    seen: dict[int, int] = {}
+
+    def pack(t):
+        if t.device.type == "cuda":
+            seen[t.untyped_storage().data_ptr()] = t.untyped_storage().nbytes()
+        return t
+
+    with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+        loss, _ = trainer.forward_loss(1, x, y, valid)
     loss.sum().backward()
-    torch.cuda.synchronize(device)
-    peak = torch.cuda.max_memory_allocated(device) - base
+    # parameter / gradient rows are state (counted by state_bytes_per_client), not activations
+    b = trainer.buffers
+    state = {t.untyped_storage().data_ptr() for t in (b.theta, b.grad, b.state1, b.state2, b.shadow) if t is not None}
+    acts = [nb for ptr, nb in seen.items() if ptr not in state]
+    saved = sum(acts)
+    biggest = max(acts, default=0)
     del trainer, x, y, loss
-    torch.cuda.empty_cache()
-    return int(peak)
+    return int(saved + 2 * biggest)
 
 
 def plan_capacity(wanted: int, layout, model, dc, hyper, device, compute_dtype,

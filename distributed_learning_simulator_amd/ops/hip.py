@@ -327,10 +327,59 @@ def embedding_bwd(dy, tokens, gtable):
     _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _s())
 
 
-# ------------------------------------------------------ not yet native (torch on GPU)
-attn_fwd = ref.attn_fwd
-attn_bwd = ref.attn_bwd
-spmm = ref.spmm
+# ------------------------------------------------------------------------ attention
+def _attn_shape(q):
+    *lead, L, DH = q.shape
+    KB = int(q.shape[0] * q.shape[1])
+    H = int(q.shape[2])
+    return KB * H, H, L, DH
+
+
+def _key_valid(key_valid, q):
+    if key_valid is None:
+        return None
+    return key_valid.to(device=q.device, dtype=torch.int32).reshape(-1).contiguous()
+
+
+def attn_fwd(q, k, v, key_valid=None):
+    """q,k,v [K,B,Hh,L,dh] bf16 → (o [K,B,Hh,L,dh] bf16, lse [K,B,Hh,L] fp32); flash-style
+    kernel (csrc/attention.hip), never materialising the L×L scores."""
+    q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    _check(q, BF16, name="q")
+    KBH, H, L, DH = _attn_shape(q)
+    if not _C.attn_supported(L, DH):
+        raise NotImplementedError(f"attention kernel: unsupported L={L} dh={DH}")
+    kv = _key_valid(key_valid, q)
+    o = torch.empty_like(q)
+    lse = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
+    _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _s())
+    return o, lse
+
+
+def attn_bwd(do, q, k, v, o, lse, key_valid=None):
+    do, q, k, v, o = do.contiguous(), q.contiguous(), k.contiguous(), v.contiguous(), o.contiguous()
+    KBH, H, L, DH = _attn_shape(q)
+    kv = _key_valid(key_valid, q)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    delta = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
+    _C.attn_bwd(_p(do), _p(q), _p(k), _p(v), _p(o), _p(lse.contiguous()), _p(kv), _p(dq), _p(dk), _p(dv), _p(delta),
+                KBH, H, L, DH, _s())
+    return dq, dk, dv
+
+
+# ----------------------------------------------------------------------------- SpMM
+def spmm(rowptr, col, val, x):
+    """CSR (shared graph, fp32 values) times per-client dense x [K,Nx,F] → [K,N,F] bf16."""
+    x = x.contiguous()
+    _check(x, BF16, name="x")
+    K, Nx, F = x.shape
+    N = rowptr.numel() - 1
+    y = torch.empty((K, N, F), dtype=BF16, device=x.device)
+    rp = rowptr.to(torch.int32).contiguous()
+    cl = col.to(torch.int32).contiguous()
+    vl = val.to(torch.float32).contiguous()
+    _C.spmm(_p(rp), _p(cl), _p(vl), _p(x), _p(y), K, N, Nx, F, Nx * F, N * F, _s())
+    return y
 
 
 # ---------------------------------------------------------------- optimiser / FL math

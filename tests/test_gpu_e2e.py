@@ -38,3 +38,17 @@ def test_memory_probe_measures_activations(hip, tmp_path):
     print("probe bytes", act, "batch", sess.hyper.batch_size, "x", sess.dc.train.shape, sess.model.name)
     # ResNet-18/CIFAR, batch 64, bf16: tens of MiB of saved activations per client
     assert 8 * 2**20 < act < 2 * 2**30
+
+
+def test_transformer_imdb_on_gpu(hip, tmp_path):
+    sess = _session("fed_avg/imdb.yaml", {"round": 1, "epoch": 1, "worker_number": 2, "dataset_kwargs.scale": 0.004,
+                                          "log_level": "WARNING"}, tmp_path)
+    res = sess.run()
+    assert torch.isfinite(torch.tensor(res["performance"][1]["test_loss"]))
+
+
+def test_fed_gnn_on_gpu(hip, tmp_path):
+    sess = _session("fed_gnn/cs.yaml", {"round": 1, "epoch": 1, "worker_number": 3, "dataset_kwargs.scale": 0.05,
+                                        "log_level": "WARNING"}, tmp_path)
+    res = sess.run()
+    assert torch.isfinite(torch.tensor(res["performance"][1]["test_loss"]))

@@ -263,3 +263,39 @@ def test_embedding_gather(hip):
     src = _bf(100, 4, 4, 8)
     idx = torch.randint(0, 100, (3, 5), device=DEV)
     assert torch.equal(hip.gather_rows(src, idx), src[idx.reshape(-1)])
+
+
+@pytest.mark.parametrize("L,dh,masked", [(300, 20, True), (64, 32, False), (128, 64, True), (37, 16, True)])
+def test_attention_fwd_bwd(hip, L, dh, masked):
+    K, B, H = 2, 3, 2
+    q, k, v = (_bf(K, B, H, L, dh) for _ in range(3))
+    kv = torch.randint(1, L + 1, (K, B), device=DEV, dtype=torch.int32) if masked else None
+    o, lse = hip.attn_fwd(q, k, v, kv)
+    o_ref, lse_ref = ref.attn_fwd(q.float(), k.float(), v.float(), kv)
+    _close(o, o_ref)
+    torch.testing.assert_close(lse, lse_ref, rtol=1e-3, atol=1e-3)
+    do = _bf(K, B, H, L, dh)
+    dq, dk, dv = hip.attn_bwd(do, q, k, v, o, lse, kv)
+    rq, rk, rv = ref.attn_bwd(do.float(), q.float(), k.float(), v.float(), o.float(), lse_ref, kv)
+    _close(dq, rq, tol=3e-2)
+    _close(dk, rk, tol=3e-2)
+    _close(dv, rv, tol=3e-2)
+
+
+def test_spmm_shared_and_flat(hip):
+    torch.manual_seed(0)
+    N, F, K, E = 500, 64, 3, 4000
+    src = torch.randint(0, N, (E,), device=DEV)
+    dst = torch.randint(0, N, (E,), device=DEV)
+    val = torch.rand(E, device=DEV)
+    from distributed_learning_simulator_amd.data.graph import EdgeSet
+
+    es = EdgeSet(src, dst, val, 1, N)
+    csr = es.csr()
+    x = _bf(K, N, F)
+    y = hip.spmm(csr.rowptr, csr.col, csr.val, x)
+    exp = torch.zeros(K, N, F, device=DEV).index_add_(1, dst, x.float()[:, src] * val[None, :, None])
+    _close(y, exp)
+    yt = hip.spmm(csr.rowptr_t, csr.col_t, csr.val_t, x)
+    expt = torch.zeros(K, N, F, device=DEV).index_add_(1, src, x.float()[:, dst] * val[None, :, None])
+    _close(yt, expt)
