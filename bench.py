@@ -3,6 +3,14 @@ CIFAR-10-shaped synthetic non-IID data, random-init weights (BASELINE.json confi
 `conf/large_scale/fed_avg/cifar10.yaml` hyper-parameters: 5 local epochs, batch 64, SGD lr 0.1
 with cosine schedule).
 
+The other BASELINE.json configs are selectable with `--workload` (same JSON contract):
+  fedavg_resnet18     (default) config 2 above
+  fedobd_transformer  FedOBD, 100 clients, TransformerClassificationModel on imdb-shaped tokens
+                      (`conf/large_scale/fed_obd/imdb.yaml`: block dropout 0.3 + NNADQ 1e-4)
+  signsgd_resnet50    sign-SGD, 128 clients, ResNet-50, ImageNet-shaped (batch 128; one round =
+                      one local epoch of 1-bit majority-vote steps over a scaled ImageNet shard)
+  gtg_resnet18        GTG-Shapley, 32 clients, ResNet-18, CIFAR-10-shaped
+
 One step = one full FL round: every selected client trains its local epochs (lock-step cohort
 on the rank's GPU), uploads are aggregated (fused weighted reduction + RCCL all-reduce across
 ranks), the global model is evaluated on the (rank-sharded) test split and broadcast.
@@ -29,6 +37,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="fedavg_resnet18",
+                    choices=["fedavg_resnet18", "fedobd_transformer", "signsgd_resnet50", "gtg_resnet18"])
     ap.add_argument("--algo", default="fed_avg", choices=["fed_avg", "fed_obd"])
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--clients", type=int, default=100)
@@ -60,21 +70,9 @@ def main() -> None:
                 time.sleep(1)
 
     comm = init_distributed()
-    algo_kwargs = {}
-    endpoint_kwargs = {}
-    if args.algo == "fed_obd":
-        algo_kwargs = {"second_phase_epoch": 1, "dropout_rate": 0.3, "random_client_number": args.clients}
-        endpoint_kwargs = {"server": {"weight": 0.001}, "worker": {"weight": 0.001}}
     rounds = args.warmup + args.steps
-    cfg = config_from_dict({
-        "distributed_algorithm": args.algo, "dataset_name": "CIFAR10", "model_name": args.model,
-        "worker_number": args.clients, "round": rounds + 1000, "epoch": args.epoch, "batch_size": args.batch,
-        "optimizer_name": "SGD", "learning_rate": 0.1, "learning_rate_scheduler_name": "CosineAnnealingLR",
-        "dataset_sampling": "random_label_iid", "dataset_sampling_kwargs": {"sampled_class_number": 5},
-        "algorithm_kwargs": algo_kwargs, "endpoint_kwargs": endpoint_kwargs,
-        "save_models": False, "log_level": "WARNING", "cohort_size": args.cohort,
-        "save_dir": os.path.join("/tmp", f"dls_bench_{os.getpid()}"),
-    })
+    wl = workload_config(args, rounds)
+    cfg = config_from_dict(wl["config"])
     sess = Session(cfg, comm=comm)
     server = sess.server
     init = server._before_start()
@@ -105,7 +103,7 @@ def main() -> None:
     if comm.rank == 0:
         ms = elapsed / args.steps * 1000.0
         out = {
-            "metric": "FL rounds/sec (FedAvg, 100 clients, ResNet-18, CIFAR-10-shaped)",
+            "metric": wl["metric"],
             "value": args.steps / elapsed,
             "unit": "rounds/s",
             "n_gpus": comm.world,
@@ -116,17 +114,71 @@ def main() -> None:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16" if sess.compute_dtype == torch.bfloat16 else "fp32",
-            "data": "synthetic (CIFAR-10-shaped, random_label_iid non-IID shards, random-init weights)",
+            "data": wl["data"],
             "comm_bytes_per_round": bytes_per_round,
             "test_accuracy_last_round": acc,
-            "images_per_s": args.clients * args.epoch * (50000 // args.clients) / (elapsed / args.steps),
+            "samples_per_s": wl["samples_per_round"](sess) / (elapsed / args.steps),
             "config": {
-                "model": args.model, "algo": args.algo, "clients": args.clients, "local_epochs": args.epoch,
-                "global_batch": args.batch * args.clients, "per_client_batch": args.batch, "seq_len": None,
-                "parallelism": f"client-dp{comm.world}", "backend": args.backend,
+                "model": cfg.model_name, "algo": cfg.distributed_algorithm, "clients": cfg.worker_number,
+                "local_epochs": cfg.epoch, "global_batch": cfg.batch_size * cfg.worker_number,
+                "per_client_batch": cfg.batch_size, "seq_len": wl.get("seq_len"),
+                "parallelism": f"client-dp{comm.world}", "backend": args.backend, "workload": args.workload,
             },
         }
         print(json.dumps(out), flush=True)
+
+
+def workload_config(args, rounds: int) -> dict:
+    common = {"round": rounds + 1000, "save_models": False, "log_level": "WARNING", "cohort_size": args.cohort,
+              "save_dir": os.path.join("/tmp", f"dls_bench_{os.getpid()}")}
+
+    def shard_samples(sess):
+        name = sess.dc.spec.name
+        return sum(p.dataset_size(name) for p in sess.practitioners.values()) * sess.config.epoch
+
+    if args.workload == "fedavg_resnet18":
+        algo_kwargs, endpoint_kwargs = {}, {}
+        if args.algo == "fed_obd":
+            algo_kwargs = {"second_phase_epoch": 1, "dropout_rate": 0.3, "random_client_number": args.clients}
+            endpoint_kwargs = {"server": {"weight": 0.001}, "worker": {"weight": 0.001}}
+        cfg = {"distributed_algorithm": args.algo, "dataset_name": "CIFAR10", "model_name": args.model,
+               "worker_number": args.clients, "epoch": args.epoch, "batch_size": args.batch,
+               "optimizer_name": "SGD", "learning_rate": 0.1, "learning_rate_scheduler_name": "CosineAnnealingLR",
+               "dataset_sampling": "random_label_iid", "dataset_sampling_kwargs": {"sampled_class_number": 5},
+               "algorithm_kwargs": algo_kwargs, "endpoint_kwargs": endpoint_kwargs}
+        metric = "FL rounds/sec (FedAvg, 100 clients, ResNet-18, CIFAR-10-shaped)"
+        if args.algo == "fed_obd":
+            metric = "FL rounds/sec (FedOBD, 100 clients, ResNet-18, CIFAR-10-shaped)"
+        data = "synthetic (CIFAR-10-shaped, random_label_iid non-IID shards, random-init weights)"
+        return {"config": {**cfg, **common}, "metric": metric, "data": data, "samples_per_round": shard_samples}
+    if args.workload == "fedobd_transformer":
+        cfg = {"distributed_algorithm": "fed_obd", "dataset_name": "imdb", "model_name": "TransformerClassificationModel",
+               "dataset_kwargs": {"max_len": 300}, "model_kwargs": {"d_model": 100, "nhead": 5, "num_encoder_layer": 2,
+                                                                     "max_len": 300},
+               "worker_number": 100, "epoch": 5, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.01,
+               "learning_rate_scheduler_name": "CosineAnnealingLR", "dataset_sampling": "random_label_iid",
+               "dataset_sampling_kwargs": {"sampled_class_number": 1},
+               "algorithm_kwargs": {"second_phase_epoch": 1, "dropout_rate": 0.3, "random_client_number": 100},
+               "endpoint_kwargs": {"server": {"weight": 0.0001}, "worker": {"weight": 0.0001}}}
+        return {"config": {**cfg, **common}, "metric": "FL rounds/sec (FedOBD, 100 clients, Transformer, imdb-shaped)",
+                "data": "synthetic (imdb-shaped token sequences, max_len 300, non-IID shards, random-init weights)",
+                "samples_per_round": shard_samples, "seq_len": 300}
+    if args.workload == "signsgd_resnet50":
+        cfg = {"distributed_algorithm": "sign_SGD", "dataset_name": "ImageNet", "model_name": "Resnet50",
+               "dataset_kwargs": {"scale": 0.01}, "worker_number": 128, "epoch": 1, "batch_size": 128,
+               "optimizer_name": "SGD", "learning_rate": 0.001, "momentum": 0.0, "distribute_init_parameters": False}
+        return {"config": {**cfg, **common}, "metric": "FL rounds/sec (sign-SGD, 128 clients, ResNet-50, ImageNet-shaped)",
+                "data": "synthetic (ImageNet-shaped 224x224, 1% scale shards, random-init weights)",
+                "samples_per_round": shard_samples}
+    # utility v(S) = test accuracy of the subset model; GTG evaluates thousands of subsets per
+    # round, so the utility set is a 1,000-image CIFAR-shaped test split (all batched on device)
+    cfg = {"distributed_algorithm": "GTG_shapley_value", "dataset_name": "CIFAR10", "model_name": "ResNet18",
+           "dataset_kwargs": {"n_test": 1000}, "worker_number": 32, "epoch": 1, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.1,
+           "dataset_sampling": "random_label_iid", "dataset_sampling_kwargs": {"sampled_class_number": 5}}
+    return {"config": {**cfg, **common}, "metric": "FL rounds/sec (GTG-Shapley, 32 clients, ResNet-18, CIFAR-10-shaped)",
+            "data": "synthetic (CIFAR-10-shaped, 1k-image utility/test split, random_label_iid non-IID shards, "
+                    "random-init weights)",
+            "samples_per_round": shard_samples}
 
 
 if __name__ == "__main__":

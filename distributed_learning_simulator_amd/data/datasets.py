@@ -89,7 +89,7 @@ class ImageDataset:
     im2col gathers are 16-byte vectors (exact: the padded weight channels see only zeros)."""
 
     def __init__(self, spec: DatasetSpec, split: str, seed: int, device, dtype,
-                 materialize_limit: int = 2_000_000_000, noise: float = 1.0, signal: float = 0.35,
+                 materialize_limit: int | None = None, noise: float = 1.0, signal: float = 0.35,
                  channels: int | None = None):
         self.spec = spec
         self.split = split
@@ -110,6 +110,8 @@ class ImageDataset:
         # weak class signal under unit noise: learnable, but not in a single step
         self.prototypes = (proto * signal).permute(0, 2, 3, 1).contiguous()  # [classes, H, W, C]
         self.salt = seed * 2654435761 + (0 if split == "train" else 97)
+        if materialize_limit is None:  # elements: 32 GB of bf16 on a 288 GB MI355X, 4 GB on the host
+            materialize_limit = 16_000_000_000 if torch.device(device).type == "cuda" else 2_000_000_000
         self.materialized = n * H * W * self.channels <= materialize_limit
         self.labels_dev = self.labels.to(device)
         self.proto_dev = self.prototypes.to(device, dtype)

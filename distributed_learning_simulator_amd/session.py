@@ -164,6 +164,8 @@ class Session:
 
     def run_one_round(self, theta_recv: torch.Tensor) -> torch.Tensor:
         server, worker = self.server, self.worker
+        if hasattr(server, "run_round"):  # methods with their own round structure (sign-SGD)
+            return server.run_round(self, theta_recv)
         r = server.round_number
         t0 = time.perf_counter()
         selected = list(server.selected)

@@ -137,21 +137,30 @@ class GradientServer(AggregationServer):
     """Drives synchronous-gradient rounds (the per-step exchange is an all-reduce inside
     `GradientWorker.train_round_sync`); records `epoch_stat.json` like the reference worker."""
 
-    def run_rounds(self, session, theta_recv):
+    def run_round(self, session, theta_recv):
+        """One synchronous round (`epoch` local epochs of per-step exchanges); returns θ."""
         worker = session.worker
+        r = self.round_number
+        t0 = time.perf_counter()
+        selected = list(self.selected)
+
+        def on_epoch(e, stats):
+            loss, acc = stats.epoch_metrics(e)
+            worker.epoch_stat[e + 1] = {"loss": float(loss.mean()), "accuracy": float(acc.mean())}
+
+        theta, up, down = worker.train_round_sync(r, theta_recv, selected, on_epoch)
+        result = FlatParameterMessage(parameter=theta, layout=session.layout)
+        theta_recv, _ = self.send_result(result)
+        session.record_round(r, t0, selected, up, down)
+        return theta_recv
+
+    def run_rounds(self, session, theta_recv):
         while not self._stopped():
-            r = self.round_number
-            t0 = time.perf_counter()
-            selected = list(self.selected)
+            theta_recv = self.run_round(session, theta_recv)
+        self._write_epoch_stat(session)
 
-            def on_epoch(e, stats):
-                loss, acc = stats.epoch_metrics(e)
-                worker.epoch_stat[e + 1] = {"loss": float(loss.mean()), "accuracy": float(acc.mean())}
-
-            theta, up, down = worker.train_round_sync(r, theta_recv, selected, on_epoch)
-            result = FlatParameterMessage(parameter=theta, layout=session.layout)
-            theta_recv, _ = self.send_result(result)
-            session.record_round(r, t0, selected, up, down)
+    def _write_epoch_stat(self, session):
+        worker = session.worker
         if session.is_main:
             os.makedirs(worker.save_dir, exist_ok=True)
             with open(os.path.join(worker.save_dir, "epoch_stat.json"), "wt", encoding="utf8") as f:
