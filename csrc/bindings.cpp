@@ -51,6 +51,7 @@ PYBIND11_MODULE(_dls_hip, m) {
   });
   m.def("conv_tn_splitk", &conv_tn_splitk);
 
+  m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
                      int R, int C, int relu, float eps, int rep, ptr ws, ptr s) {
     bn_fwd(P<const bf16_t>(x), P<const bf16_t>(gamma), P<const bf16_t>(beta), P<const bf16_t>(res), P<bf16_t>(y),

@@ -69,6 +69,7 @@ void conv_tn(ConvTNParams p, int K, hipStream_t s);
 int conv_tn_splitk(int K, int Co, int R, int M);
 
 // ---------------------------------------------------------------- normalisation
+long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
             float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
             float* ws, hipStream_t s);

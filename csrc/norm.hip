@@ -7,6 +7,8 @@
 // pass (dx, and dpre for the residual branch); dγ/dβ land directly in the flat fp32
 // gradient buffer (row stride P).
 #include "common.h"
+#include <algorithm>
+
 #include "dls.h"
 
 namespace {
@@ -42,7 +44,16 @@ __device__ __forceinline__ void store_vec(bf16_t* p, const float* f) {
   }
 }
 
-constexpr int ROWS_PER_BLOCK = 512;
+constexpr int ROWS_PER_BLOCK = 512;  // upper bound; launches pick rows per block for >= ~2048 blocks
+
+// Rows per workgroup for a (clients × rows) channel pass: enough workgroups to fill 256 CUs
+// even when few clients are resident (K = 13 per GPU at 100 clients / 8 GPUs) and late layers
+// are short (ResNet l4: 1,024 rows per client), but ≥ 64 rows so per-channel atomics stay few.
+static int rows_per_block(long R, int K) {
+  const long want = (2048 + K - 1) / K;
+  const long bpc = std::max(1L, std::min(want, std::max(1L, R / 64)));
+  return (int)std::min<long>(ROWS_PER_BLOCK, (R + bpc - 1) / bpc);
+}
 
 // Generic per-(client, channel) double reduction over rows [0, nrows_valid):
 //   mode 0: s0 += x, s1 += x²                       (BN fwd stats)
@@ -53,14 +64,14 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ yv, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
                                                           const int* __restrict__ valid_rows, int R, int C, int relu,
-                                                          float* __restrict__ ws, long ws_cs) {
+                                                          float* __restrict__ ws, long ws_cs, int rpb) {
   __shared__ float red[2][256 * V];
   const int k = blockIdx.y;
   const int CT = C / V;
   const int tid = threadIdx.x;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
-  const int r0 = blockIdx.x * ROWS_PER_BLOCK;
-  const int r1 = min(nvalid, r0 + ROWS_PER_BLOCK);
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(nvalid, r0 + rpb);
   const long base = (long)k * R * C;
   for (int cg = 0; cg < CT; cg += 256) {
     const int ctn = min(256, CT - cg);
@@ -121,10 +132,16 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
           s1[i] += red[1][t2 * V + i];
         }
       }
+      if (MODE == 2) {  // column sums straight into a (pre-zeroed) strided output
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
-        atomicAdd(&ws[(long)k * ws_cs + c0 + i], s0[i]);
-        if (MODE != 2) atomicAdd(&ws[(long)k * ws_cs + C + c0 + i], s1[i]);
+        for (int i = 0; i < V; ++i) atomicAdd(&ws[(long)k * ws_cs + c0 + i], s0[i]);
+      } else {  // per-workgroup partials [K][gridDim.x][2C]: deterministic, no memset, no atomics
+        float* part = ws + ((long)k * gridDim.x + blockIdx.x) * 2 * C;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          part[c0 + i] = s0[i];
+          part[C + c0 + i] = s1[i];
+        }
       }
     }
     __syncthreads();
@@ -136,7 +153,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
 //  fwd:  coef = {scale = γ·rstd, shift = β − mean·scale};  also publishes mean / rstd
 //  bwd:  dx = a·g + d + e·x  with a = γ·rstd, e = −a·rstd·Σgx̂/n, d = −a·Σg/n − e·mean;
 //        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
-__global__ void bn_coef_kernel(const float* __restrict__ ws, const bf16_t* __restrict__ gamma,
+__global__ void bn_coef_kernel(const float* __restrict__ ws, int nparts, const bf16_t* __restrict__ gamma,
                                const bf16_t* __restrict__ beta, const int* __restrict__ valid_rows,
                                const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef,
@@ -147,7 +164,12 @@ __global__ void bn_coef_kernel(const float* __restrict__ ws, const bf16_t* __res
   const int k = i / C, c = i % C;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const float n = (float)max(nvalid, 1);
-  const float s0 = ws[(long)k * 2 * C + c], s1 = ws[(long)k * 2 * C + C + c];
+  float s0 = 0.f, s1 = 0.f;
+  const float* part = ws + (long)k * nparts * 2 * C;
+  for (int b = 0; b < nparts; ++b) {  // fixed order: deterministic statistics
+    s0 += part[(long)b * 2 * C + c];
+    s1 += part[(long)b * 2 * C + C + c];
+  }
   const float g = bf2f(gamma[(long)(k / rep) * g_cs + c]);
   if (!bwd) {
     const float mu = s0 / n;
@@ -177,11 +199,12 @@ __global__ void bn_coef_kernel(const float* __restrict__ ws, const bf16_t* __res
 template <int V>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y, const int* __restrict__ valid_rows,
-                                                       const float* __restrict__ coef, int R, int C, int relu) {
+                                                       const float* __restrict__ coef, int R, int C, int relu,
+                                                       int rpb) {
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
-  const int r0 = blockIdx.x * ROWS_PER_BLOCK, r1 = min(R, r0 + ROWS_PER_BLOCK);
+  const int r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
   const long base = (long)k * R * C;
   for (int cg = 0; cg < CT; cg += 256) {
     const int ctn = min(256, CT - cg);
@@ -227,11 +250,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ y,
                                                            const int* __restrict__ valid_rows,
                                                            const float* __restrict__ coef, int R, int C, int relu,
-                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre) {
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre,
+                                                           int rpb) {
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
-  const int r0 = blockIdx.x * ROWS_PER_BLOCK, r1 = min(R, r0 + ROWS_PER_BLOCK);
+  const int r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
   const long base = (long)k * R * C;
   for (int cg = 0; cg < CT; cg += 256) {
     const int ctn = min(256, CT - cg);
@@ -377,43 +401,51 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     __VA_ARGS__;                    \
   }
 
+long bn_workspace_floats(int K, long R, int C) {
+  const long parts = (R + rows_per_block(R, K) - 1) / rows_per_block(R, K);
+  return (long)K * 3 * C + (long)K * parts * 2 * C;
+}
+
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
             float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
             float* ws, hipStream_t s) {
-  // ws layout: [K][2C] sums, then [K][2C] coefficients
-  float* coef = ws + (long)2 * C * K;
-  DLS_CHECK(hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * K, s));
-  dim3 grid(cdiv(R, ROWS_PER_BLOCK), K);
+  // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
+  float* coef = ws;
+  float* part = ws + (long)3 * C * K;
+  const int rpb = rows_per_block(R, K);
+  dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, valid_rows, R, C, 0, ws, (long)2 * C));
-  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, ws, gamma, beta, valid_rows,
-                     nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+                                   nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb));
+  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
+                     valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
   DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, res, y, valid_rows, coef, R, C,
-                                   relu));
+                                   relu, rpb));
 }
 
 void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
             const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
             bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, hipStream_t s) {
-  float* coef = ws + (long)2 * C * K;
-  DLS_CHECK(hipMemsetAsync(ws, 0, sizeof(float) * 2 * C * K, s));
-  dim3 grid(cdiv(R, ROWS_PER_BLOCK), K);
+  float* coef = ws;
+  float* part = ws + (long)3 * C * K;
+  const int rpb = rows_per_block(R, K);
+  dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
-                                   valid_rows, R, C, relu, ws, (long)2 * C));
-  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, ws, gamma, nullptr, valid_rows,
-                     mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
+                                   valid_rows, R, C, relu, part, (long)2 * C, rpb));
+  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
+                     valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
   DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, valid_rows, coef, R, C,
-                                   relu, dx, dpre));
+                                   relu, dx, dpre, rpb));
 }
 
 void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s) {
   // out must be zeroed by the caller (it is a strided view of the grad buffer)
-  dim3 grid(cdiv(rows, ROWS_PER_BLOCK), K);
+  const int rpb = rows_per_block(rows, K);
+  dim3 grid(cdiv(rows, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 2>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs));
+                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs, rpb));
 }
 
 void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,

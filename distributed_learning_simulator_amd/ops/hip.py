@@ -191,7 +191,7 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5)
     y = torch.empty_like(x)
     mean = torch.empty((K, C), dtype=torch.float32, device=x.device)
     rstd = torch.empty((K, C), dtype=torch.float32, device=x.device)
-    ws = _workspace(5 * K * C, x.device)
+    ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     if residual is not None:
         residual = residual.contiguous()
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
@@ -207,7 +207,7 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     assert rep == 1 or gamma.shape[0] == 1, "bn_bwd supports per-client or fully shared γ"
     dx = torch.empty_like(x)
     dpre = torch.empty_like(x) if need_dpre else None
-    ws = _workspace(5 * K * C, x.device)
+    ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     dg_cs = ggamma.stride(0) if ggamma is not None else 0
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
