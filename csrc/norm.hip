@@ -50,7 +50,7 @@ constexpr int ROWS_PER_BLOCK = 512;  // upper bound; launches pick rows per bloc
 // even when few clients are resident (K = 13 per GPU at 100 clients / 8 GPUs) and late layers
 // are short (ResNet l4: 1,024 rows per client), but ≥ 64 rows so per-channel atomics stay few.
 static int rows_per_block(long R, int K) {
-  const long want = (2048 + K - 1) / K;
+  const long want = std::min<long>(64, (2048 + K - 1) / K);  // ≤ 64 partials per client
   const long bpc = std::max(1L, std::min(want, std::max(1L, R / 64)));
   return (int)std::min<long>(ROWS_PER_BLOCK, (R + bpc - 1) / bpc);
 }
@@ -153,23 +153,40 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
 //  fwd:  coef = {scale = γ·rstd, shift = β − mean·scale};  also publishes mean / rstd
 //  bwd:  dx = a·g + d + e·x  with a = γ·rstd, e = −a·rstd·Σgx̂/n, d = −a·Σg/n − e·mean;
 //        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
-__global__ void bn_coef_kernel(const float* __restrict__ ws, int nparts, const bf16_t* __restrict__ gamma,
-                               const bf16_t* __restrict__ beta, const int* __restrict__ valid_rows,
-                               const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-                               float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef,
-                               float* __restrict__ dgamma, float* __restrict__ dbeta, long dg_cs, long g_cs, int K,
-                               int R, int C, float eps, int rep, int bwd) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= K * C) return;
-  const int k = i / C, c = i % C;
+// grid (cdiv(C, 32), K), 256 threads = 32 channels × 8 part-groups: the per-workgroup partial
+// sums of a client are reduced in a fixed order (deterministic) by 8 lanes per channel.
+__global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ ws, int nparts,
+                                                      const bf16_t* __restrict__ gamma,
+                                                      const bf16_t* __restrict__ beta, const int* __restrict__ valid_rows,
+                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      float* __restrict__ coef, float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta, long dg_cs, long g_cs, int K, int R, int C,
+                                                      float eps, int rep, int bwd) {
+  __shared__ float red[2][8][33];
+  const int k = blockIdx.y;
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    const float* part = ws + (long)k * nparts * 2 * C;
+    for (int b = grp; b < nparts; b += 8) {
+      s0 += part[(long)b * 2 * C + c];
+      s1 += part[(long)b * 2 * C + C + c];
+    }
+  }
+  red[0][grp][cl] = s0;
+  red[1][grp][cl] = s1;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+#pragma unroll
+  for (int g2 = 1; g2 < 8; ++g2) {
+    s0 += red[0][g2][cl];
+    s1 += red[1][g2][cl];
+  }
+  const long i = (long)k * C + c;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const float n = (float)max(nvalid, 1);
-  float s0 = 0.f, s1 = 0.f;
-  const float* part = ws + (long)k * nparts * 2 * C;
-  for (int b = 0; b < nparts; ++b) {  // fixed order: deterministic statistics
-    s0 += part[(long)b * 2 * C + c];
-    s1 += part[(long)b * 2 * C + C + c];
-  }
   const float g = bf2f(gamma[(long)(k / rep) * g_cs + c]);
   if (!bwd) {
     const float mu = s0 / n;
@@ -417,7 +434,7 @@ void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
                                    nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb));
-  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
+  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
                      valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
   DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, res, y, valid_rows, coef, R, C,
                                    relu, rpb));
@@ -433,7 +450,7 @@ void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mea
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
                                    valid_rows, R, C, relu, part, (long)2 * C, rpb));
-  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv((long)K * C, 256)), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
+  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
                      valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
   DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, valid_rows, coef, R, C,
                                    relu, dx, dpre, rpb));
