@@ -146,9 +146,9 @@ def workload_config(args, rounds: int) -> dict:
                "optimizer_name": "SGD", "learning_rate": 0.1, "learning_rate_scheduler_name": "CosineAnnealingLR",
                "dataset_sampling": "random_label_iid", "dataset_sampling_kwargs": {"sampled_class_number": 5},
                "algorithm_kwargs": algo_kwargs, "endpoint_kwargs": endpoint_kwargs}
-        metric = "FL rounds/sec (FedAvg, 100 clients, ResNet-18, CIFAR-10-shaped)"
-        if args.algo == "fed_obd":
-            metric = "FL rounds/sec (FedOBD, 100 clients, ResNet-18, CIFAR-10-shaped)"
+        model = "ResNet-18" if args.model == "ResNet18" else args.model
+        algo = "FedOBD" if args.algo == "fed_obd" else "FedAvg"
+        metric = f"FL rounds/sec ({algo}, {args.clients} clients, {model}, CIFAR-10-shaped)"
         data = "synthetic (CIFAR-10-shaped, random_label_iid non-IID shards, random-init weights)"
         return {"config": {**cfg, **common}, "metric": metric, "data": data, "samples_per_round": shard_samples}
     if args.workload == "fedobd_transformer":
