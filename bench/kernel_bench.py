@@ -89,6 +89,13 @@ def main():
                 sw[v] = (round(flops / tf_v / 1e12, 1), round(flops / td_v / 1e12, 1))
             hip.nt_variant = -1
             row["sweep_fwd_dgrad"] = sw
+            swt = {}
+            for v in range(hip._C.conv_tn_num_variants()):
+                hip.tn_variant = v
+                tw_v = timeit(lambda: hip.conv_wgrad(dy, x, gw, s, pad), args.iters)
+                swt[v] = round(flops / tw_v / 1e12, 1)
+            hip.tn_variant = -1
+            row["sweep_wgrad"] = swt
         if args.torch:
             tf = timeit(lambda: ref.conv_fwd(x, w, s, pad), max(2, args.iters // 4))
             row["torch_fwd_ms"] = tf * 1e3

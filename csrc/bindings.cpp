@@ -39,7 +39,7 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt_num_variants", &conv_nt_num_variants);
   m.def("conv_nt_default_variant", &conv_nt_default_variant);
   m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,
-                      int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, ptr s) {
+                      int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, int variant, ptr s) {
     ConvTNParams p{};
     p.dy = P<const bf16_t>(dy);
     p.x = P<const bf16_t>(x);
@@ -47,9 +47,10 @@ PYBIND11_MODULE(_dls_hip, m) {
     p.dy_cs = dy_cs; p.x_cs = x_cs; p.dw_cs = dw_cs;
     p.B = B; p.H = H; p.W = W; p.C = C; p.OH = OH; p.OW = OW; p.KH = KH; p.KW = KW; p.stride = stride; p.pad = pad;
     p.M = M; p.Co = Co; p.R = R; p.splitk = 1; p.m_per_split = M;
-    conv_tn(p, K, S(s));
+    conv_tn(p, K, variant, S(s));
   });
   m.def("conv_tn_splitk", &conv_tn_splitk);
+  m.def("conv_tn_num_variants", &conv_tn_num_variants);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,

@@ -315,12 +315,11 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   if (va == 1 && vb == 4) vb = 1;
   if (variant < 0) {
     variant = conv_nt_default_variant(p.M, p.N, p.R, p.b_kmajor);
-    // keep >= 2 workgroups per CU when few clients are resident (100 clients over 8 GPUs =
-    // 13 per launch) on short late layers: shrink the tile rather than idle half the chip
+    // few resident clients (100 clients over 8 GPUs = 13 per launch) on the narrow stride-2
+    // dgrad classes: 64x64 tiles keep the chip busy (measured at K = 13; the wide tiles stay
+    // faster even below 2 blocks/CU: profiles/kernel_bench_resnet18_sweep_K13.jsonl)
     auto blocks = [&](int bm, int bn) { return (long)K * cdiv(p.M, bm) * cdiv(p.N, bn); };
-    if (variant == 10 && blocks(256, 128) < 512) variant = 0;
     if (variant == 9 && blocks(256, 64) < 512) variant = 5;
-    if (variant == 0 && blocks(128, 128) < 512) variant = 5;
   }
   // narrow / scalar-gather layers (stem, LeNet, tiny linears) keep the small-K-tile config
   if ((va != 8 || vb != 8) && (variant < 6 || variant > 7)) variant = (p.N <= 64) ? 7 : 6;

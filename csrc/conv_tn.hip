@@ -13,12 +13,11 @@
 
 namespace {
 
-constexpr int BKT = 64;  // pixel (reduction) tile
+constexpr int BKT_MAX = 64;  // largest pixel (reduction) tile: split-K granularity
 
-template <int BMc, int BNr, int VA, int VB, int DEPTH>
-__global__ void __launch_bounds__(256) conv_tn_kernel(ConvTNParams p) {
-  constexpr int T = 256;
-  constexpr int WM = 2, WN = 2;
+template <int BMc, int BNr, int BKT, int WM, int WN, int VA, int VB, int DEPTH>
+__global__ void __launch_bounds__(WM* WN * 64) conv_tn_kernel(ConvTNParams p) {
+  constexpr int T = WM * WN * 64;
   constexpr int TM = BMc / (WM * 32), TN = BNr / (WN * 32);
   constexpr int LDA = BMc + 32;
   constexpr int LDB = BNr + 32;
@@ -177,54 +176,94 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(ConvTNParams p) {
   }
 }
 
-template <int BMc, int BNr>
-void launch_tn_v(const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
-#define TN_CASE(A, B)                                                                          \
-  if (va == A && vb == B) {                                                                    \
-    hipLaunchKernelGGL((conv_tn_kernel<BMc, BNr, A, B, 1>), dim3(grid), dim3(256), 0, s, p); \
-    return;                                                                                    \
+template <int BMc, int BNr, int BKT, int WM, int WN, bool ALLV>
+bool launch_tn_cfg(const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
+#define TN_CASE(A, B)                                                                                        \
+  if (va == A && vb == B) {                                                                                  \
+    hipLaunchKernelGGL((conv_tn_kernel<BMc, BNr, BKT, WM, WN, A, B, 1>), dim3(grid), dim3(WM * WN * 64), 0, s, \
+                       p);                                                                                   \
+    return true;                                                                                             \
   }
-  TN_CASE(8, 8) TN_CASE(4, 4) TN_CASE(1, 1) TN_CASE(8, 4) TN_CASE(4, 8) TN_CASE(8, 1) TN_CASE(1, 8) TN_CASE(4, 1)
-  TN_CASE(1, 4)
+  TN_CASE(8, 8)
+  if constexpr (ALLV) {
+    TN_CASE(4, 4) TN_CASE(1, 1) TN_CASE(8, 4) TN_CASE(4, 8) TN_CASE(8, 1) TN_CASE(1, 8) TN_CASE(4, 1) TN_CASE(1, 4)
+  }
 #undef TN_CASE
-  fprintf(stderr, "conv_tn: unsupported vector widths %d %d\n", va, vb);
+  return false;
+}
+
+struct TnTile {
+  int bm, bn;
+};
+// variant ids are stable (bench/kernel_bench.py --sweep-tn)
+constexpr TnTile kTnTiles[] = {{128, 128}, {64, 128}, {256, 128}, {128, 256}, {128, 128}, {64, 256}};
+constexpr int kTnVariants = sizeof(kTnTiles) / sizeof(kTnTiles[0]);
+
+bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
+  switch (v) {
+    case 0: return launch_tn_cfg<128, 128, 64, 2, 2, true>(p, va, vb, grid, s);
+    case 1: return launch_tn_cfg<64, 128, 64, 2, 2, true>(p, va, vb, grid, s);
+    case 2: return launch_tn_cfg<256, 128, 32, 4, 2, false>(p, va, vb, grid, s);
+    case 3: return launch_tn_cfg<128, 256, 32, 2, 4, false>(p, va, vb, grid, s);
+    case 4: return launch_tn_cfg<128, 128, 32, 2, 2, false>(p, va, vb, grid, s);
+    case 5: return launch_tn_cfg<64, 256, 32, 2, 2, false>(p, va, vb, grid, s);
+    default: return false;
+  }
 }
 
 int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 
-void tn_split(int K, int Co, int R, int M, int& splitk, int& mps) {
-  const int BMc = Co <= 64 ? 64 : 128, BNr = 128;
-  const long tiles = (long)K * cdiv(Co, BMc) * cdiv(R, BNr);
+// measured (profiles/kernel_bench_resnet18_sweep.jsonl, K = 100 and 13 clients): 256x128 BK32
+// tiles win big-Co layers when the launch needs no split-K (l3 769 vs 594 TFLOP/s), 128x256 the
+// Co = 128 layers, 64x128 the Co = 64 layers; otherwise 128x128 BK32 (best at 13 clients/GPU)
+int tn_default_variant(int K, int Co, int R) {
+  auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
+  if (Co <= 64) return 1;
+  if (Co >= 256 && tiles(256, 128) >= 1024) return 2;
+  if (Co == 128 && tiles(128, 256) >= 480) return 3;
+  return 4;
+}
+
+void tn_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
+  const TnTile t = kTnTiles[variant];
+  const long tiles = (long)K * cdiv(Co, t.bm) * cdiv(R, t.bn);
   splitk = 1;
   const int target = 1024;  // >= 4 blocks per CU
   if (tiles < target) {
     splitk = (int)((target + tiles - 1) / tiles);
-    splitk = min(splitk, max(1, M / (4 * BKT)));
+    splitk = min(splitk, max(1, M / (4 * BKT_MAX)));
   }
   mps = cdiv(M, splitk);
-  mps = ((mps + BKT - 1) / BKT) * BKT;
+  mps = ((mps + BKT_MAX - 1) / BKT_MAX) * BKT_MAX;  // slices are whole K tiles of every variant
   splitk = cdiv(M, mps);
+}
+
+int resolve_tn_variant(int variant, int K, int Co, int R, int va, int vb) {
+  if (variant < 0 || variant >= kTnVariants) variant = tn_default_variant(K, Co, R);
+  if ((va != 8 || vb != 8) && variant > 1) variant = Co <= 64 ? 1 : 0;  // narrow layers: all widths
+  return variant;
 }
 
 }  // namespace
 
-void conv_tn(ConvTNParams p, int K, hipStream_t s) {
+int conv_tn_num_variants() { return kTnVariants; }
+
+void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s) {
   p.fd_ohw = make_fastdiv((uint32_t)(p.OH * p.OW));
   p.fd_ow = make_fastdiv((uint32_t)p.OW);
   const int va = vec_width(p.Co);
   const int vb = vec_width(p.C);
-  const bool small_m = p.Co <= 64;
-  tn_split(K, p.Co, p.R, p.M, p.splitk, p.m_per_split);
-  const long tiles = (long)K * cdiv(p.Co, small_m ? 64 : 128) * cdiv(p.R, 128);
+  variant = resolve_tn_variant(variant, K, p.Co, p.R, va, vb);
+  tn_split(K, p.Co, p.R, p.M, variant, p.splitk, p.m_per_split);
+  const TnTile t = kTnTiles[variant];
+  const long tiles = (long)K * cdiv(p.Co, t.bm) * cdiv(p.R, t.bn);
   const int grid = (int)(tiles * p.splitk);
-  if (small_m)
-    launch_tn_v<64, 128>(p, va, vb, grid, s);
-  else
-    launch_tn_v<128, 128>(p, va, vb, grid, s);
+  if (!launch_tn_variant(variant, p, va, vb, grid, s)) fprintf(stderr, "conv_tn: bad variant %d\n", variant);
 }
 
-int conv_tn_splitk(int K, int Co, int R, int M) {
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant) {
   int splitk, mps;
-  tn_split(K, Co, R, M, splitk, mps);
+  variant = resolve_tn_variant(variant, K, Co, R, vec_width(Co), vec_width(C));
+  tn_split(K, Co, R, M, variant, splitk, mps);
   return splitk;
 }

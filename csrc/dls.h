@@ -65,8 +65,10 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, hipStream_t s);
-void conv_tn(ConvTNParams p, int K, hipStream_t s);
-int conv_tn_splitk(int K, int Co, int R, int M);
+void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
+int conv_tn_num_variants();
+// split-K factor the launch will use (callers zero the gradient rows first when > 1)
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant);
 
 // ---------------------------------------------------------------- normalisation
 long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd

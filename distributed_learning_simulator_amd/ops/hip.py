@@ -78,6 +78,7 @@ def _workspace(numel: int, device) -> torch.Tensor:
 # NT-GEMM tile configuration: -1 = per-shape heuristic (csrc/conv_nt.hip); the kernel
 # microbenchmark (bench/kernel_bench.py) sets explicit variant ids to sweep them.
 nt_variant = -1
+tn_variant = -1  # weight-gradient (TN) tile configuration, same convention
 
 
 def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
@@ -128,10 +129,10 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int):
     assert Co2 == Co and Ci == C
     M = B * OH * OW
     R = KH * KW * C
-    if _C.conv_tn_splitk(K, Co, R, M) > 1:
+    if _C.conv_tn_splitk(K, Co, R, M, C, tn_variant) > 1:
         gw.zero_()
     _C.conv_tn(_p(dy), _p(x), _p(gw), M * Co, B * H * W * C, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M,
-               Co, R, K, _s())
+               Co, R, K, tn_variant, _s())
 
 
 def bias_grad(dy, gb):
@@ -175,9 +176,10 @@ def linear_wgrad(dy, x, gw, gb=None):
     dy = dy.contiguous()
     x = x.contiguous()
     assert gw.shape == (K, Fo, Fi) and gw[0].is_contiguous()
-    if _C.conv_tn_splitk(K, Fo, Fi, N) > 1:
+    if _C.conv_tn_splitk(K, Fo, Fi, N, Fi, tn_variant) > 1:
         gw.zero_()
-    _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K, _s())
+    _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K,
+               tn_variant, _s())
     if gb is not None:
         gb.zero_()
         _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, _s())

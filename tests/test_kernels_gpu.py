@@ -78,6 +78,23 @@ def test_conv_nt_every_variant(hip, case):
         hip.nt_variant = -1
 
 
+@pytest.mark.parametrize("case", [(2, 2, 9, 9, 64, 128, 3, 2, 1), (2, 3, 8, 8, 128, 64, 3, 1, 1),
+                                  (3, 2, 6, 6, 24, 40, 3, 1, 1), (2, 8, 16, 16, 64, 64, 3, 1, 1)])
+def test_conv_tn_every_variant(hip, case):
+    K, B, H, W, Ci, Co, k, s, p = case
+    x = _bf(K, B, H, W, Ci)
+    dy = _bf(K, B, (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1, Co)
+    exp = ref.conv_wgrad(dy.float(), x.float(), (K, Co, k, k, Ci), s, p)
+    try:
+        for v in range(hip._C.conv_tn_num_variants()):
+            hip.tn_variant = v
+            gw = torch.full((K, Co, k, k, Ci), 5.0, device=DEV)
+            hip.conv_wgrad(dy, x, gw, s, p)
+            _close(gw, exp)
+    finally:
+        hip.tn_variant = -1
+
+
 def test_conv_shared_weights_rep(hip):
     # eval path: 6 virtual clients share 2 weight rows (rep = 3)
     x = _bf(6, 2, 8, 8, 16)
