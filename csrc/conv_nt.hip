@@ -32,8 +32,9 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
   constexpr int NB = BKM ? PK : PB;
   static_assert(PA >= 1 && NB >= 1, "tile too small for thread count");
   static_assert(TM >= 1 && TN >= 1, "wave tile");
-  __shared__ __attribute__((aligned(16))) bf16_t As[2][BM][LDA];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BKM ? BK : BN][BKM ? LDBK : LDA];
+  constexpr int NBUF = DEPTH == 0 ? 1 : 2;  // DEPTH 0: one LDS buffer, two barriers per K tile
+  __shared__ __attribute__((aligned(16))) bf16_t As[NBUF][BM][LDA];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[NBUF][BKM ? BK : BN][BKM ? LDBK : LDA];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
@@ -177,7 +178,22 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
     }
   };
 
-  if constexpr (DEPTH == 1) {
+  if constexpr (DEPTH == 0) {
+    // half the LDS of the double-buffered loop ⇒ more resident workgroups per CU; the global
+    // loads of tile k+1 are still in flight during compute(k)
+    load_into(ra0, rb0);
+    store_from(ra0, rb0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load_into(ra0, rb0);
+      compute(0);
+      if (kt + 1 < nk) {
+        __syncthreads();
+        store_from(ra0, rb0, 0);
+        __syncthreads();
+      }
+    }
+  } else if constexpr (DEPTH == 1) {
     load_into(ra0, rb0);
     store_from(ra0, rb0, 0);
     __syncthreads();
@@ -273,6 +289,10 @@ bool launch_variant(int v, const ConvNTParams& p, int K, int va, int vb, bool bk
     case 8: return launch_cfg<256, 64, 64, 4, 1, 1, false>(p, K, va, vb, bkm, s);
     case 9: return launch_cfg<256, 64, 32, 4, 1, 1, false>(p, K, va, vb, bkm, s);
     case 10: return launch_cfg<256, 128, 32, 4, 2, 1, false>(p, K, va, vb, bkm, s);
+    case 11: return launch_cfg<128, 128, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
+    case 12: return launch_cfg<256, 128, 32, 4, 2, 0, false>(p, K, va, vb, bkm, s);
+    case 13: return launch_cfg<64, 64, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
+    case 14: return launch_cfg<256, 64, 32, 4, 1, 0, false>(p, K, va, vb, bkm, s);
     default: return false;
   }
 }
@@ -284,13 +304,16 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 
 }  // namespace
 
-int conv_nt_num_variants() { return 11; }
+int conv_nt_num_variants() { return 15; }
 
 int conv_nt_default_variant(int M, int N, int R, int b_kmajor) {
   // measured (profiles/kernel_bench_resnet18_sweep.jsonl): forward wants 64-deep K tiles (B rows
   // are 128-B lines), dgrad's k-major B streams full lines at any depth and prefers 256-row tiles
-  if (b_kmajor) return N <= 64 ? 9 : 10;  // 256x64 / 256x128 BK32: l3 dgrad 666 vs 571 TFLOP/s
-  return N <= 64 ? 5 : 0;                 // 64x64 (l1 361) / 128x128 BK64 (l3 607)
+  // N <= 64 (ResNet l1, stride-2 dgrad classes): single-LDS-buffer 64x64 tiles, 4 blocks/CU
+  // (l1 fwd 428 vs 364, dgrad 376 vs 331 TFLOP/s for the double-buffered 64x64 / 256x64)
+  if (N <= 64) return 13;
+  if (b_kmajor) return 10;  // 256x128 BK32: l3 dgrad 672 vs 564 TFLOP/s (128x128)
+  return 0;                 // 128x128 BK64 (l3 fwd 600)
 }
 
 void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
@@ -315,11 +338,9 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   if (va == 1 && vb == 4) vb = 1;
   if (variant < 0) {
     variant = conv_nt_default_variant(p.M, p.N, p.R, p.b_kmajor);
-    // few resident clients (100 clients over 8 GPUs = 13 per launch) on the narrow stride-2
-    // dgrad classes: 64x64 tiles keep the chip busy (measured at K = 13; the wide tiles stay
-    // faster even below 2 blocks/CU: profiles/kernel_bench_resnet18_sweep_K13.jsonl)
-    auto blocks = [&](int bm, int bn) { return (long)K * cdiv(p.M, bm) * cdiv(p.N, bn); };
-    if (variant == 9 && blocks(256, 64) < 512) variant = 5;
+    // (at 13 clients per launch the wide tiles stay faster even below 2 blocks/CU:
+    // profiles/kernel_bench_resnet18_sweep_K13.jsonl)
+    (void)K;
   }
   // narrow / scalar-gather layers (stem, LeNet, tiny linears) keep the small-K-tile config
   if ((va != 8 || vb != 8) && (variant < 6 || variant > 7)) variant = (p.N <= 64) ? 7 : 6;

@@ -24,8 +24,9 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_kernel(ConvTNParams p) {
   constexpr int CCA = BMc / VA, RPA = T / CCA, PA = BKT / RPA;
   constexpr int CCB = BNr / VB, RPB = T / CCB, PB = BKT / RPB;
   static_assert(PA >= 1 && PB >= 1, "tile too small");
-  __shared__ __attribute__((aligned(16))) bf16_t As[2][BKT][LDA];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BKT][LDB];
+  constexpr int NBUF = DEPTH == 0 ? 1 : 2;  // DEPTH 0: one LDS buffer, two barriers per K tile
+  __shared__ __attribute__((aligned(16))) bf16_t As[NBUF][BKT][LDA];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[NBUF][BKT][LDB];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tilesM = (p.Co + BMc - 1) / BMc, tilesN = (p.R + BNr - 1) / BNr;
@@ -125,7 +126,20 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_kernel(ConvTNParams p) {
 
   const int nk = (mend - mbeg + BKT - 1) / BKT;
   if (nk <= 0) return;
-  if constexpr (DEPTH == 1) {
+  if constexpr (DEPTH == 0) {
+    load_into(ra0, rb0);
+    store_from(ra0, rb0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load_into(ra0, rb0);
+      compute(0);
+      if (kt + 1 < nk) {
+        __syncthreads();
+        store_from(ra0, rb0, 0);
+        __syncthreads();
+      }
+    }
+  } else if constexpr (DEPTH == 1) {
     load_into(ra0, rb0);
     store_from(ra0, rb0, 0);
     __syncthreads();
@@ -176,11 +190,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_kernel(ConvTNParams p) {
   }
 }
 
-template <int BMc, int BNr, int BKT, int WM, int WN, bool ALLV>
+template <int BMc, int BNr, int BKT, int WM, int WN, bool ALLV, int DEPTH = 1>
 bool launch_tn_cfg(const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
 #define TN_CASE(A, B)                                                                                        \
   if (va == A && vb == B) {                                                                                  \
-    hipLaunchKernelGGL((conv_tn_kernel<BMc, BNr, BKT, WM, WN, A, B, 1>), dim3(grid), dim3(WM * WN * 64), 0, s, \
+    hipLaunchKernelGGL((conv_tn_kernel<BMc, BNr, BKT, WM, WN, A, B, DEPTH>), dim3(grid), dim3(WM * WN * 64), 0, s, \
                        p);                                                                                   \
     return true;                                                                                             \
   }
@@ -196,7 +210,8 @@ struct TnTile {
   int bm, bn;
 };
 // variant ids are stable (bench/kernel_bench.py --sweep-tn)
-constexpr TnTile kTnTiles[] = {{128, 128}, {64, 128}, {256, 128}, {128, 256}, {128, 128}, {64, 256}};
+constexpr TnTile kTnTiles[] = {{128, 128}, {64, 128}, {256, 128}, {128, 256}, {128, 128},
+                               {64, 256},  {128, 128}, {256, 128}, {64, 128}};
 constexpr int kTnVariants = sizeof(kTnTiles) / sizeof(kTnTiles[0]);
 
 bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
@@ -207,6 +222,9 @@ bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, h
     case 3: return launch_tn_cfg<128, 256, 32, 2, 4, false>(p, va, vb, grid, s);
     case 4: return launch_tn_cfg<128, 128, 32, 2, 2, false>(p, va, vb, grid, s);
     case 5: return launch_tn_cfg<64, 256, 32, 2, 2, false>(p, va, vb, grid, s);
+    case 6: return launch_tn_cfg<128, 128, 64, 2, 2, false, 0>(p, va, vb, grid, s);
+    case 7: return launch_tn_cfg<256, 128, 32, 4, 2, false, 0>(p, va, vb, grid, s);
+    case 8: return launch_tn_cfg<64, 128, 64, 2, 2, false, 0>(p, va, vb, grid, s);
     default: return false;
   }
 }
@@ -218,7 +236,7 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 // Co = 128 layers, 64x128 the Co = 64 layers; otherwise 128x128 BK32 (best at 13 clients/GPU)
 int tn_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
-  if (Co <= 64) return 1;
+  if (Co <= 64) return 8;  // 64x128 single LDS buffer: l1 445 vs 359 TFLOP/s
   if (Co >= 256 && tiles(256, 128) >= 1024) return 2;
   if (Co == 128 && tiles(128, 256) >= 480) return 3;
   return 4;
