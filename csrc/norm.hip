@@ -64,7 +64,8 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ yv, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
                                                           const int* __restrict__ valid_rows, int R, int C, int relu,
-                                                          float* __restrict__ ws, long ws_cs, int rpb) {
+                                                          float* __restrict__ ws, long ws_cs, int rpb,
+                                                          const uint8_t* __restrict__ rmask) {
   __shared__ float red[2][256 * V];
   const int k = blockIdx.y;
   const int CT = C / V;
@@ -107,10 +108,16 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
         } else {
           float vx[V], vy[V];
           load_vec<V>(b + off, vx);
-          if (relu) load_vec<V>(yv + off, vy);
+          uint32_t mbits = 0xFFu;
+          if (rmask) {  // 1-bit ReLU mask written by the forward (V == 8): 1/16 of reading y
+            mbits = rmask[((long)k * R + r) * (C / 8) + c0 / 8];
+          } else if (relu) {
+            load_vec<V>(yv + off, vy);
+          }
 #pragma unroll
           for (int i = 0; i < V; ++i) {
-            const float g = (relu && vy[i] <= 0.f) ? 0.f : va[i];
+            const bool dead = rmask ? !((mbits >> i) & 1u) : (relu && vy[i] <= 0.f);
+            const float g = dead ? 0.f : va[i];
             s0[i] += g;
             s1[i] += g * (vx[i] - mu[i]) * rs[i];
           }
@@ -217,7 +224,7 @@ template <int V>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y, const int* __restrict__ valid_rows,
                                                        const float* __restrict__ coef, int R, int C, int relu,
-                                                       int rpb) {
+                                                       int rpb, uint8_t* __restrict__ rmask) {
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
@@ -257,6 +264,12 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int j = 0; j < V; ++j) out[j] = 0.f;
       }
+      if (rmask) {  // bit j = (bf16(out_j) > 0): exactly the mask the backward would read from y
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) m |= (bf2f(f2bf(out[j])) > 0.f ? 1u : 0u) << j;
+        rmask[((long)k * R + r) * (C / 8) + c0 / 8] = (uint8_t)m;
+      }
       store_vec<V>(y + off, out);
     }
   }
@@ -268,7 +281,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const int* __restrict__ valid_rows,
                                                            const float* __restrict__ coef, int R, int C, int relu,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre,
-                                                           int rpb) {
+                                                           int rpb, const uint8_t* __restrict__ rmask) {
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
@@ -295,7 +308,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
         float vdy[V], vx[V];
         load_vec<V>(dy + off, vdy);
         load_vec<V>(x + off, vx);
-        if (relu) {
+        if (rmask) {
+          const uint32_t mbits = rmask[((long)k * R + r) * (C / 8) + c0 / 8];
+#pragma unroll
+          for (int j = 0; j < V; ++j) vdy[j] = ((mbits >> j) & 1u) ? vdy[j] : 0.f;
+        } else if (relu) {
           float vy[V];
           load_vec<V>(y + off, vy);
 #pragma unroll
@@ -425,7 +442,7 @@ long bn_workspace_floats(int K, long R, int C) {
 
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
             float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
-            float* ws, hipStream_t s) {
+            float* ws, uint8_t* rmask, hipStream_t s) {
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
@@ -433,27 +450,28 @@ void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb));
+                                   nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr));
   hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
                      valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+  if (V != 8) rmask = nullptr;  // bit masks need 8-channel vectors
   DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, res, y, valid_rows, coef, R, C,
-                                   relu, rpb));
+                                   relu, rpb, rmask));
 }
 
 void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
             const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
-            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, hipStream_t s) {
+            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, hipStream_t s) {
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
-                                   valid_rows, R, C, relu, part, (long)2 * C, rpb));
+                                   valid_rows, R, C, relu, part, (long)2 * C, rpb, V == 8 ? rmask : nullptr));
   hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
                      valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
   DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, valid_rows, coef, R, C,
-                                   relu, dx, dpre, rpb));
+                                   relu, dx, dpre, rpb, V == 8 ? rmask : nullptr));
 }
 
 void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s) {
@@ -462,7 +480,7 @@ void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, 
   dim3 grid(cdiv(rows, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 2>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs, rpb));
+                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs, rpb, nullptr));
 }
 
 void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,

@@ -146,8 +146,13 @@ class _BN(torch.autograd.Function):
         C = x.shape[-1]
         x3 = x.reshape(K, -1, C)
         r3 = residual.reshape(K, -1, C) if residual is not None else None
-        y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
+        mask = None
+        if be is ref:
+            y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
+        else:  # native: 1-bit ReLU mask so the backward need not re-read y
+            y, mean, rstd, mask = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True)
         ctx.save_for_backward(x3, y, mean, rstd, gamma)
+        ctx.relu_mask = mask
         ctx.valid_rows, ctx.relu, ctx.has_res = valid_rows, relu, residual is not None
         ctx.ggamma, ctx.gbeta, ctx.shape = ggamma, gbeta, x.shape
         return y.reshape(x.shape)
@@ -165,7 +170,7 @@ class _BN(torch.autograd.Function):
                 ctx.gbeta.copy_(dbeta)
         else:
             dx, dpre = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
-                                 ctx.ggamma, ctx.gbeta, ctx.has_res)
+                                 ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask)
         dres = dpre.reshape(ctx.shape) if ctx.has_res else None
         return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres
 

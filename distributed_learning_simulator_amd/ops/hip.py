@@ -186,7 +186,9 @@ def linear_wgrad(dy, x, gw, gb=None):
 
 
 # ------------------------------------------------------------------------ batchnorm
-def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5):
+def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False):
+    """Returns (y, mean, rstd); with_mask=True (ReLU, C % 8 == 0) also returns the 1-bit ReLU
+    mask [K, R, C/8] uint8 that bn_bwd can read instead of y."""
     K, R, C = x.shape
     x = x.contiguous()
     g_cs, rep = _client_view(gamma, K)
@@ -197,12 +199,17 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5)
     if residual is not None:
         residual = residual.contiguous()
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    mask = None
+    if with_mask and relu and C % 8 == 0:
+        mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
-              eps, rep, _p(ws), _s())
+              eps, rep, _p(ws), _p(mask), _s())
+    if with_mask:
+        return y, mean, rstd, mask
     return y, mean, rstd
 
 
-def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre):
+def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None):
     K, R, C = x.shape
     g_cs, rep = _client_view(gamma, K)
     # the kernels index γ by client k with stride g_cs: shared (Kw=1 → stride 0) or per client
@@ -213,7 +220,7 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     dg_cs = ggamma.stride(0) if ggamma is not None else 0
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
-              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _s())
+              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _s())
     return dx, dpre
 
 

@@ -150,6 +150,14 @@ def test_batchnorm(hip, C, relu, res):
     gbeta = torch.zeros((K, C), device=DEV)
     dx, dpre = hip.bn_bwd(dy, x, y, mean, rstd, g, valid, relu, gg, gbeta, res)
     dx2, dg2, db2, dpre2 = ref.bn_bwd(dy.float(), x.float(), y.float(), mean2, rstd2, g.float(), valid, relu)
+    if relu and C % 8 == 0:  # the 1-bit ReLU mask path gives the same gradients bit for bit
+        y_m, _, _, mask = hip.bn_fwd(x, g, b, valid, relu, r, with_mask=True)
+        assert torch.equal(y_m, y)
+        bits = torch.stack([(mask >> j) & 1 for j in range(8)], -1).reshape(K, 300, C).bool()
+        assert torch.equal(bits, y.float() > 0)
+        gg2, gb2 = torch.zeros_like(gg), torch.zeros_like(gbeta)
+        dx_m, dpre_m = hip.bn_bwd(dy, x, y, mean, rstd, g, valid, relu, gg2, gb2, res, relu_mask=mask)
+        assert torch.equal(dx_m, dx) and torch.equal(gg2, gg)
     _close(dx, dx2, 3e-2)
     _close(gg, dg2, 2e-2)
     _close(gbeta, db2, 2e-2)
