@@ -80,6 +80,8 @@ class DistributedTrainingConfig:
     save_dir: str = ""
     save_models: bool = True
     deterministic: bool = False
+    checkpoint_every: int = 0  # rounds between resumable checkpoints (0 => off)
+    resume_from: str = ""  # checkpoint.pt to resume the run from
     extra: dict = field(default_factory=dict)
 
     # ------------------------------------------------------------------ processing

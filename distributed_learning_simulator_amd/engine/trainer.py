@@ -98,6 +98,7 @@ class CohortTrainer:
         self.capacity = capacity
         self.layout = model.layout
         self.buffers = CohortBuffers(self.layout, capacity, self.device, compute_dtype, hyper.optimizer_name)
+        self.debug = False  # `debug` config: per-step NaN/Inf scan (synchronises every step)
         self.hooks = HookRegistry()
         self.adam_step_count = torch.zeros(capacity, dtype=torch.float32, device=self.device)
         self.graph = dataset_collection.graph
@@ -255,6 +256,9 @@ class CohortTrainer:
                 valid = schedule.counts[s]
                 loss, correct = self.forward_loss(K, x, labels, valid)
                 loss.sum().backward()
+                if self.debug and not bool(torch.isfinite(loss).all()):  # synchronising NaN scan
+                    bad = (~torch.isfinite(loss)).nonzero().flatten().tolist()
+                    raise FloatingPointError(f"step {s}: non-finite loss for cohort rows {bad}")
                 with torch.no_grad():
                     vf = valid.float()
                     stats.loss_sum[e] += loss.detach() * vf

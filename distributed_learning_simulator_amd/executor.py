@@ -49,3 +49,11 @@ class Executor:
     @property
     def peak_bytes(self) -> int | None:
         return self._peak_bytes
+
+    # resumable state (Session.save_checkpoint / load_checkpoint): tensors and plain numbers
+    # only; subclasses with state that outlives a round extend these
+    def state_dict(self) -> dict:
+        return {}
+
+    def load_state_dict(self, state: dict) -> None:
+        pass

@@ -48,6 +48,15 @@ class FedOBDWorker(AggregationWorker):
     def local_epochs(self) -> int:
         return 1 if self.phase == Phase.STAGE_TWO else self._epochs
 
+    def state_dict(self) -> dict:
+        return {"phase": self.phase.value, "stage2_epoch": self._stage2_epoch}
+
+    def load_state_dict(self, state: dict) -> None:
+        self.phase = Phase(state.get("phase", Phase.STAGE_ONE.value))
+        self._stage2_epoch = int(state.get("stage2_epoch", 0))
+        if self.phase == Phase.STAGE_TWO:
+            self.disable_choose_model_by_validation()
+
     def run_round(self, round_num, theta_g, client_ids):
         last = getattr(self.session.server, "last_result", None)
         if self.phase == Phase.STAGE_ONE and last is not None and last.other_data.get("phase_two"):
@@ -92,6 +101,15 @@ class FedOBDServer(AggregationServer):
         self.last_result = None
         # a plateau switches FedOBD to stage 2 instead of ending training
         self._obd_early_stop, self.early_stop = self.early_stop, False
+
+    def state_dict(self) -> dict:
+        return {**super().state_dict(), "phase": self.phase.value}
+
+    def load_state_dict(self, state: dict) -> None:
+        super().load_state_dict(state)
+        self.phase = Phase(state.get("phase", Phase.STAGE_ONE.value))
+        if self.phase != Phase.STAGE_ONE:
+            self._algorithm.num_blocks = 0
 
     def _select_workers(self):
         if self.phase != Phase.STAGE_ONE:

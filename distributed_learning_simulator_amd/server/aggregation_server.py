@@ -43,6 +43,21 @@ class AggregationServer(Server):
     def round_number(self) -> int:
         return self._round_number
 
+    def state_dict(self) -> dict:
+        st = {"max_acc": self._max_acc, "plateau": self._plateau, "ended": self._ended,
+              "selected": list(self.selected)}
+        if self._algorithm is not None and hasattr(self._algorithm, "state_dict"):
+            st["algorithm"] = self._algorithm.state_dict()
+        return st
+
+    def load_state_dict(self, state: dict) -> None:
+        self._max_acc = float(state.get("max_acc", 0.0))
+        self._plateau = int(state.get("plateau", 0))
+        self._ended = bool(state.get("ended", False))
+        self.selected = list(state.get("selected", []))
+        if "algorithm" in state and self._algorithm is not None and hasattr(self._algorithm, "load_state_dict"):
+            self._algorithm.load_state_dict(state["algorithm"])
+
     @property
     def performance_stat(self) -> dict:
         return self._stat

@@ -93,6 +93,7 @@ class Session:
             capacity = plan_capacity(per_rank, self.layout, self.model, self.dc, self.hyper, self.device,
                                      self.compute_dtype, explicit=cfg.cohort_size)
         self.trainer = CohortTrainer(self.model, self.dc, self.hyper, self.device, self.compute_dtype, capacity)
+        self.trainer.debug = bool(cfg.debug)
         algo = cfg.distributed_algorithm
         self.server = CentralizedAlgorithmFactory.create_server(
             algo, {"config": cfg, "session": self}, dict(cfg.endpoint_kwargs.get("server", {})))
@@ -132,17 +133,21 @@ class Session:
         cfg = self.config
         server, worker = self.server, self.worker
         t_start = time.perf_counter()
-        init = server._before_start()
-        theta_recv, down = server.send_result(init)
-        self.bytes_down_total += down
-        server.last_recorded = None  # the round-0 (init) stat is not a round row
-        if hasattr(server, "run_rounds"):  # methods with their own round structure
-            server.run_rounds(self, theta_recv)
+        if cfg.resume_from:
+            theta_recv = self.load_checkpoint(cfg.resume_from)
         else:
-            while not server._stopped():
-                theta_recv = self.run_one_round(theta_recv)
+            init = server._before_start()
+            theta_recv, down = server.send_result(init)
+            self.bytes_down_total += down
+            server.last_recorded = None  # the round-0 (init) stat is not a round row
+        while not server._stopped():
+            theta_recv = self.run_one_round(theta_recv)
+            if cfg.checkpoint_every and (server.round_number - 1) % cfg.checkpoint_every == 0:
+                self.save_checkpoint(theta_recv)
         self.sync()
         total = time.perf_counter() - t_start
+        if hasattr(server, "_write_epoch_stat"):
+            server._write_epoch_stat(self)
         server._server_exit()
         worker._after_training()
         get_logger().info("training use %s seconds", total)
@@ -162,28 +167,114 @@ class Session:
             result["sv_S"] = getattr(algo, "shapley_values_S", {})
         return result
 
+    # ------------------------------------------------------------- checkpoints
+    def save_checkpoint(self, theta_recv: torch.Tensor, path: str | None = None) -> str | None:
+        """Resumable state after a finished round: global θ (as held by the server
+        and as received by the clients), round counter, per-round records, early-stop state,
+        next round's selection, and the method's own state (`state_dict` hooks). Plain tensors /
+        numbers only, so `torch.load(weights_only=True)` reads it back."""
+        if not self.is_main:
+            return None
+        server = self.server
+        path = path or os.path.join(self.config.save_dir, "checkpoint.pt")
+        state = {
+            "version": 1,
+            "round_number": server.round_number,
+            "global_parameter": server.global_parameter.detach().cpu(),
+            "theta_recv": theta_recv.detach().cpu(),
+            "stat": {int(k) if isinstance(k, int) else str(k): v for k, v in server.performance_stat.items()},
+            "server": server.state_dict(),
+            "worker": self.worker.state_dict(),
+            "bytes_up": self.bytes_up_total,
+            "bytes_down": self.bytes_down_total,
+            "metrics": [{k: v for k, v in m.items() if isinstance(v, (int, float, str))} for m in self.metrics],
+        }
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, path)
+        return path
+
+    def load_checkpoint(self, path: str) -> torch.Tensor:
+        state = torch.load(path, map_location="cpu", weights_only=True)
+        server = self.server
+        server.global_parameter = state["global_parameter"].to(self.device)
+        server._stat.update(state["stat"])
+        server.load_state_dict(state["server"])
+        server._round_number = int(state["round_number"])
+        self.worker.load_state_dict(state["worker"])
+        self.bytes_up_total = int(state["bytes_up"])
+        self.bytes_down_total = int(state["bytes_down"])
+        self.metrics = list(state["metrics"])
+        get_logger().info("resumed from %s at round %d", path, server.round_number)
+        return state["theta_recv"].to(self.device)
+
+    # ------------------------------------------------------------------- round
+    def _failed_clients(self, r: int, selected: list[int]) -> list[int]:
+        """Deterministic client-failure injection (`algorithm_kwargs.failure_rate`, SURVEY
+        §5.3): a failed client neither trains nor uploads; the server sees it as skipped."""
+        p = float(self.config.algorithm_kwargs.get("failure_rate", 0.0) or 0.0)
+        if p <= 0:
+            return []
+        g = torch.Generator().manual_seed((self.config.seed + 7) * 1_000_033 + r)
+        drop = torch.rand(len(selected), generator=g) < p
+        return [c for c, d in zip(selected, drop.tolist()) if d]
+
+    def _mark(self, marks: list, name: str) -> None:
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            marks.append((name, ev))
+        else:
+            marks.append((name, time.perf_counter()))
+
+    @staticmethod
+    def _phase_times(marks: list) -> dict:
+        out = {}
+        for (_, a), (name, b) in zip(marks, marks[1:]):
+            out[name] = (a.elapsed_time(b) / 1e3) if hasattr(a, "elapsed_time") else (b - a)
+        return out
+
     def run_one_round(self, theta_recv: torch.Tensor) -> torch.Tensor:
         server, worker = self.server, self.worker
         if hasattr(server, "run_round"):  # methods with their own round structure (sign-SGD)
             return server.run_round(self, theta_recv)
         r = server.round_number
         t0 = time.perf_counter()
+        marks: list = []
+        self._mark(marks, "start")
         selected = list(server.selected)
-        local = self.local_clients(selected)
+        failed = self._failed_clients(r, selected)
+        active = [c for c in selected if c not in set(failed)]
+        local = self.local_clients(active)
         if server.algorithm is not None:
             server.algorithm.expected_kind = "delta" if getattr(worker, "_send_parameter_diff", True) else "parameter"
         up0 = worker.endpoint.bytes_sent
         for msg in worker.run_round(r, theta_recv, local):
             server._process_worker_data(msg)
-        skipped = sorted(set(range(self.config.worker_number)) - set(selected))
+        skipped = sorted(set(range(self.config.worker_number)) - set(active))
         if skipped:
             server._process_worker_data(None, worker_ids=skipped)
         up_local = worker.endpoint.bytes_sent - up0
+        self._mark(marks, "train_s")
         result = server._aggregate_worker_data()
+        self._mark(marks, "aggregate_s")
         theta_recv, down = server.send_result(result)
+        self._mark(marks, "eval_broadcast_s")
         up = self._sum_scalar(up_local)
-        self.record_round(r, t0, selected, up, down)
+        if self.config.debug:
+            self._debug_check(r, server.global_parameter)
+        extra = {"failed_clients": len(failed)} if failed else {}
+        self.record_round(r, t0, active, up, down, marks=marks, **extra)
         return theta_recv
+
+    def _debug_check(self, r: int, theta: torch.Tensor) -> None:
+        """`debug` mode (reference `debug` flag): synchronise and scan the global
+        model for NaN/Inf after every round (the reference asserts on NaN in aggregation)."""
+        self.sync()
+        if theta is not None and not bool(torch.isfinite(theta).all()):
+            bad = (~torch.isfinite(theta)).nonzero().flatten()[:8].tolist()
+            raise FloatingPointError(f"round {r}: non-finite global parameters at flat indices {bad}")
 
     def _sum_scalar(self, v: int) -> int:
         if self.comm.world == 1:
@@ -192,10 +283,12 @@ class Session:
         self.comm.all_reduce_(t)
         return int(t.item())
 
-    def record_round(self, r, t0, selected, up, down, **extra) -> dict:
+    def record_round(self, r, t0, selected, up, down, marks=None, **extra) -> dict:
         if self.config.extra.get("sync_round_timing", True):
             self.sync()
         wall = time.perf_counter() - t0
+        if marks and self.config.extra.get("sync_round_timing", True):
+            extra.update(self._phase_times(marks))
         self.bytes_up_total += up
         self.bytes_down_total += down
         rec = getattr(self.server, "last_recorded", None)

@@ -25,6 +25,13 @@ class ErrorFeedbackWorker(AggregationWorker):
         assert self._send_parameter_diff, "error feedback needs delta uploads"
         self._error: torch.Tensor | None = None  # [worker_number, P_pad] residuals
 
+    def state_dict(self) -> dict:
+        return {"error": self._error.cpu()} if self._error is not None else {}
+
+    def load_state_dict(self, state: dict) -> None:
+        if "error" in state:
+            self._error = state["error"].to(self.trainer.buffers.theta.device)
+
     def sparsify(self, rows: torch.Tensor) -> tuple[torch.Tensor, list[int]]:
         """rows [K,P] (Δ + e) → (sparse rows [K,P] with zeros where not sent, wire bytes per row)."""
         raise NotImplementedError

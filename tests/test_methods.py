@@ -232,3 +232,32 @@ def test_topk_error_feedback_worker(tmp_path):
     # residual carried into round 2: what round 1 did not send
     err = sess.worker._error
     torch.testing.assert_close(err, b2 - s2)
+
+
+def test_checkpoint_resume_reproduces_run(tmp_path):
+    """Resumable checkpoints: a run resumed from its round-2 checkpoint ends with
+    exactly the global model of the uninterrupted run."""
+    base = {"round": 3, "epoch": 1, "worker_number": 3, "dataset_kwargs.scale": 0.04, "log_level": "WARNING",
+            "checkpoint_every": 1}
+    full, res_full = _run("fed_avg/mnist.yaml", base, tmp_path / "full")
+    ck = tmp_path / "full" / "checkpoint.pt"
+    assert ck.exists()
+    # stop after round 2 (the checkpoint written then), resume for round 3
+    part, _ = _run("fed_avg/mnist.yaml", {**base, "round": 2}, tmp_path / "part")
+    resumed, res = _run("fed_avg/mnist.yaml", {**base, "resume_from": str(tmp_path / "part" / "checkpoint.pt")},
+                        tmp_path / "resumed")
+    torch.testing.assert_close(resumed.server.global_parameter, full.server.global_parameter, rtol=0, atol=0)
+    assert sorted(res["performance"]) == sorted(res_full["performance"])
+    assert [m["round"] for m in resumed.metrics] == [1, 2, 3]
+
+
+def test_failure_injection_and_phase_timers(tmp_path):
+    sess, res = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 6, "dataset_kwargs.scale": 0.04,
+                                            "log_level": "WARNING", "algorithm_kwargs.failure_rate": 0.5,
+                                            "debug": True}, tmp_path)
+    rows = sess.metrics
+    assert any(r.get("failed_clients", 0) > 0 for r in rows)
+    for r in rows:
+        assert r["selected_clients"] + r.get("failed_clients", 0) == 6
+        assert r["comm_bytes_up"] == r["selected_clients"] * sess.layout.num_params * 4
+        assert {"train_s", "aggregate_s", "eval_broadcast_s"} <= set(r)
