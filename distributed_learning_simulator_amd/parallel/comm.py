@@ -119,10 +119,12 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> Comm:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if use_gpu else "gloo"
+        # "nccl" is RCCL on ROCm (xGMI). DLS_DIST_BACKEND=gloo rehearses the multi-rank GPU
+        # path with ranks sharing one GPU (RCCL needs one GPU per rank).
+        backend = os.environ.get("DLS_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kwargs = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kwargs["device_id"] = device
         dist.init_process_group(**kwargs)
     _COMM = Comm(rank, world, device)
