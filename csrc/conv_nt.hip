@@ -293,6 +293,9 @@ bool launch_variant(int v, const ConvNTParams& p, int K, int va, int vb, bool bk
     case 12: return launch_cfg<256, 128, 32, 4, 2, 0, false>(p, K, va, vb, bkm, s);
     case 13: return launch_cfg<64, 64, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
     case 14: return launch_cfg<256, 64, 32, 4, 1, 0, false>(p, K, va, vb, bkm, s);
+    case 15: return launch_cfg<256, 128, 64, 4, 2, 0, false>(p, K, va, vb, bkm, s);
+    case 16: return launch_cfg<128, 128, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
+    case 17: return launch_cfg<128, 64, 64, 2, 1, 0, false>(p, K, va, vb, bkm, s);
     default: return false;
   }
 }
@@ -304,7 +307,7 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 
 }  // namespace
 
-int conv_nt_num_variants() { return 15; }
+int conv_nt_num_variants() { return 18; }
 
 int conv_nt_default_variant(int M, int N, int R, int b_kmajor) {
   // measured (profiles/kernel_bench_resnet18_sweep.jsonl): forward wants 64-deep K tiles (B rows

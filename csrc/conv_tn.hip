@@ -211,7 +211,7 @@ struct TnTile {
 };
 // variant ids are stable (bench/kernel_bench.py --sweep-tn)
 constexpr TnTile kTnTiles[] = {{128, 128}, {64, 128}, {256, 128}, {128, 256}, {128, 128},
-                               {64, 256},  {128, 128}, {256, 128}, {64, 128}};
+                               {64, 256},  {128, 128}, {256, 128}, {64, 128}, {256, 128}, {128, 256}};
 constexpr int kTnVariants = sizeof(kTnTiles) / sizeof(kTnTiles[0]);
 
 bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
@@ -225,6 +225,8 @@ bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, h
     case 6: return launch_tn_cfg<128, 128, 64, 2, 2, false, 0>(p, va, vb, grid, s);
     case 7: return launch_tn_cfg<256, 128, 32, 4, 2, false, 0>(p, va, vb, grid, s);
     case 8: return launch_tn_cfg<64, 128, 64, 2, 2, false, 0>(p, va, vb, grid, s);
+    case 9: return launch_tn_cfg<256, 128, 64, 4, 2, false, 0>(p, va, vb, grid, s);
+    case 10: return launch_tn_cfg<128, 256, 64, 2, 4, false, 0>(p, va, vb, grid, s);
     default: return false;
   }
 }
@@ -237,8 +239,8 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 int tn_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
   if (Co <= 64) return 8;  // 64x128 single LDS buffer: l1 445 vs 359 TFLOP/s
-  if (Co >= 256 && tiles(256, 128) >= 1024) return 2;
-  if (Co == 128 && tiles(128, 256) >= 480) return 3;
+  if (Co >= 256 && tiles(256, 128) >= 1024) return 9;  // 256x128 BK64 single buffer: l4 752
+  if (Co == 128 && tiles(128, 256) >= 480) return 10;  // 128x256 BK64 single buffer: l2 700
   return 4;
 }
 
