@@ -66,7 +66,8 @@ _ws_cache: dict = {}
 
 
 def _workspace(numel: int, device) -> torch.Tensor:
-    key = (device, "ws")
+    # one scratch buffer per (device, stream): sub-cohorts on concurrent streams must not share it
+    key = (device, torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0)
     t = _ws_cache.get(key)
     if t is None or t.numel() < numel:
         t = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
