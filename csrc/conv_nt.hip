@@ -296,6 +296,7 @@ bool launch_variant(int v, const ConvNTParams& p, int K, int va, int vb, bool bk
     case 15: return launch_cfg<256, 128, 64, 4, 2, 0, false>(p, K, va, vb, bkm, s);
     case 16: return launch_cfg<128, 128, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
     case 17: return launch_cfg<128, 64, 64, 2, 1, 0, false>(p, K, va, vb, bkm, s);
+    case 18: return launch_cfg<256, 32, 64, 4, 1, 0, true>(p, K, va, vb, bkm, s);  // N <= 32 (DenseNet k=12)
     default: return false;
   }
 }
@@ -307,14 +308,14 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 
 }  // namespace
 
-int conv_nt_num_variants() { return 18; }
+int conv_nt_num_variants() { return 19; }
 
 int conv_nt_default_variant(int M, int N, int R, int b_kmajor) {
   // measured (profiles/kernel_bench_resnet18_sweep.jsonl): forward wants 64-deep K tiles (B rows
   // are 128-B lines), dgrad's k-major B streams full lines at any depth and prefers 256-row tiles
   // N <= 64 (ResNet l1, stride-2 dgrad classes): single-LDS-buffer 64x64 tiles, 4 blocks/CU
   // (l1 fwd 428 vs 364, dgrad 376 vs 331 TFLOP/s for the double-buffered 64x64 / 256x64)
-  if (N <= 64) return 13;
+  if (N <= 64) return 13;  // (the 32-wide v18 measured slower on DenseNet's 12-channel outputs)
   if (b_kmajor) return 10;  // 256x128 BK32: l3 dgrad 672 vs 564 TFLOP/s (128x128)
   return 0;                 // 128x128 BK64 (l3 fwd 600)
 }
@@ -346,7 +347,7 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
     (void)K;
   }
   // narrow / scalar-gather layers (stem, LeNet, tiny linears) keep the small-K-tile config
-  if ((va != 8 || vb != 8) && (variant < 6 || variant > 7)) variant = (p.N <= 64) ? 7 : 6;
+  if ((va != 8 || vb != 8) && !(variant == 6 || variant == 7 || variant == 18)) variant = (p.N <= 64) ? 7 : 6;
   if (!launch_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt: bad variant %d\n", variant);
 }
 

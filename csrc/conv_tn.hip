@@ -211,7 +211,8 @@ struct TnTile {
 };
 // variant ids are stable (bench/kernel_bench.py --sweep-tn)
 constexpr TnTile kTnTiles[] = {{128, 128}, {64, 128}, {256, 128}, {128, 256}, {128, 128},
-                               {64, 256},  {128, 128}, {256, 128}, {64, 128}, {256, 128}, {128, 256}};
+                               {64, 256},  {128, 128}, {256, 128}, {64, 128}, {256, 128}, {128, 256},
+                               {32, 256}};
 constexpr int kTnVariants = sizeof(kTnTiles) / sizeof(kTnTiles[0]);
 
 bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
@@ -227,6 +228,7 @@ bool launch_tn_variant(int v, const ConvTNParams& p, int va, int vb, int grid, h
     case 8: return launch_tn_cfg<64, 128, 64, 2, 2, false, 0>(p, va, vb, grid, s);
     case 9: return launch_tn_cfg<256, 128, 64, 4, 2, false, 0>(p, va, vb, grid, s);
     case 10: return launch_tn_cfg<128, 256, 64, 2, 4, false, 0>(p, va, vb, grid, s);
+    case 11: return launch_tn_cfg<32, 256, 64, 1, 4, true>(p, va, vb, grid, s);  // Co <= 32 (DenseNet)
     default: return false;
   }
 }
@@ -238,7 +240,7 @@ int vec_width(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 // Co = 128 layers, 64x128 the Co = 64 layers; otherwise 128x128 BK32 (best at 13 clients/GPU)
 int tn_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
-  if (Co <= 64) return 8;  // 64x128 single LDS buffer: l1 445 vs 359 TFLOP/s
+  if (Co <= 64) return 8;  // 64x128 single LDS buffer: l1 445 vs 359 TFLOP/s (32x256 v11 slower on Co=12)
   if (Co >= 256 && tiles(256, 128) >= 1024) return 9;  // 256x128 BK64 single buffer: l4 752
   if (Co == 128 && tiles(128, 256) >= 480) return 10;  // 128x256 BK64 single buffer: l2 700
   return 4;
@@ -260,7 +262,7 @@ void tn_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
 
 int resolve_tn_variant(int variant, int K, int Co, int R, int va, int vb) {
   if (variant < 0 || variant >= kTnVariants) variant = tn_default_variant(K, Co, R);
-  if ((va != 8 || vb != 8) && variant > 1) variant = Co <= 64 ? 1 : 0;  // narrow layers: all widths
+  if ((va != 8 || vb != 8) && variant > 1 && variant != 11) variant = Co <= 64 ? 1 : 0;  // all vector widths
   return variant;
 }
 
