@@ -161,6 +161,10 @@ PYBIND11_MODULE(_dls_hip, m) {
     spmm(P<const int>(rowptr), P<const int>(col), P<const float>(val), P<const bf16_t>(x), P<bf16_t>(y), K, N, Nx, F,
          x_cs, y_cs, S(s));
   });
+  m.def("nnadq_qdq", [](ptr x, ptr seg, ptr lo, ptr scale, ptr levels, int K, long Pn, long ld, int nseg, ptr s) {
+    nnadq_qdq(P<float>(x), P<const int>(seg), P<const float>(lo), P<const float>(scale), P<const float>(levels), K, Pn,
+              ld, nseg, S(s));
+  });
   m.def("gather_rows", [](ptr src, ptr idx, ptr dst, long n, long row_elems, ptr s) {
     gather_rows(P<const bf16_t>(src), P<const int>(idx), P<bf16_t>(dst), n, row_elems, S(s));
   });

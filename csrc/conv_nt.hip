@@ -33,8 +33,14 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
   static_assert(PA >= 1 && NB >= 1, "tile too small for thread count");
   static_assert(TM >= 1 && TN >= 1, "wave tile");
   constexpr int NBUF = DEPTH == 0 ? 1 : 2;  // DEPTH 0: one LDS buffer, two barriers per K tile
-  __shared__ __attribute__((aligned(16))) bf16_t As[NBUF][BM][LDA];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[NBUF][BKM ? BK : BN][BKM ? LDBK : LDA];
+  constexpr int B_ROWS = BKM ? BK : BN, B_COLS = BKM ? LDBK : LDA;
+  constexpr int A_BYTES = NBUF * BM * LDA * 2, B_BYTES = NBUF * B_ROWS * B_COLS * 2;
+  constexpr int SW = TN * 32 + 8;                   // epilogue slab row (bf16), 16-B padded
+  constexpr int EPI_BYTES = WM * WN * 32 * SW * 2;  // one 32-row slab per wave
+  constexpr int SMEM = (A_BYTES + B_BYTES) > EPI_BYTES ? (A_BYTES + B_BYTES) : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  auto& As = *reinterpret_cast<bf16_t(*)[NBUF][BM][LDA]>(smem);
+  auto& Bs = *reinterpret_cast<bf16_t(*)[NBUF][B_ROWS][B_COLS]>(smem + A_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
@@ -224,39 +230,60 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
     }
   }
 
-  // --- epilogue: optional bias (+ReLU), bf16 store
+  // --- epilogue: bias (+ReLU) → bf16 → per-wave 32-row LDS slab → 16-B coalesced global
+  // stores (one 2-B store per element would make the epilogue store-issue-bound on wide
+  // outputs such as the Transformer FFN: 1.9 M rows × 2048)
   bf16_t* __restrict__ y = p.y + (long)client * p.y_cs;
   const bf16_t* bias = p.bias ? p.bias + (long)(client / p.rep) * p.b_cs : nullptr;
+  float bvals[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn0 + j * 32 + (lane & 31);
-    const float bv = (bias && n < p.N) ? bf2f(bias[n]) : 0.f;
+    bvals[j] = (bias && n < p.N) ? bf2f(bias[n]) : 0.f;
+  }
+  bf16_t* slab = reinterpret_cast<bf16_t*>(smem) + wid * 32 * SW;
+  const bool vec_ok = (p.N % 8) == 0;
+  __syncthreads();  // every wave is done reading the K-loop tiles that the slabs overwrite
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wm0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        if (m < p.M && n < p.N) {
-          float v = acc[i][j][e] + bv;
-          if (p.relu) v = fmaxf(v, 0.f);
-          long row = m;
-          if (p.out_s > 1) {
-            const uint32_t b = fdiv(m, p.fd_ohw);
-            const uint32_t rem = m - b * p.OH * p.OW;
-            const uint32_t oh = fdiv(rem, p.fd_ow);
-            const uint32_t ow = rem - oh * p.OW;
-            row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
-          }
-          y[row * p.N + n] = f2bf(v);
-        }
+        float v = acc[i][j][e] + bvals[j];
+        if (p.relu) v = fmaxf(v, 0.f);
+        slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = f2bf(v);
       }
     }
+    __syncthreads();
+    for (int qd = lane; qd < 32 * TN * 4; qd += 64) {
+      const int r = qd / (TN * 4), cc = (qd % (TN * 4)) * 8;
+      const int m = m0 + wm0 + i * 32 + r, n = n0 + wn0 + cc;
+      if (m >= p.M || n >= p.N) continue;
+      long row = m;
+      if (p.out_s > 1) {
+        const uint32_t b = fdiv(m, p.fd_ohw);
+        const uint32_t rem = m - b * p.OH * p.OW;
+        const uint32_t oh = fdiv(rem, p.fd_ow);
+        const uint32_t ow = rem - oh * p.OW;
+        row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
+      }
+      bf16_t* dst = y + row * p.N + n;
+      const bf16_t* src = slab + r * SW + cc;
+      if (vec_ok && n + 8 <= p.N) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      } else {
+        for (int t = 0; t < 8 && n + t < p.N; ++t) dst[t] = src[t];
+      }
+    }
+    __syncthreads();  // the slab is rewritten for the next row block
   }
 }
 
-// ALLV: instantiate every vector-width combination (narrow-channel layers); otherwise only
-// the 16-B (8,8) gathers that every wide layer uses.
-template <int BM, int BN, int BK, int WM, int WN, int DEPTH, bool ALLV>
+// VSET: which (A, B) vector widths to instantiate — 0: the 16-B (8,8) gathers every wide layer
+// uses; 1: + the 8-B combinations of channel counts ≡ 4 (mod 8) (Transformer d_model = 100);
+// 2: every combination incl. scalar (stem-less narrow layers, LeNet).
+template <int BM, int BN, int BK, int WM, int WN, int DEPTH, int VSET>
 bool launch_cfg(const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStream_t s) {
   const int grid = K * cdiv(p.M, BM) * cdiv(p.N, BN);
 #define NT_CASE(A, B)                                                                                           \
@@ -270,7 +297,8 @@ bool launch_cfg(const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStrea
     return true;                                                                                                \
   }
   NT_CASE(8, 8)
-  if constexpr (ALLV) { NT_CASE(8, 1) NT_CASE(4, 4) NT_CASE(4, 1) NT_CASE(1, 8) NT_CASE(1, 1) }
+  if constexpr (VSET >= 1) { NT_CASE(4, 4) NT_CASE(8, 4) NT_CASE(4, 8) }  // d_model = 100 style widths
+  if constexpr (VSET >= 2) { NT_CASE(8, 1) NT_CASE(4, 1) NT_CASE(1, 8) NT_CASE(1, 1) }
 #undef NT_CASE
   return false;
 }
@@ -278,25 +306,25 @@ bool launch_cfg(const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStrea
 // Tile configurations (variant ids are stable: the microbenchmark sweeps them)
 bool launch_variant(int v, const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStream_t s) {
   switch (v) {
-    case 0: return launch_cfg<128, 128, 64, 2, 2, 1, false>(p, K, va, vb, bkm, s);
-    case 1: return launch_cfg<128, 64, 64, 4, 1, 1, false>(p, K, va, vb, bkm, s);
-    case 2: return launch_cfg<128, 64, 64, 4, 1, 2, false>(p, K, va, vb, bkm, s);
-    case 3: return launch_cfg<256, 128, 64, 4, 2, 1, false>(p, K, va, vb, bkm, s);
-    case 4: return launch_cfg<128, 128, 32, 2, 2, 1, false>(p, K, va, vb, bkm, s);
-    case 5: return launch_cfg<64, 64, 64, 2, 2, 1, false>(p, K, va, vb, bkm, s);
-    case 6: return launch_cfg<128, 128, 32, 2, 2, 1, true>(p, K, va, vb, bkm, s);
-    case 7: return launch_cfg<128, 64, 32, 2, 1, 1, true>(p, K, va, vb, bkm, s);
-    case 8: return launch_cfg<256, 64, 64, 4, 1, 1, false>(p, K, va, vb, bkm, s);
-    case 9: return launch_cfg<256, 64, 32, 4, 1, 1, false>(p, K, va, vb, bkm, s);
-    case 10: return launch_cfg<256, 128, 32, 4, 2, 1, false>(p, K, va, vb, bkm, s);
-    case 11: return launch_cfg<128, 128, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
-    case 12: return launch_cfg<256, 128, 32, 4, 2, 0, false>(p, K, va, vb, bkm, s);
-    case 13: return launch_cfg<64, 64, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
-    case 14: return launch_cfg<256, 64, 32, 4, 1, 0, false>(p, K, va, vb, bkm, s);
-    case 15: return launch_cfg<256, 128, 64, 4, 2, 0, false>(p, K, va, vb, bkm, s);
-    case 16: return launch_cfg<128, 128, 64, 2, 2, 0, false>(p, K, va, vb, bkm, s);
-    case 17: return launch_cfg<128, 64, 64, 2, 1, 0, false>(p, K, va, vb, bkm, s);
-    case 18: return launch_cfg<256, 32, 64, 4, 1, 0, true>(p, K, va, vb, bkm, s);  // N <= 32 (DenseNet k=12)
+    case 0: return launch_cfg<128, 128, 64, 2, 2, 1, 1>(p, K, va, vb, bkm, s);
+    case 1: return launch_cfg<128, 64, 64, 4, 1, 1, 0>(p, K, va, vb, bkm, s);
+    case 2: return launch_cfg<128, 64, 64, 4, 1, 2, 0>(p, K, va, vb, bkm, s);
+    case 3: return launch_cfg<256, 128, 64, 4, 2, 1, 0>(p, K, va, vb, bkm, s);
+    case 4: return launch_cfg<128, 128, 32, 2, 2, 1, 0>(p, K, va, vb, bkm, s);
+    case 5: return launch_cfg<64, 64, 64, 2, 2, 1, 0>(p, K, va, vb, bkm, s);
+    case 6: return launch_cfg<128, 128, 32, 2, 2, 1, 2>(p, K, va, vb, bkm, s);
+    case 7: return launch_cfg<128, 64, 32, 2, 1, 1, 2>(p, K, va, vb, bkm, s);
+    case 8: return launch_cfg<256, 64, 64, 4, 1, 1, 0>(p, K, va, vb, bkm, s);
+    case 9: return launch_cfg<256, 64, 32, 4, 1, 1, 0>(p, K, va, vb, bkm, s);
+    case 10: return launch_cfg<256, 128, 32, 4, 2, 1, 1>(p, K, va, vb, bkm, s);
+    case 11: return launch_cfg<128, 128, 64, 2, 2, 0, 0>(p, K, va, vb, bkm, s);
+    case 12: return launch_cfg<256, 128, 32, 4, 2, 0, 0>(p, K, va, vb, bkm, s);
+    case 13: return launch_cfg<64, 64, 64, 2, 2, 0, 1>(p, K, va, vb, bkm, s);
+    case 14: return launch_cfg<256, 64, 32, 4, 1, 0, 0>(p, K, va, vb, bkm, s);
+    case 15: return launch_cfg<256, 128, 64, 4, 2, 0, 0>(p, K, va, vb, bkm, s);
+    case 16: return launch_cfg<128, 128, 64, 2, 2, 0, 0>(p, K, va, vb, bkm, s);
+    case 17: return launch_cfg<128, 64, 64, 2, 1, 0, 0>(p, K, va, vb, bkm, s);
+    case 18: return launch_cfg<256, 32, 64, 4, 1, 0, 2>(p, K, va, vb, bkm, s);  // N <= 32 (DenseNet k=12)
     default: return false;
   }
 }
@@ -337,8 +365,6 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   const bool bkm = p.b_kmajor != 0;
   int va = vec_width(p.C);
   int vb = bkm ? vec_width(p.N) : vec_width(p.R);
-  if (va == 8 && vb == 4) vb = 1;
-  if (va == 4 && vb == 8) vb = 4;
   if (va == 1 && vb == 4) vb = 1;
   if (variant < 0) {
     variant = conv_nt_default_variant(p.M, p.N, p.R, p.b_kmajor);
@@ -347,7 +373,13 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
     (void)K;
   }
   // narrow / scalar-gather layers (stem, LeNet, tiny linears) keep the small-K-tile config
-  if ((va != 8 || vb != 8) && !(variant == 6 || variant == 7 || variant == 18)) variant = (p.N <= 64) ? 7 : 6;
+  const bool w84 = (va == 8 || va == 4) && (vb == 8 || vb == 4);  // covered by VSET 1 variants
+  if (w84 && !(va == 8 && vb == 8) && !(variant == 0 || variant == 10 || variant == 13 || variant == 6 ||
+                                        variant == 7 || variant == 18)) {
+    variant = (p.N <= 64) ? 13 : (bkm ? 10 : 0);
+  } else if (!w84 && !(variant == 6 || variant == 7 || variant == 18)) {
+    variant = (p.N <= 64) ? 7 : 6;
+  }
   if (!launch_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt: bad variant %d\n", variant);
 }
 

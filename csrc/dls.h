@@ -116,6 +116,8 @@ void seg_minmax(const float* x, const int* seg, float* mn, float* mx, int K, lon
                 hipStream_t s);
 void stochastic_qdq(float* x, const int* seg, const float* mn, const float* mx, int K, long P, long ld, int nseg,
                     const uint32_t* seeds, int levels, hipStream_t s);
+void nnadq_qdq(float* x, const int* seg, const float* lo, const float* scale, const float* levels, int K, long P,
+               long ld, int nseg, hipStream_t s);
 void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s);
 void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, long P, hipStream_t s);
 void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, long n_tok, int D, long t_cs,

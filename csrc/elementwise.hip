@@ -390,6 +390,22 @@ __global__ void stochastic_qdq_kernel(float* __restrict__ x, const int* __restri
   }
 }
 
+// NNADQ (FedOBD): deterministic per-(client, tensor) quantisation with an adaptive level count;
+// lo / scale / levels are per (row, segment). Writes the dequantised value in place.
+__global__ void nnadq_qdq_kernel(float* __restrict__ x, const int* __restrict__ seg, const float* __restrict__ lo,
+                                 const float* __restrict__ scale, const float* __restrict__ levels, long P, long ld,
+                                 int nseg) {
+  const int k = blockIdx.y;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    const long q0 = (long)k * nseg + seg[i];
+    const float l = lo[q0], sc = scale[q0];
+    const long gi = (long)k * ld + i;
+    float q = rintf((x[gi] - l) / sc);
+    q = fminf(fmaxf(q, 0.f), levels[q0]);
+    x[gi] = l + q * sc;
+  }
+}
+
 __global__ void sign_pack_kernel(const float* __restrict__ g, uint8_t* __restrict__ out, long P, long ld,
                                  long nbytes) {
   const int k = blockIdx.y;
@@ -543,6 +559,12 @@ void stochastic_qdq(float* x, const int* seg, const float* mn, const float* mx, 
                     const uint32_t* seed, int levels, hipStream_t s) {
   dim3 grid(grid_for(P, 256, 2048), K);
   hipLaunchKernelGGL(stochastic_qdq_kernel, grid, dim3(256), 0, s, x, seg, mn, mx, P, ld, nseg, seed, levels);
+}
+
+void nnadq_qdq(float* x, const int* seg, const float* lo, const float* scale, const float* levels, int K, long P,
+               long ld, int nseg, hipStream_t s) {
+  dim3 grid(grid_for(P, 256, 2048), K);
+  hipLaunchKernelGGL(nnadq_qdq_kernel, grid, dim3(256), 0, s, x, seg, lo, scale, levels, P, ld, nseg);
 }
 
 void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s) {

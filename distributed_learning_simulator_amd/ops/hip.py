@@ -485,6 +485,31 @@ def stochastic_qdq(x, seg_ids, nseg, seeds, levels):
     return out
 
 
+def seg_minmax(x, seg_ids, nseg):
+    K, P, ld = _row_args(x)
+    mn = torch.full((K, nseg), float("inf"), dtype=torch.float32, device=x.device)
+    mx = torch.full((K, nseg), float("-inf"), dtype=torch.float32, device=x.device)
+    _C.seg_minmax(_p(x), _p(seg_ids.to(torch.int32).contiguous()), _p(mn), _p(mx), K, P, ld, nseg, _s())
+    return mn, mx
+
+
+def seg_sq_sums(x, seg_ids, nseg):
+    """Σx² per (row, segment); segments are 16-element aligned layout tensors."""
+    K, P, ld = _row_args(x)
+    out = torch.empty((K, nseg), dtype=torch.float32, device=x.device)
+    _C.block_sq_norms(_p(x), _p(seg_ids.to(torch.int32).contiguous()), _p(out), K, P, ld, nseg, _s())
+    return out
+
+
+def nnadq_qdq(x, seg_ids, lo, scale, levels):
+    K, P, ld = _row_args(x)
+    out = x.contiguous().clone()
+    nseg = lo.shape[1]
+    _C.nnadq_qdq(_p(out), _p(seg_ids.to(torch.int32).contiguous()), _p(lo.contiguous()), _p(scale.contiguous()),
+                 _p(levels.float().contiguous()), K, P, out.stride(0), nseg, _s())
+    return out
+
+
 def sign_pack(g):
     K, P, ld = _row_args(g)
     out = torch.empty((K, (P + 7) // 8), dtype=torch.uint8, device=g.device)

@@ -79,20 +79,30 @@ def nnadq_quantize(x: torch.Tensor, seg_ids: torch.Tensor, seg_sizes: torch.Tens
     (dequantised x, wire_bytes list, mean bits)."""
     K = x.shape[0]
     nseg = int(seg_sizes.numel())
-    sid = seg_ids.long()
-    mn, mx = _seg_minmax(x, seg_ids, nseg + 1)
-    sq = torch.zeros((K, nseg + 1), device=x.device)
-    sq.index_add_(1, sid, x.float() ** 2)
+    be = backend.get(x)
+    native = be is not ref
+    if native:  # segmented min/max and Σx² kernels: no atomics-on-one-address scatter_reduce
+        mn, mx = be.seg_minmax(x, seg_ids, nseg + 1)
+        sq = be.seg_sq_sums(x, seg_ids, nseg + 1)
+    else:
+        mn, mx = _seg_minmax(x, seg_ids, nseg + 1)
+        sq = torch.zeros((K, nseg + 1), device=x.device)
+        sq.index_add_(1, seg_ids.long(), x.float() ** 2)
     sizes = torch.cat([seg_sizes.to(x.device).float(), torch.zeros(1, device=x.device)])
     rms = (sq / sizes.clamp(min=1)).sqrt()
     bits = nnadq_bits(mn, mx, rms, weight)
     levels = (2 ** bits - 1)
     scale = ((mx - mn) / levels).clamp(min=1e-30)
-    lo = mn[:, sid]
-    sc = scale[:, sid]
-    q = torch.round((x.float() - lo) / sc).clamp(min=0)
-    q = torch.minimum(q, levels[:, sid])
-    dq = lo + q * sc
+    if native:
+        lo_seg = torch.where(torch.isfinite(mn), mn, torch.zeros_like(mn))
+        dq = be.nnadq_qdq(x, seg_ids, lo_seg, scale, levels)
+    else:
+        sid = seg_ids.long()
+        lo = mn[:, sid]
+        sc = scale[:, sid]
+        q = torch.round((x.float() - lo) / sc).clamp(min=0)
+        q = torch.minimum(q, levels[:, sid])
+        dq = lo + q * sc
     seg_bytes = (torch.ceil(bits * sizes / 8.0) + 8.0)[:, :nseg]  # [K, nseg]
     if row_seg_mask is not None:
         seg_bytes = seg_bytes * row_seg_mask.float()

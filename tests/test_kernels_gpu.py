@@ -324,3 +324,20 @@ def test_spmm_shared_and_flat(hip):
     yt = hip.spmm(csr.rowptr_t, csr.col_t, csr.val_t, x)
     expt = torch.zeros(K, N, F, device=DEV).index_add_(1, src, x.float()[:, dst] * val[None, :, None])
     _close(yt, expt)
+
+
+def test_nnadq_native_matches_oracle(hip):
+    from distributed_learning_simulator_amd.data.datasets import get_spec
+    from distributed_learning_simulator_amd.models.zoo import build_model
+    from distributed_learning_simulator_amd.ops import quant
+
+    layout = build_model("LeNet5", get_spec("MNIST")).layout
+    seg = layout.segment_ids()
+    sizes = layout.segment_sizes()
+    x = torch.randn(3, layout.padded_size) * layout.valid_mask().float()
+    dq_cpu, wire_cpu, bits_cpu = quant.nnadq_quantize(x, seg, sizes, 0.001)
+    dq_gpu, wire_gpu, bits_gpu = quant.nnadq_quantize(x.to(DEV), seg.to(DEV), sizes.to(DEV), 0.001)
+    valid = layout.valid_mask()
+    torch.testing.assert_close(dq_gpu.cpu()[:, valid], dq_cpu[:, valid], rtol=1e-5, atol=1e-6)
+    assert wire_gpu == wire_cpu
+    torch.testing.assert_close(bits_gpu.cpu(), bits_cpu)
