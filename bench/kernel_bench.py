@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--sweep", action="store_true", help="time every conv_nt tile variant")
     ap.add_argument("--skip-misc", action="store_true", help="conv layers only (no BN/SGD)")
+    ap.add_argument("--gl", action="store_true", help="A/B the LDS-DMA large-tile kernel (conv_gl) vs conv_nt")
     args = ap.parse_args()
     from distributed_learning_simulator_amd.ops import build
 
@@ -79,6 +80,19 @@ def main():
                "fwd_ms": t_f * 1e3, "fwd_tflops": flops / t_f / 1e12,
                "dgrad_ms": t_d * 1e3, "dgrad_tflops": flops / t_d / 1e12,
                "wgrad_ms": t_w * 1e3, "wgrad_tflops": flops / t_w / 1e12}
+        if args.gl:
+            # interleaved A/B in one process: conv_gl forced on vs forced off (TFLOP/s)
+            ab = {"gl": [], "nt": []}
+            for _ in range(3):
+                for mode, key in ((1, "gl"), (0, "nt")):
+                    hip.gl_mode = mode
+                    tf_m = timeit(lambda: hip.conv_fwd(x, w, s, pad), args.iters)
+                    td_m = timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad), args.iters)
+                    ab[key].append((flops / tf_m / 1e12, flops / td_m / 1e12))
+            hip.gl_mode = -1
+            for key in ab:
+                row[f"{key}_fwd_tflops"] = round(max(a for a, _ in ab[key]), 1)
+                row[f"{key}_dgrad_tflops"] = round(max(b for _, b in ab[key]), 1)
         if args.sweep:
             # every NT tile configuration on this shape (fwd / dgrad TFLOP/s per variant id)
             sw = {}

@@ -36,6 +36,21 @@ PYBIND11_MODULE(_dls_hip, m) {
     conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
                stride, pad, variant, S(s));
   });
+  m.def("conv_gl_wanted", &conv_gl_wanted);
+  m.def("conv_gl_fwd", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int K, int rep,
+                          int B, int H, int W, int C, int OH, int OW, int KH, int KW, int stride, int pad, int N,
+                          int relu, ptr s) {
+    conv_gl_fwd(P<const bf16_t>(x), P<const bf16_t>(w), P<bf16_t>(y), P<const bf16_t>(bias), x_cs, y_cs, w_cs, b_cs,
+                K, rep, B, H, W, C, OH, OW, KH, KW, stride, pad, N, relu, S(s));
+  });
+  m.def("conv_weight_flip_t", [](ptr w, ptr wt, long w_cs, int Kw, int Co, int KH, int KW, int Ci, ptr s) {
+    conv_weight_flip_t(P<const bf16_t>(w), P<bf16_t>(wt), w_cs, Kw, Co, KH, KW, Ci, S(s));
+  });
+  m.def("conv_gl_dgrad", [](ptr dy, ptr wt, ptr dx, int K, int rep, int B, int OH, int OW, int Co, int H, int W,
+                            int Ci, int KH, int KW, int stride, int pad, ptr s) {
+    conv_gl_dgrad(P<const bf16_t>(dy), P<const bf16_t>(wt), P<bf16_t>(dx), K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
+                  stride, pad, S(s));
+  });
   m.def("conv_nt_num_variants", &conv_nt_num_variants);
   m.def("conv_nt_default_variant", &conv_nt_default_variant);
   m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,

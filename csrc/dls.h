@@ -57,6 +57,38 @@ struct ConvTNParams {
   FastDiv fd_ohw, fd_ow;  // filled by conv_tn()
 };
 
+// Large-tile conv GEMM fed by the LDS-DMA (conv_gl.hip): K loop over a tap table × 64-channel
+// chunks (C % 64 == 0); A pixel of GEMM row (b, oh, ow) and tap t is
+// (oh·stride − pad_h + tap_dh[t], ow·stride − pad_w + tap_dw[t]); B row n starts at n·ldb, the
+// tap's 64-channel chunk at tap_boff[t] + c0. Output rows remapped as in ConvNTParams.
+struct ConvGLParams {
+  const bf16_t* x;
+  const bf16_t* w;
+  bf16_t* y;
+  const bf16_t* bias;
+  const bf16_t* zero;  // ≥ 128 B of zeros: the DMA source of out-of-image taps (filled by the launcher)
+  long x_cs, y_cs, w_cs, b_cs;
+  int B, H, W, C;  // A image
+  int OH, OW;      // GEMM row grid
+  int stride, pad_h, pad_w;
+  int M, N, ldb, ntaps, cchunks;
+  int tap_dh[9], tap_dw[9], tap_boff[9];
+  int rep, relu;
+  int out_s, out_ph, out_pw, out_H, out_W;
+  FastDiv fd_ohw, fd_ow;
+};
+bool conv_gl_supported(int C, int N, int ntaps);
+// mode: -1 heuristic (env DLS_CONV_GL overrides), 0 never, 1 whenever supported
+bool conv_gl_wanted(int K, int M, int N, int C, int ntaps, int mode);
+void conv_gl_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const bf16_t* bias, long x_cs, long y_cs, long w_cs,
+                 long b_cs, int K, int rep, int B, int H, int W, int C, int OH, int OW, int KH, int KW, int stride,
+                 int pad, int N, int relu, hipStream_t s);
+// Wt[row][ci][kh'][kw'][co] = W[row][co][KH-1-kh'][KW-1-kw'][ci] (dgrad B operand, k-contiguous)
+void conv_weight_flip_t(const bf16_t* w, bf16_t* wt, long w_cs, int Kw, int Co, int KH, int KW, int Ci,
+                        hipStream_t s);
+void conv_gl_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int K, int rep, int B, int OH, int OW, int Co,
+                   int H, int W, int Ci, int KH, int KW, int stride, int pad, hipStream_t s);
+
 // variant < 0: shape heuristic; 0..conv_nt_num_variants()-1: explicit tile config (benchmarks)
 void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s);
 int conv_nt_num_variants();

@@ -80,6 +80,14 @@ def _workspace(numel: int, device) -> torch.Tensor:
 # microbenchmark (bench/kernel_bench.py) sets explicit variant ids to sweep them.
 nt_variant = -1
 tn_variant = -1  # weight-gradient (TN) tile configuration, same convention
+# large-tile LDS-DMA kernel (csrc/conv_gl.hip) for fwd / dgrad: -1 = shape heuristic (or env
+# DLS_CONV_GL), 0 = never, 1 = whenever the shape is supported (tests, A/B benchmarks)
+gl_mode = -1
+
+
+def _gl(K: int, M: int, N: int, C: int, taps: int) -> bool:
+    mode = gl_mode if nt_variant < 0 else 0  # an explicit NT variant (sweeps) bypasses it
+    return bool(_C.conv_gl_wanted(K, M, N, C, taps, mode))
 
 
 def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
@@ -97,6 +105,10 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
     if bias is not None:
         b_cs, _ = _client_view(bias, K)
     M = B * OH * OW
+    if _gl(K, M, Co, C, KH * KW):
+        _C.conv_gl_fwd(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, K, rep, B, H, W, C, OH, OW,
+                       KH, KW, stride, pad, Co, int(relu), _s())
+        return y
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
                pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_variant, _s())
     return y
@@ -111,6 +123,14 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
     w_cs, rep = _client_view(w, K)
     H, W = int(in_hw[0]), int(in_hw[1])
     dx = torch.empty((K, B, H, W, Ci), dtype=BF16, device=dy.device)
+    if (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
+        # (strided dgrad splits into stride² short-K parity classes: conv_nt's smaller tiles win
+        # there, l3a dgrad 447 vs 396 TFLOP/s). Large tiles want a k-contiguous B: one flip+transpose pass over the weight rows
+        # (weights are small next to the activations), then stride² parity-class launches
+        wt = torch.empty((Kw, Ci, KH, KW, Co), dtype=BF16, device=dy.device)
+        _C.conv_weight_flip_t(_p(w), _p(wt), w.stride(0), Kw, Co, KH, KW, Ci, _s())
+        _C.conv_gl_dgrad(_p(dy), _p(wt), _p(dx), K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, _s())
+        return dx
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
     _C.conv_dgrad(_p(dy), _p(w), _p(dx), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, nt_variant,

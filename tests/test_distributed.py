@@ -68,8 +68,14 @@ def test_two_ranks_match_single_rank(tmp_path, algo, extra):
     from distributed_learning_simulator_amd.parallel.comm import Comm
     from distributed_learning_simulator_amd.session import Session
 
-    single = Session(_cfg(algo, str(tmp_path / "s"), extra), comm=Comm())
-    res1 = single.run()
+    # same intra-op thread count as the spawned ranks: fp32 reduction order then matches
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        single = Session(_cfg(algo, str(tmp_path / "s"), extra), comm=Comm())
+        res1 = single.run()
+    finally:
+        torch.set_num_threads(nthreads)
     theta1 = single.server.global_parameter
     outs = _run_world(2, algo, str(tmp_path / "d"), extra)
     (r0, th0, perf0, up0), (r1, th1, perf1, up1) = outs

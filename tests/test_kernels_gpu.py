@@ -95,6 +95,62 @@ def test_conv_tn_every_variant(hip, case):
         hip.tn_variant = -1
 
 
+GL_CASES = [
+    # K, B, H, W, Ci, Co, k, stride, pad — csrc/conv_gl.hip (forced on: gl_mode = 1)
+    (2, 2, 8, 8, 64, 128, 3, 1, 1),      # M = 128: a partial 256-row tile
+    (2, 3, 9, 9, 64, 128, 3, 2, 1),      # stride 2, odd size: 4 dgrad parity classes
+    (2, 2, 8, 8, 64, 128, 1, 2, 0),      # 1x1 stride 2: three empty dgrad classes (dx = 0)
+    (1, 4, 16, 16, 128, 256, 3, 1, 1),   # 256-wide tiles, 4 row tiles
+    (2, 2, 7, 7, 128, 384, 3, 1, 1),     # N tail of a 256-wide tile
+    (2, 2, 8, 8, 128, 64, 3, 1, 1),      # N = 64 forward; dgrad N = Ci = 128
+    (3, 2, 6, 6, 64, 200, 3, 1, 1),      # N % 8 == 0 tail (dgrad C = 200: falls back to conv_nt)
+    (2, 8, 16, 16, 128, 128, 3, 1, 1),   # M = 2048 per client
+]
+
+
+@pytest.mark.parametrize("case", GL_CASES)
+def test_conv_gl_fwd_dgrad(hip, case):
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(1)
+    x = _bf(K, B, H, W, Ci)
+    w = _bf(K, Co, k, k, Ci, scale=0.2)
+    OH = (H + 2 * p - k) // s + 1
+    assert hip._C.conv_gl_wanted(K, B * OH * OH, Co, Ci, k * k, 1)
+    old = hip.gl_mode
+    hip.gl_mode = 1
+    try:
+        y = hip.conv_fwd(x, w, s, p)
+        _close(y, ref.conv_fwd(x.float(), w.float(), s, p))
+        dy = _bf(*y.shape)
+        dx = hip.conv_dgrad(dy, w, (H, W), s, p)
+        _close(dx, ref.conv_dgrad(dy.float(), w.float(), (H, W), s, p))
+        # the same results as the register-staged kernels
+        hip.gl_mode = 0
+        _close(hip.conv_fwd(x, w, s, p), y, tol=1e-2)
+    finally:
+        hip.gl_mode = old
+
+
+def test_conv_gl_shared_weights_rep(hip):
+    x = _bf(6, 4, 8, 8, 64)
+    w = _bf(2, 128, 3, 3, 64, scale=0.2)
+    old = hip.gl_mode
+    hip.gl_mode = 1
+    try:
+        _close(hip.conv_fwd(x, w, 1, 1), ref.conv_fwd(x.float(), w.float(), 1, 1))
+    finally:
+        hip.gl_mode = old
+
+
+def test_conv_weight_flip_t(hip):
+    w = _bf(3, 72, 3, 3, 136)  # tails in both 64-wide tile dims
+    wt = torch.empty((3, 136, 3, 3, 72), dtype=torch.bfloat16, device=DEV)
+    hip._C.conv_weight_flip_t(w.data_ptr(), wt.data_ptr(), w.stride(0), 3, 72, 3, 3, 136,
+                              torch.cuda.current_stream().cuda_stream)
+    exp = w.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous()
+    assert torch.equal(wt, exp)
+
+
 def test_conv_shared_weights_rep(hip):
     # eval path: 6 virtual clients share 2 weight rows (rep = 3)
     x = _bf(6, 2, 8, 8, 16)
