@@ -76,6 +76,24 @@ class RoundSchedule:
     epoch_end: list[int]  # step index after which epoch e ends
     steps: int
     K: int
+    # [S, K, B + 4] int32: idx | count | active | first | lr (fp32 bits) — one row per step, the
+    # single copy a graph-replayed step needs (see CohortTrainer._train_graphed)
+    packed: torch.Tensor | None = None
+
+
+class _StepGraph:
+    """One captured lock-step training step of a K-client cohort: every sub-cohort stream,
+    forward + backward + optimizer, replayed as a single HIP graph launch. Inputs come from a
+    static slot (one D2D copy per step); per-client loss/accuracy sums accumulate in static
+    buffers that the host drains at epoch ends."""
+
+    def __init__(self, K: int, B: int, device):
+        self.slot = torch.zeros((K, B + 4), dtype=torch.int32, device=device)
+        self.loss = torch.zeros(K, dtype=torch.float32, device=device)
+        self.correct = torch.zeros_like(self.loss)
+        self.samples = torch.zeros_like(self.loss)
+        self.graph = None
+        self.eager_steps = 0
 
 
 def _nullctx():
@@ -107,6 +125,11 @@ class CohortTrainer:
         self.debug = False  # `debug` config: per-step NaN/Inf scan (synchronises every step)
         self.num_streams = int(os.environ.get("DLS_STREAMS", "3"))  # concurrent sub-cohorts on GPU
         self._stream_pool: list = []
+        # HIP-graph replay of whole training steps (DLS_GRAPHS=0 disables): a ResNet-18 step is
+        # ≈400 launches per sub-cohort, which at the 8-GPU per-rank load (13 clients) costs more
+        # host time than the GPU needs to run them
+        self.use_graphs = os.environ.get("DLS_GRAPHS", "1") != "0"
+        self._graphs: dict = {}
         self.hooks = HookRegistry()
         self.adam_step_count = torch.zeros(capacity, dtype=torch.float32, device=self.device)
         self.graph = dataset_collection.graph
@@ -185,8 +208,12 @@ class CohortTrainer:
                 first[s] = active[s] & ~seen
             seen |= active[s]
         dev = self.device
+        packed = None
+        if self._graphs_enabled():
+            packed = torch.cat([idx, counts[..., None], active.to(torch.int32)[..., None],
+                                first.to(torch.int32)[..., None], lr.view(torch.int32)[..., None]], dim=2).to(dev)
         return RoundSchedule(idx.to(dev), counts.to(dev), active.to(dev), first.to(dev), lr.to(dev),
-                             epoch_end, S, K)
+                             epoch_end, S, K, packed)
 
     # --------------------------------------------------------------------- train
     def forward_loss(self, K: int, x, labels, valid, shared: bool = False, grad_rows=None, row0: int = 0):
@@ -268,6 +295,12 @@ class CohortTrainer:
             self._stream_pool.append(torch.cuda.Stream(device=self.device))
         return self._stream_pool[:n]
 
+    def _graphs_enabled(self) -> bool:
+        """Graph replay covers the image models' plain training step (no per-step hooks, no
+        debug scans); text/graph models keep the eager path."""
+        return (self.use_graphs and self.device.type == "cuda" and self.model.input_kind == "image"
+                and not self.debug)
+
     def train(self, schedule: RoundSchedule, executor=None, stats: TrainStats | None = None,
               epoch_base: int = 0) -> TrainStats:
         K = schedule.K
@@ -277,6 +310,9 @@ class CohortTrainer:
         parts = self._sub_cohorts(K)
         if self.hooks.has_hook(ExecutorHookPoint.OPTIMIZER_STEP) or self.model.input_kind == "graph":
             parts = [(0, K)]  # step hooks see the whole cohort; graph halos couple the clients
+        elif (schedule.packed is not None and self._graphs_enabled()
+              and not self.hooks.has_hook(ExecutorHookPoint.AFTER_BATCH)):
+            return self._train_graphed(schedule, parts, executor, stats, epoch_base)
         multi = len(parts) > 1
         streams = self._streams(len(parts)) if multi else [None]
         main = torch.cuda.current_stream(self.device) if multi else None
@@ -342,6 +378,91 @@ class CohortTrainer:
                                 valid=valid, K=K)
             else:
                 self.optimizer_step(K, schedule.lr[s, a:b], schedule.active[s, a:b], schedule.first[s, a:b], row0=a)
+
+    # ------------------------------------------------------------- graph replay
+    def _slot_step(self, sg: _StepGraph, ds, a: int, b: int) -> None:
+        """One training step of rows [a, b) reading its inputs from the static slot."""
+        B = self.hyper.batch_size
+        slot = sg.slot[a:b]
+        idx = slot[:, :B]
+        valid = slot[:, B].contiguous()
+        active = slot[:, B + 1].contiguous().bool()
+        first = slot[:, B + 2].contiguous().bool()
+        lr = slot[:, B + 3].contiguous().view(torch.float32)
+        x = self._gather(ds, idx)
+        labels = ds.gather_labels(idx)
+        loss, correct = self.forward_loss(b - a, x, labels, valid, row0=a)
+        loss.sum().backward()
+        with torch.no_grad():
+            vf = valid.float()
+            sg.loss[a:b] += loss.detach() * vf
+            sg.correct[a:b] += correct
+            sg.samples[a:b] += vf
+            self.optimizer_step(b - a, lr, active, first, row0=a)
+
+    def _train_graphed(self, schedule: RoundSchedule, parts, executor, stats: TrainStats,
+                       epoch_base: int) -> TrainStats:
+        """Same step sequence as `train`, each step one HIP-graph replay. The first step of a
+        new (K, sub-cohort split) runs eagerly (allocator and lazy-init warm-up), the second is
+        captured — capture records without executing, so it is replayed right away — and every
+        later step, in this and later rounds, is one slot copy + one graph launch."""
+        K = schedule.K
+        ds = self.dc.train
+        B = self.hyper.batch_size
+        key = (K, B, tuple(parts))
+        sg = self._graphs.get(key)
+        if sg is None:
+            sg = self._graphs[key] = _StepGraph(K, B, self.device)
+        streams = self._streams(len(parts))
+
+        def run_parts():
+            cur = torch.cuda.current_stream(self.device)
+            for st in streams:
+                st.wait_stream(cur)
+            for (a, b), st in zip(parts, streams):
+                with torch.cuda.stream(st):
+                    self._slot_step(sg, ds, a, b)
+            for st in streams:
+                cur.wait_stream(st)
+
+        sg.loss.zero_()
+        sg.correct.zero_()
+        sg.samples.zero_()
+        self.hooks.exec(ExecutorHookPoint.BEFORE_EXECUTE, executor=executor)
+        e = 0
+        try:
+            for s in range(schedule.steps):
+                sg.slot.copy_(schedule.packed[s])
+                if sg.graph is not None:
+                    sg.graph.replay()
+                elif sg.eager_steps < 1:
+                    run_parts()
+                    sg.eager_steps += 1
+                else:
+                    # the eager step's cached blocks go back to the driver so the graph's private
+                    # pool can take them (else activation memory is held twice)
+                    torch.cuda.synchronize(self.device)
+                    torch.cuda.empty_cache()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        run_parts()
+                    sg.graph = g
+                    g.replay()
+                if s + 1 == schedule.epoch_end[e]:
+                    stats.loss_sum[e] += sg.loss
+                    stats.correct[e] += sg.correct
+                    stats.samples[e] += sg.samples
+                    sg.loss.zero_()
+                    sg.correct.zero_()
+                    sg.samples.zero_()
+                    if self.hooks.has_hook(ExecutorHookPoint.AFTER_EPOCH):
+                        self.hooks.exec(ExecutorHookPoint.AFTER_EPOCH, executor=executor, epoch=epoch_base + e + 1,
+                                        stats=stats, local_epoch=e)
+                    e += 1
+        except StopExecutingException:
+            pass
+        self.hooks.exec(ExecutorHookPoint.AFTER_EXECUTE, executor=executor, stats=stats)
+        return stats
 
     # ------------------------------------------------------------------ evaluate
     @torch.no_grad()
