@@ -46,7 +46,12 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--cohort", type=int, default=0)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="diagnostic: time rank 0's share of an N-rank round alone on one GPU "
+                         "(collectives are no-ops; not the benchmark contract)")
     args = ap.parse_args()
+    if args.emulate_world and args.workload != "fedavg_resnet18":
+        ap.error("--emulate-world supports the fedavg_resnet18 workload only")
 
     if args.backend == "torch":
         os.environ["DLS_BACKEND"] = "torch"
@@ -70,6 +75,12 @@ def main() -> None:
                 time.sleep(1)
 
     comm = init_distributed()
+    emulated = args.emulate_world > 1
+    if emulated:
+        from distributed_learning_simulator_amd.parallel.comm import EmulatedRankComm
+
+        assert comm.world == 1, "--emulate-world runs as a single process"
+        comm = EmulatedRankComm(0, args.emulate_world, comm.device)
     rounds = args.warmup + args.steps
     wl = workload_config(args, rounds)
     cfg = config_from_dict(wl["config"])
@@ -93,7 +104,7 @@ def main() -> None:
         theta = sess.run_one_round(theta)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    if comm.world > 1:
+    if comm.world > 1 and not emulated:
         t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -106,7 +117,7 @@ def main() -> None:
             "metric": wl["metric"],
             "value": args.steps / elapsed,
             "unit": "rounds/s",
-            "n_gpus": comm.world,
+            "n_gpus": 1 if emulated else comm.world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms,
@@ -117,12 +128,14 @@ def main() -> None:
             "data": wl["data"],
             "comm_bytes_per_round": bytes_per_round,
             "test_accuracy_last_round": acc,
-            "samples_per_s": wl["samples_per_round"](sess) / (elapsed / args.steps),
+            # (emulated: this rank trains 1/N of the round's samples)
+            "samples_per_s": wl["samples_per_round"](sess) / (comm.world if emulated else 1) / (elapsed / args.steps),
             "config": {
                 "model": cfg.model_name, "algo": cfg.distributed_algorithm, "clients": cfg.worker_number,
                 "local_epochs": cfg.epoch, "global_batch": cfg.batch_size * cfg.worker_number,
                 "per_client_batch": cfg.batch_size, "seq_len": wl.get("seq_len"),
-                "parallelism": f"client-dp{comm.world}", "backend": args.backend, "workload": args.workload,
+                "parallelism": f"emulated-rank0-of-{comm.world}" if emulated else f"client-dp{comm.world}",
+                "backend": args.backend, "workload": args.workload,
             },
         }
         print(json.dumps(out), flush=True)

@@ -131,6 +131,9 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("weighted_sum", [](ptr x, ptr w, ptr out, int K, long Pn, long ld, ptr s) {
     weighted_sum(P<const float>(x), P<const float>(w), P<float>(out), K, Pn, ld, S(s));
   });
+  m.def("mix_rows", [](ptr x, ptr w, ptr out, int K, int M, long Pn, long ld, long ld_out, ptr s) {
+    mix_rows(P<const float>(x), P<const float>(w), P<bf16_t>(out), K, M, Pn, ld, ld_out, S(s));
+  });
   m.def("masked_weighted_sum", [](ptr x, ptr mask, ptr w, ptr num, ptr den, int K, long Pn, long ld, ptr s) {
     masked_weighted_sum(P<const float>(x), P<const uint8_t>(mask), P<const float>(w), P<float>(num), P<float>(den), K, Pn,
                         ld, S(s));

@@ -139,6 +139,8 @@ void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shad
 void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s);
 void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s);
 void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s);
+void mix_rows(const float* x, const float* w, bf16_t* out, int K, int M, long P, long ld, long ld_out,
+              hipStream_t s);
 void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
                          long ld, hipStream_t s);
 void dropout_mask(uint8_t* mask, int K, long P, float p, const uint32_t* seeds, hipStream_t s);

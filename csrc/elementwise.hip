@@ -278,6 +278,47 @@ __global__ void __launch_bounds__(256) weighted_sum_kernel(const float* __restri
   }
 }
 
+// Subset-model mixing for Shapley utilities: out[m, :] = Σ_k W[m, k]·x[k, :] for a
+// slice of ≤ 32 subset models per blockIdx.y, written straight in the bf16 compute dtype the
+// batched evaluation consumes. Each x row is read once per 32 models (a per-subset weighted
+// sum re-reads all K rows for every model); fp32 accumulation, W staged in LDS.
+constexpr int MIX_M = 32;
+constexpr int MIX_KMAX = 256;
+__global__ void __launch_bounds__(256) mix_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                       bf16_t* __restrict__ out, int K, int M, long P4, long ld,
+                                                       long ld_out) {
+  __shared__ float wl[MIX_M * MIX_KMAX];
+  const int m0 = blockIdx.y * MIX_M;
+  const int mn = min(MIX_M, M - m0);
+  for (int t = threadIdx.x; t < MIX_M * K; t += blockDim.x) wl[t] = t < mn * K ? w[(long)m0 * K + t] : 0.f;
+  __syncthreads();
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
+    float acc[MIX_M][4];
+#pragma unroll
+    for (int m = 0; m < MIX_M; ++m) acc[m][0] = acc[m][1] = acc[m][2] = acc[m][3] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(x + (long)k * ld)[i];
+#pragma unroll
+      for (int m = 0; m < MIX_M; ++m) {
+        const float c = wl[m * K + k];  // wave-uniform address: LDS broadcast
+        acc[m][0] = fmaf(c, v.x, acc[m][0]);
+        acc[m][1] = fmaf(c, v.y, acc[m][1]);
+        acc[m][2] = fmaf(c, v.z, acc[m][2]);
+        acc[m][3] = fmaf(c, v.w, acc[m][3]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MIX_M; ++m) {
+      if (m < mn) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(acc[m][0]) | ((uint32_t)f2bf(acc[m][1]) << 16);
+        u.y = (uint32_t)f2bf(acc[m][2]) | ((uint32_t)f2bf(acc[m][3]) << 16);
+        reinterpret_cast<uint2*>(out + (long)(m0 + m) * ld_out)[i] = u;
+      }
+    }
+  }
+}
+
 __global__ void masked_weighted_sum_kernel(const float* __restrict__ x, const uint8_t* __restrict__ mask,
                                            const float* __restrict__ w, float* __restrict__ num,
                                            float* __restrict__ den, int K, long P, long ld) {
@@ -529,6 +570,16 @@ void delta_rows(const float* theta, const float* base, float* out, int K, long P
 
 void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s) {
   hipLaunchKernelGGL(weighted_sum_kernel, dim3(grid_for(P / 4, 256, 8192)), dim3(256), 0, s, x, w, out, K, P / 4, ld);
+}
+
+void mix_rows(const float* x, const float* w, bf16_t* out, int K, int M, long P, long ld, long ld_out,
+              hipStream_t s) {
+  if (K > MIX_KMAX || M <= 0) {  // the wrapper (ops/hip.py) routes larger K elsewhere
+    DLS_CHECK(hipErrorInvalidValue);
+    return;
+  }
+  dim3 grid(grid_for(P / 4, 256, 2048), cdiv(M, MIX_M));
+  hipLaunchKernelGGL(mix_rows_kernel, grid, dim3(256), 0, s, x, w, out, K, M, P / 4, ld, ld_out);
 }
 
 void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,

@@ -74,15 +74,16 @@ class ShapleyValueAlgorithm(FedAVGAlgorithm):
         return all_ids, torch.stack([rows[c] for c in all_ids]), [all_sizes[c] for c in all_ids]
 
     def _subset_models(self, subsets, ids, rows, sizes) -> torch.Tensor:
+        """All subset models of a chunk in one pass: W[M, K] · rows (dataset-size weights
+        renormalised within each subset, reference `aggregation_algorithm.py:14-50`), emitted in
+        the evaluation's compute dtype."""
         pos = {c: i for i, c in enumerate(ids)}
-        out = torch.empty((len(subsets), rows.shape[1]), dtype=torch.float32, device=rows.device)
+        W = torch.zeros((len(subsets), len(ids)), dtype=torch.float32)
         for j, s in enumerate(subsets):
-            w = torch.zeros(len(ids), dtype=torch.float32)
             tot = sum(sizes[pos[c]] for c in s)
             for c in s:
-                w[pos[c]] = sizes[pos[c]] / tot
-            out[j] = fl.weighted_sum(rows, w.to(rows.device))
-        return out
+                W[j, pos[c]] = sizes[pos[c]] / tot
+        return fl.mix_rows(rows, W.to(rows.device), self.server.session.compute_dtype)
 
     def aggregate_worker_data(self, old_parameter: torch.Tensor) -> FlatParameterMessage:
         server = self.server
@@ -102,12 +103,13 @@ class ShapleyValueAlgorithm(FedAVGAlgorithm):
         chunk = int(self.config.algorithm_kwargs.get("sv_eval_batch", 32))
 
         def batch_metric(subsets):
+            # chunks are queued back to back; the host reads the utilities once at the end
             vals = []
             for s0 in range(0, len(subsets), chunk):
                 models = self._subset_models(subsets[s0 : s0 + chunk], ids, rows, sizes)
-                _, acc = server.get_metrics_many(models)
-                vals.extend(acc if self.metric_type == "accuracy" else _)
-            return vals
+                loss, acc = server.session.evaluate_tensors(models)
+                vals.append(acc if self.metric_type == "accuracy" else loss)
+            return torch.cat(vals).tolist() if vals else []
 
         self.sv_algorithm.set_batch_metric_function(batch_metric)
         self.sv_algorithm.compute(round_number=rnd)

@@ -102,7 +102,7 @@ class MultiRoundShapleyValue(_Base):
 class GTGShapleyValue(_Base):
     def __init__(self, players, last_round_metric=0.0, eps: float = 0.001, round_trunc_threshold: float = 0.001,
                  max_iterations: int = 30, min_iterations: int = 3, converge_threshold: float = 0.05, seed: int = 0,
-                 **kwargs):
+                 parallel_iterations: int = 4, **kwargs):
         super().__init__(players, last_round_metric, **kwargs)
         self.eps = eps
         self.round_trunc_threshold = round_trunc_threshold
@@ -110,6 +110,29 @@ class GTGShapleyValue(_Base):
         self.min_iterations = min_iterations
         self.converge_threshold = converge_threshold
         self.seed = seed
+        # iterations whose permutations advance together: one utility batch per position covers
+        # them all (≤ parallel_iterations·n subset models). Results equal the one-iteration-at-a-
+        # time order exactly (same permutations, convergence checked per iteration afterwards);
+        # iterations past the converged one are evaluated but discarded.
+        self.parallel_iterations = max(1, int(parallel_iterations))
+
+    def _marginals(self, perms: list[list], v0: float, vN: float) -> list[list[tuple]]:
+        """Position-by-position lock-step over `perms` with within-round truncation: one batched
+        utility evaluation per position. Returns per permutation [(player, marginal), ...]."""
+        n = len(self.players)
+        v_prev = [v0] * len(perms)
+        out: list[list[tuple]] = [[] for _ in perms]
+        for j in range(n):
+            live = [abs(vN - v_prev[i]) >= self.eps for i in range(len(perms))]
+            self.values([frozenset(perm[: j + 1]) for i, perm in enumerate(perms) if live[i] and j + 1 < n])
+            for i, perm in enumerate(perms):
+                if live[i]:
+                    v = self._cache[frozenset(perm[: j + 1])] if j + 1 < n else vN
+                else:
+                    v = v_prev[i]  # within-round truncation: marginal 0
+                out[i].append((perm[j], v - v_prev[i]))
+                v_prev[i] = v
+        return out
 
     def compute(self, round_number: int) -> None:
         self._cache.clear()
@@ -125,34 +148,34 @@ class GTGShapleyValue(_Base):
         sums = {p: 0.0 for p in players}
         counts = {p: 0 for p in players}
         prev_means: dict | None = None
-        history = []
-        for it in range(1, self.max_iterations + 1):
+        means = dict(sums)
+        it = 0
+        done = False
+        while not done and it < self.max_iterations:
+            g = min(self.parallel_iterations, self.max_iterations - it)
             perms = []
-            for first in players:  # guided sampling: each player leads one permutation
-                rest = [p for p in players if p != first]
-                rng.shuffle(rest)
-                perms.append([first] + rest)
-            v_prev = [v0] * n
-            for j in range(n):
-                need = [frozenset(perm[: j + 1]) for i, perm in enumerate(perms) if abs(vN - v_prev[i]) >= self.eps]
-                self.values(need)
-                for i, perm in enumerate(perms):
-                    p = perm[j]
-                    if abs(vN - v_prev[i]) >= self.eps:
-                        v = self._cache[frozenset(perm[: j + 1])] if j + 1 < n else vN
-                    else:
-                        v = v_prev[i]  # within-round truncation: marginal 0
-                    sums[p] += v - v_prev[i]
-                    counts[p] += 1
-                    v_prev[i] = v
-            means = {p: sums[p] / max(counts[p], 1) for p in players}
-            if prev_means is not None:
-                denom = sum(abs(v) for v in means.values()) / n + 1e-12
-                change = sum(abs(means[p] - prev_means[p]) for p in players) / n / denom
-                history.append(change)
-                if it >= self.min_iterations and change < self.converge_threshold:
-                    break
-            prev_means = means
+            for _ in range(g):
+                for first in players:  # guided sampling: each player leads one permutation
+                    rest = [p for p in players if p != first]
+                    rng.shuffle(rest)
+                    perms.append([first] + rest)
+            marg = self._marginals(perms, v0, vN)
+            for t in range(g):  # iterations in order: convergence exactly as if run one by one
+                it += 1
+                block = marg[t * n : (t + 1) * n]
+                for j in range(n):  # (position, permutation) order of the sequential loop
+                    for contrib in block:
+                        p, d = contrib[j]
+                        sums[p] += d
+                        counts[p] += 1
+                means = {p: sums[p] / max(counts[p], 1) for p in players}
+                if prev_means is not None:
+                    denom = sum(abs(v) for v in means.values()) / n + 1e-12
+                    change = sum(abs(means[p] - prev_means[p]) for p in players) / n / denom
+                    if it >= self.min_iterations and change < self.converge_threshold:
+                        done = True
+                        break
+                prev_means = means
         get_logger().info("GTG round %s: %d iterations, %d subset evaluations", round_number, it, self.evaluations)
         self._finish(means)
 

@@ -7,6 +7,7 @@
 | broadcast_rows       | load_parameters of θ_g into every client (`util/model.py:6-23`)|
 | delta_rows           | ModelCache.get_parameter_diff (K4, `util/model_cache.py:30-36`)|
 | weighted_sum         | FedAVGAlgorithm accumulate (K6, `fed_avg_algorithm.py:39-52`)  |
+| mix_rows             | Shapley subset models (K8, `aggregation_algorithm.py:30-50`)   |
 | masked_weighted_sum  | FedDropoutAvg aggregation (K10, `fed_dropout_avg/algorithm.py`)|
 | dropout_mask         | FedDropoutAvg Bernoulli mask (K9, `fed_dropout_avg/worker.py`) |
 | block_sq_norms       | OBD per-block ‖Δ‖ (K11, `obd_algorithm.py:129-145`)            |
@@ -62,6 +63,12 @@ def delta_rows(theta_rows, base, out=None):
 def weighted_sum(x, w):
     """Σ_k w_k x[k,:] -> fp32 [P] (fp64 accumulation)."""
     return backend.get(x).weighted_sum(x, w)
+
+
+def mix_rows(x, w, out_dtype):
+    """Rows of W[M, K] · x[K, P] in `out_dtype`: M weighted combinations of the K client rows
+    in one pass (Shapley subset models, K8)."""
+    return backend.get(x).mix_rows(x, w, out_dtype)
 
 
 def masked_weighted_sum(x, mask, w):

@@ -460,6 +460,21 @@ def weighted_sum(x, w):
     return out
 
 
+def mix_rows(x, w, out_dtype=BF16):
+    """[M, P] = W[M, K] · x[K, P]: subset models for Shapley utilities, emitted in bf16 (the
+    eval compute dtype) by one native pass that reads each x row once per 32 models."""
+    K, P, ld = _row_args(x)
+    M = w.shape[0]
+    assert w.shape == (M, K)
+    if out_dtype != BF16 or K > 256:
+        return (w.float().to(x.device) @ x).to(out_dtype)  # plain library GEMM
+    w = w.float().to(x.device).contiguous()
+    out = torch.empty((M, P), dtype=BF16, device=x.device)
+    if M:
+        _C.mix_rows(_p(x), _p(w), _p(out), K, M, P, ld, P, _s())
+    return out
+
+
 def masked_weighted_sum(x, mask, w):
     K, P, ld = _row_args(x)
     mask = mask.to(torch.uint8)

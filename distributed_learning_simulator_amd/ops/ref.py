@@ -354,6 +354,11 @@ def weighted_sum(x, w, base=None):
     return acc.float()
 
 
+def mix_rows(x, w, out_dtype=torch.float32):
+    """Subset models W[M, K] · x[K, P] (fp64 accumulation), cast to `out_dtype`."""
+    return (w.double().to(x.device) @ x.double()).to(out_dtype)
+
+
 def masked_weighted_sum(x, mask, w):
     """FedDropoutAvg: numerator Σ w_k m_k x_k and per-element denominator Σ w_k m_k."""
     wm = mask.double() * w.double().to(x.device)[:, None]

@@ -99,6 +99,39 @@ class Comm:
                 dist.barrier()
 
 
+class EmulatedRankComm(Comm):
+    """Rank `rank` of a `world`-rank job run ALONE on one device, for timing only: the rank
+    hosts exactly the clients and test shard it would host in the real job, and every
+    collective is a local no-op (sums are this rank's partials). `bench.py --emulate-world N`
+    uses it to measure one rank's share of the N-GPU round on a single GPU (the per-rank load
+    behind the scaling curve), without the xGMI collectives (≈0.1–0.5 ms per round)."""
+
+    def all_reduce_(self, t, op=dist.ReduceOp.SUM):
+        return t
+
+    def all_reduce_many_(self, tensors):
+        return tensors
+
+    def all_gather(self, t):
+        return [t] + [torch.zeros_like(t) for _ in range(self.world - 1)]
+
+    def all_gather_object(self, obj):
+        return [obj] * self.world
+
+    def broadcast_(self, t, src: int = 0):
+        return t
+
+    def broadcast_object(self, obj, src: int = 0):
+        return obj
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
+        out.zero_()
+        return out
+
+    def barrier(self) -> None:
+        pass
+
+
 _COMM: Comm | None = None
 
 

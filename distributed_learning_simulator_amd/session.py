@@ -115,13 +115,20 @@ class Session:
     def local_clients(self, selected: list[int]) -> list[int]:
         return list(selected[self.comm.rank :: self.comm.world])
 
-    def evaluate(self, rows: torch.Tensor):
-        """Sharded test evaluation of M parameter rows; returns (loss [M], acc [M]) lists."""
+    def evaluate_tensors(self, rows: torch.Tensor):
+        """Sharded test evaluation of M parameter rows (fp32 or compute dtype); returns device
+        tensors (loss [M], acc [M]) without synchronising the host."""
         ls, cs, n = self.trainer.evaluate(rows, batch_size=self.config.eval_batch_size or None,
                                           shard=(self.comm.rank, self.comm.world))
         both = torch.stack([ls, cs])
         self.comm.all_reduce_(both)
-        both = (both / n).cpu()
+        both = both / n
+        return both[0], both[1]
+
+    def evaluate(self, rows: torch.Tensor):
+        """Sharded test evaluation of M parameter rows; returns (loss [M], acc [M]) lists."""
+        loss, acc = self.evaluate_tensors(rows)
+        both = torch.stack([loss, acc]).cpu()
         return both[0].tolist(), both[1].tolist()
 
     def sync(self) -> None:

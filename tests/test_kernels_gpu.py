@@ -299,6 +299,17 @@ def test_sgd_and_fl_math(hip):
     torch.testing.assert_close(d1, d2)
 
 
+@pytest.mark.parametrize("K,M", [(5, 3), (32, 32), (32, 70), (100, 33)])
+def test_mix_rows(hip, K, M):
+    P = 4096 + 48
+    x = torch.randn(K, P, device=DEV)
+    w = torch.rand(M, K, device=DEV)
+    w = w / w.sum(1, keepdim=True)
+    out = hip.mix_rows(x, w)
+    assert out.dtype == torch.bfloat16 and out.shape == (M, P)
+    torch.testing.assert_close(out.float(), ref.mix_rows(x, w, torch.float32), rtol=1e-2, atol=1e-2)
+
+
 def test_compression_kernels(hip):
     from distributed_learning_simulator_amd.ops import fl
 
