@@ -89,4 +89,4 @@ def test_graph_replayed_steps_match_eager(hip):
     # reproducible, and a diverging run amplifies that noise)
     torch.testing.assert_close(loss_g, loss_e, rtol=1e-2, atol=1e-2)
     diff = (th_g - th_e).abs()
-    assert diff.max().item() < 1e-2 and diff.mean().item() < 1e-5, (diff.max().item(), diff.mean().item())
+    assert diff.max().item() < 1e-2 and diff.mean().item() < 1e-4, (diff.max().item(), diff.mean().item())
