@@ -128,6 +128,9 @@ def main() -> None:
             "data": wl["data"],
             "comm_bytes_per_round": bytes_per_round,
             "test_accuracy_last_round": acc,
+            # mean per-round phase split (HIP-event timed, Session.run_one_round)
+            "phase_s": {k: sum(r.get(k, 0.0) for r in rows) / max(len(rows), 1)
+                        for k in ("train_s", "aggregate_s", "eval_broadcast_s") if rows and k in rows[0]},
             # (emulated: this rank trains 1/N of the round's samples)
             "samples_per_s": wl["samples_per_round"](sess) / (comm.world if emulated else 1) / (elapsed / args.steps),
             "config": {

@@ -31,9 +31,9 @@ PYBIND11_MODULE(_dls_hip, m) {
     p.b_kmajor = b_kmajor;
     conv_nt(p, K, variant, S(s));
   });
-  m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
+  m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, ptr acc, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
                          int W, int Ci, int KH, int KW, int stride, int pad, int variant, ptr s) {
-    conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
+    conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), P<const bf16_t>(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
                stride, pad, variant, S(s));
   });
   m.def("conv_gl_wanted", &conv_gl_wanted);
@@ -46,9 +46,9 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_weight_flip_t", [](ptr w, ptr wt, long w_cs, int Kw, int Co, int KH, int KW, int Ci, ptr s) {
     conv_weight_flip_t(P<const bf16_t>(w), P<bf16_t>(wt), w_cs, Kw, Co, KH, KW, Ci, S(s));
   });
-  m.def("conv_gl_dgrad", [](ptr dy, ptr wt, ptr dx, int K, int rep, int B, int OH, int OW, int Co, int H, int W,
+  m.def("conv_gl_dgrad", [](ptr dy, ptr wt, ptr dx, ptr acc, int K, int rep, int B, int OH, int OW, int Co, int H, int W,
                             int Ci, int KH, int KW, int stride, int pad, ptr s) {
-    conv_gl_dgrad(P<const bf16_t>(dy), P<const bf16_t>(wt), P<bf16_t>(dx), K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
+    conv_gl_dgrad(P<const bf16_t>(dy), P<const bf16_t>(wt), P<bf16_t>(dx), P<const bf16_t>(acc), K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
                   stride, pad, S(s));
   });
   m.def("conv_nt_num_variants", &conv_nt_num_variants);

@@ -39,6 +39,16 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   }
 }
 
+__device__ __forceinline__ uint4 pack8(const float* f);
+// 8 bf16 + 8 bf16 (fp32 add, one rounding): epilogue accumulate of a second gradient branch
+__device__ __forceinline__ uint4 add_bf16x8(const uint4& a, const uint4& b) {
+  float fa[8], fb[8];
+  unpack8(a, fa);
+  unpack8(b, fb);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[i] += fb[i];
+  return pack8(fa);
+}
 __device__ __forceinline__ uint4 pack8(const float* f) {
   uint32_t w[4];
 #pragma unroll

@@ -166,6 +166,7 @@ __global__ void __launch_bounds__(512) conv_gl_kernel(ConvGLParams p) {
 
   // ---- epilogue: bias (+ReLU) → bf16 → per-wave 32-row LDS slab → 16-B coalesced stores
   bf16_t* __restrict__ y = p.y + (long)client * p.y_cs;
+  const bf16_t* accp = p.acc ? p.acc + (long)client * p.y_cs : nullptr;
   const bf16_t* bias = p.bias ? p.bias + (long)(client / p.rep) * p.b_cs : nullptr;
   float bvals[TN];
 #pragma unroll
@@ -200,11 +201,14 @@ __global__ void __launch_bounds__(512) conv_gl_kernel(ConvGLParams p) {
         row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
       }
       bf16_t* dst = y + row * p.N + n;
+      const bf16_t* acc_row = accp ? accp + row * p.N + n : nullptr;
       const bf16_t* src = slab + r * SW + cc;
       if (vec_ok && n + 8 <= p.N) {
-        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+        uint4 v = *reinterpret_cast<const uint4*>(src);
+        if (acc_row) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(acc_row));
+        *reinterpret_cast<uint4*>(dst) = v;
       } else {
-        for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = src[q];
+        for (int q = 0; q < 8 && n + q < p.N; ++q) dst[q] = acc_row ? f2bf(bf2f(src[q]) + bf2f(acc_row[q])) : src[q];
       }
     }
     __syncthreads();
@@ -357,13 +361,14 @@ void conv_weight_flip_t(const bf16_t* w, bf16_t* wt, long w_cs, int Kw, int Co, 
   hipLaunchKernelGGL(flip_t_kernel, dim3(grid), dim3(256), 0, s, w, wt, w_cs, Co, KH, KW, Ci);
 }
 
-void conv_gl_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int K, int rep, int B, int OH, int OW, int Co,
+void conv_gl_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, const bf16_t* acc, int K, int rep, int B, int OH, int OW, int Co,
                    int H, int W, int Ci, int KH, int KW, int stride, int pad, hipStream_t s) {
   ConvGLParams p{};
   p.x = dy;
   p.w = wt;
   p.y = dx;
   p.bias = nullptr;
+  p.acc = acc;
   p.x_cs = (long)B * OH * OW * Co;
   p.y_cs = (long)B * H * W * Ci;
   p.w_cs = (long)Ci * KH * KW * Co;

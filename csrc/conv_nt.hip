@@ -234,6 +234,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
   // stores (one 2-B store per element would make the epilogue store-issue-bound on wide
   // outputs such as the Transformer FFN: 1.9 M rows × 2048)
   bf16_t* __restrict__ y = p.y + (long)client * p.y_cs;
+  const bf16_t* accp = p.acc ? p.acc + (long)client * p.y_cs : nullptr;
   const bf16_t* bias = p.bias ? p.bias + (long)(client / p.rep) * p.b_cs : nullptr;
   float bvals[TN];
 #pragma unroll
@@ -269,11 +270,14 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
         row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
       }
       bf16_t* dst = y + row * p.N + n;
+      const bf16_t* acc_row = accp ? accp + row * p.N + n : nullptr;
       const bf16_t* src = slab + r * SW + cc;
       if (vec_ok && n + 8 <= p.N) {
-        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+        uint4 v = *reinterpret_cast<const uint4*>(src);
+        if (acc_row) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(acc_row));
+        *reinterpret_cast<uint4*>(dst) = v;
       } else {
-        for (int t = 0; t < 8 && n + t < p.N; ++t) dst[t] = src[t];
+        for (int t = 0; t < 8 && n + t < p.N; ++t) dst[t] = acc_row ? f2bf(bf2f(src[t]) + bf2f(acc_row[t])) : src[t];
       }
     }
     __syncthreads();  // the slab is rewritten for the next row block
@@ -383,13 +387,14 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   if (!launch_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt: bad variant %d\n", variant);
 }
 
-void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, long w_cs, int K, int rep, int B, int OH, int OW,
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, hipStream_t s) {
   ConvNTParams p{};
   p.x = dy;
   p.w = w;
   p.y = dx;
   p.bias = nullptr;
+  p.acc = acc;
   p.x_cs = (long)B * OH * OW * Co;
   p.y_cs = (long)B * H * W * Ci;
   p.w_cs = w_cs;

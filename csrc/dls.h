@@ -31,6 +31,7 @@ struct ConvNTParams {
   const bf16_t* w;  // B rows [N][R] per weight row
   bf16_t* y;        // [K][M][N]
   const bf16_t* bias;
+  const bf16_t* acc;  // optional [K][rows][N] (y layout) added to the result in the epilogue
   long x_cs, y_cs, w_cs, b_cs;
   int B, H, W, C;
   int OH, OW, KH, KW, stride, pad, dil;
@@ -66,6 +67,7 @@ struct ConvGLParams {
   const bf16_t* w;
   bf16_t* y;
   const bf16_t* bias;
+  const bf16_t* acc;   // optional, y layout: added to the result in the epilogue
   const bf16_t* zero;  // ≥ 128 B of zeros: the DMA source of out-of-image taps (filled by the launcher)
   long x_cs, y_cs, w_cs, b_cs;
   int B, H, W, C;  // A image
@@ -86,7 +88,7 @@ void conv_gl_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const bf16_t* bias
 // Wt[row][ci][kh'][kw'][co] = W[row][co][KH-1-kh'][KW-1-kw'][ci] (dgrad B operand, k-contiguous)
 void conv_weight_flip_t(const bf16_t* w, bf16_t* wt, long w_cs, int Kw, int Co, int KH, int KW, int Ci,
                         hipStream_t s);
-void conv_gl_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int K, int rep, int B, int OH, int OW, int Co,
+void conv_gl_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, const bf16_t* acc, int K, int rep, int B, int OH, int OW, int Co,
                    int H, int W, int Ci, int KH, int KW, int stride, int pad, hipStream_t s);
 
 // variant < 0: shape heuristic; 0..conv_nt_num_variants()-1: explicit tile config (benchmarks)
@@ -95,7 +97,7 @@ int conv_nt_num_variants();
 int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // dX of a conv (any stride): stride-1 → one flipped-weight NT GEMM; stride s > 1 → s² parity
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
-void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, long w_cs, int K, int rep, int B, int OH, int OW,
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, hipStream_t s);
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();

@@ -115,11 +115,11 @@ class Conv2d(Module):
     def own_params(self):
         return [self.w] + ([self.b] if self.b else [])
 
-    def forward(self, x, ctx):
+    def forward(self, x, ctx, link=None):
         P = ctx.P
         b = P.w(self.b) if self.b else None
         gb = P.g(self.b) if self.b else None
-        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb)
+        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb, link=link)
 
 
 class BatchNorm(Module):
@@ -139,13 +139,13 @@ class BatchNorm(Module):
     def own_params(self):
         return [self.gamma, self.beta]
 
-    def forward(self, x, ctx, residual=None, relu=None):
+    def forward(self, x, ctx, residual=None, relu=None, link=None):
         P = ctx.P
         rps = 1
         for d in x.shape[2:-1]:
             rps *= d
         return Fn.batch_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta),
-                             ctx.valid_rows(rps), self.relu if relu is None else relu, residual)
+                             ctx.valid_rows(rps), self.relu if relu is None else relu, residual, link=link)
 
 
 class Linear(Module):

@@ -86,6 +86,14 @@ class LeNet5Net(Module):
 
 
 # ------------------------------------------------------------------------- ResNets
+def _residual_link(block, x, ctx):
+    """Identity-shortcut blocks in training route the shortcut gradient through conv1's dgrad
+    epilogue (Fn.ResidualLink) instead of a separate autograd add over the block input."""
+    if block.down is None and ctx.training and x.requires_grad:
+        return Fn.ResidualLink()
+    return None
+
+
 class BasicBlock(Module):
     kind = "BasicBlock"
     expansion = 1
@@ -101,10 +109,11 @@ class BasicBlock(Module):
             self.down = self.child("downsample", Seq(Conv2d(cin, cout, 1, stride, 0), BatchNorm(cout)))
 
     def forward(self, x, ctx):
-        out = self.bn1.forward(self.conv1.forward(x, ctx), ctx)
+        link = _residual_link(self, x, ctx)
+        out = self.bn1.forward(self.conv1.forward(x, ctx, link=link), ctx)
         out = self.conv2.forward(out, ctx)
         sc = x if self.down is None else self.down.forward(x, ctx)
-        return self.bn2.forward(out, ctx, residual=sc, relu=True)
+        return self.bn2.forward(out, ctx, residual=sc, relu=True, link=link)
 
 
 class Bottleneck(Module):
@@ -125,11 +134,12 @@ class Bottleneck(Module):
             self.down = self.child("downsample", Seq(Conv2d(cin, cout, 1, stride, 0), BatchNorm(cout)))
 
     def forward(self, x, ctx):
-        out = self.bn1.forward(self.conv1.forward(x, ctx), ctx)
+        link = _residual_link(self, x, ctx)
+        out = self.bn1.forward(self.conv1.forward(x, ctx, link=link), ctx)
         out = self.bn2.forward(self.conv2.forward(out, ctx), ctx)
         out = self.conv3.forward(out, ctx)
         sc = x if self.down is None else self.down.forward(x, ctx)
-        return self.bn3.forward(out, ctx, residual=sc, relu=True)
+        return self.bn3.forward(out, ctx, residual=sc, relu=True, link=link)
 
 
 class ResNetNet(Module):

@@ -20,13 +20,25 @@ def _be(t):
 
 
 # --------------------------------------------------------------------------- conv2d
+class ResidualLink:
+    """Hands the identity-shortcut gradient of a residual block from the block's last BN
+    (whose backward runs first) to the block's first conv, whose dgrad adds it in its epilogue:
+    autograd then never materialises `dX_conv + dX_shortcut` with a separate add pass over the
+    block input (ResNet BasicBlock / Bottleneck without downsample)."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class _Conv(torch.autograd.Function):
     """Conv2d over the client dim. If the input carries more channels than the weight (image
     data stored zero-padded to 8 channels), the weight is zero-padded to match and only the
     real channels' gradient is written back."""
 
     @staticmethod
-    def forward(ctx, x, token, w, gw, stride, pad, b, gb):
+    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None):
         be = _be(x)
         ci = w.shape[-1]
         if x.shape[-1] > ci:
@@ -34,6 +46,7 @@ class _Conv(torch.autograd.Function):
         y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
+        ctx.link = link
         return y
 
     @staticmethod
@@ -42,10 +55,16 @@ class _Conv(torch.autograd.Function):
         be = _be(dy)
         dy = dy.contiguous()
         dx = None
+        link = ctx.link
+        acc = link.grad if link is not None else None
+        if link is not None:
+            link.grad = None
         if ctx.needs_input_grad[0]:
-            dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad)
+            dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc)
             if dx.shape[-1] > ctx.ci:
                 dx = dx[..., : ctx.ci]
+        elif acc is not None:
+            dx = acc
         if ctx.gw is not None:
             padded = w.shape[-1] > ctx.ci
             K = x.shape[0]
@@ -60,11 +79,15 @@ class _Conv(torch.autograd.Function):
                     be.bias_grad(dy, ctx.gb)
             if padded:
                 ctx.gw.copy_(gw[..., : ctx.ci])
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
-def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None):
-    return _Conv.apply(x, token, w, gw, stride, pad, b, gb)
+def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None, link: ResidualLink | None = None):
+    """`link`: this conv's input is also the identity shortcut of a residual BN fed the same
+    link (its gradient then arrives through the dgrad epilogue)."""
+    if link is not None:
+        assert stride == 1 and w.shape[-1] == x.shape[-1], "residual link needs a stride-1, unpadded conv"
+    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link)
 
 
 # --------------------------------------------------------------------------- linear
@@ -140,7 +163,7 @@ def linear_shared_input(x, token, w, gw):
 # ------------------------------------------------------------------------ batchnorm
 class _BN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual):
+    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link=None):
         be = _be(x)
         K = x.shape[0]
         C = x.shape[-1]
@@ -154,6 +177,7 @@ class _BN(torch.autograd.Function):
         ctx.save_for_backward(x3, y, mean, rstd, gamma)
         ctx.relu_mask = mask
         ctx.valid_rows, ctx.relu, ctx.has_res = valid_rows, relu, residual is not None
+        ctx.link = link
         ctx.ggamma, ctx.gbeta, ctx.shape = ggamma, gbeta, x.shape
         return y.reshape(x.shape)
 
@@ -172,11 +196,15 @@ class _BN(torch.autograd.Function):
             dx, dpre = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
                                  ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask)
         dres = dpre.reshape(ctx.shape) if ctx.has_res else None
-        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres
+        if dres is not None and ctx.link is not None:
+            ctx.link.grad = dres  # delivered by the block's first conv (ResidualLink)
+            dres = None
+        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres, None
 
 
-def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False, residual=None):
-    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual)
+def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False, residual=None,
+               link: ResidualLink | None = None):
+    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link)
 
 
 # ------------------------------------------------------------------------ layernorm

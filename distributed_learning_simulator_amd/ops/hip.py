@@ -114,7 +114,9 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
     return y
 
 
-def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
+    """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
+    residual branch of a ResNet block, so autograd never materialises the sum separately)."""
     K, B, OH, OW, Co = dy.shape
     dy = dy.contiguous()
     _check(dy, BF16, name="dy")
@@ -123,17 +125,19 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
     w_cs, rep = _client_view(w, K)
     H, W = int(in_hw[0]), int(in_hw[1])
     dx = torch.empty((K, B, H, W, Ci), dtype=BF16, device=dy.device)
+    if acc is not None:
+        assert stride == 1 and acc.shape == dx.shape and acc.dtype == BF16 and acc.is_contiguous(), acc.shape
     if (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
         # (strided dgrad splits into stride² short-K parity classes: conv_nt's smaller tiles win
         # there, l3a dgrad 447 vs 396 TFLOP/s). Large tiles want a k-contiguous B: one flip+transpose pass over the weight rows
         # (weights are small next to the activations), then stride² parity-class launches
         wt = torch.empty((Kw, Ci, KH, KW, Co), dtype=BF16, device=dy.device)
         _C.conv_weight_flip_t(_p(w), _p(wt), w.stride(0), Kw, Co, KH, KW, Ci, _s())
-        _C.conv_gl_dgrad(_p(dy), _p(wt), _p(dx), K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, _s())
+        _C.conv_gl_dgrad(_p(dy), _p(wt), _p(dx), _p(acc), K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, _s())
         return dx
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
-    _C.conv_dgrad(_p(dy), _p(w), _p(dx), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, nt_variant,
+    _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, nt_variant,
                   _s())
     return dx
 

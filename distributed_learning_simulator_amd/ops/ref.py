@@ -52,7 +52,7 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None):
     return _from_grouped(y, K).contiguous()
 
 
-def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
     K, B = dy.shape[:2]
     w = _match(w, K)
     Ci = w.shape[-1]
@@ -60,7 +60,8 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int):
         (B, K * Ci, in_hw[0], in_hw[1]), _w_grouped(w), _to_grouped(dy),
         stride=stride, padding=pad, groups=K,
     )
-    return _from_grouped(dx, K).contiguous()
+    dx = _from_grouped(dx, K).contiguous()
+    return dx if acc is None else dx + acc.to(dx.dtype)
 
 
 def conv_wgrad(dy, x, w_shape, stride: int, pad: int):

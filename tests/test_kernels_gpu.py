@@ -131,6 +131,26 @@ def test_conv_gl_fwd_dgrad(hip, case):
         hip.gl_mode = old
 
 
+@pytest.mark.parametrize("gl", [0, 1])
+@pytest.mark.parametrize("case", [(2, 3, 8, 8, 64, 64, 3), (2, 2, 8, 8, 128, 128, 3), (3, 2, 6, 6, 64, 256, 1),
+                                  (2, 2, 5, 5, 8, 24, 3)])
+def test_conv_dgrad_accumulate(hip, gl, case):
+    """dX + acc fused in the dgrad epilogue (identity-shortcut gradient, Fn.ResidualLink) on
+    both the LDS-DMA and the register-staged kernels."""
+    K, B, H, W, Ci, Co, k = case
+    torch.manual_seed(2)
+    w = _bf(K, Co, k, k, Ci, scale=0.2)
+    dy = _bf(K, B, H, W, Co)
+    acc = _bf(K, B, H, W, Ci)
+    old = hip.gl_mode
+    hip.gl_mode = gl
+    try:
+        dx = hip.conv_dgrad(dy, w, (H, W), 1, k // 2, acc=acc)
+    finally:
+        hip.gl_mode = old
+    _close(dx, ref.conv_dgrad(dy.float(), w.float(), (H, W), 1, k // 2, acc=acc.float()))
+
+
 def test_conv_gl_shared_weights_rep(hip):
     x = _bf(6, 4, 8, 8, 64)
     w = _bf(2, 128, 3, 3, 64, scale=0.2)
