@@ -21,6 +21,7 @@ import torch  # noqa: E402
 # (name, H, Cin, Cout, k, stride)  (input spatial H = W)
 RESNET18_CIFAR = [
     ("stem", 32, 3, 64, 3, 1),
+    ("stem8", 32, 8, 64, 3, 1),  # the stem as the model runs it: images stored zero-padded to 8 channels
     ("l1", 32, 64, 64, 3, 1),
     ("l2a", 32, 64, 128, 3, 2),
     ("l2", 16, 128, 128, 3, 1),

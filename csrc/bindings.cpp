@@ -69,16 +69,18 @@ PYBIND11_MODULE(_dls_hip, m) {
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
-                     int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr s) {
+                     int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, ptr s) {
     bn_fwd(P<const bf16_t>(x), P<const bf16_t>(gamma), P<const bf16_t>(beta), P<const bf16_t>(res), P<bf16_t>(y),
            P<float>(mean), P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws),
-           P<uint8_t>(mask), S(s));
+           P<uint8_t>(mask), P<unsigned>(counters), S(s));
   });
   m.def("bn_bwd", [](ptr dy, ptr x, ptr y, ptr mean, ptr rstd, ptr gamma, ptr valid, long g_cs, int K, int R, int C,
-                     int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr mask, ptr s) {
+                     int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr mask, ptr counters,
+                     ptr s) {
     bn_bwd(P<const bf16_t>(dy), P<const bf16_t>(x), P<const bf16_t>(y), P<const float>(mean), P<const float>(rstd),
            P<const bf16_t>(gamma), P<const int>(valid), g_cs, K, R, C, relu, P<bf16_t>(dx), P<bf16_t>(dpre),
-           P<float>(dgamma), P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), S(s));
+           P<float>(dgamma), P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), P<unsigned>(counters),
+           S(s));
   });
   m.def("ln_fwd", [](ptr x, ptr gamma, ptr beta, ptr y, ptr mean, ptr rstd, long g_cs, int K, long rpc, int C,
                      float eps, int rep, ptr s) {

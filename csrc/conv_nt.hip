@@ -425,6 +425,10 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
     p.out_s = 1;
     p.M = B * H * W;
     p.R = KH * KW * Co;
+    // N <= 64 full-correlation dgrad (ResNet l1): the 256x64 BK32 single-buffer tile streams the
+    // k-major weight rows best — l1 dgrad 420-435 vs 377-385 TFLOP/s for the 64x64 tile at 13 and
+    // 100 clients (bench/kernel_bench.py --sweep); the stride-2 parity classes keep the 64x64 tile
+    if (variant < 0 && Ci <= 64 && vec_width(Ci) == 8 && vec_width(Co) == 8) variant = 14;
     conv_nt(p, K, variant, s);
     return;
   }

@@ -108,11 +108,12 @@ int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant);
 long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
             float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
-            float* ws, uint8_t* relu_mask, hipStream_t s);  // relu_mask: optional [K][R][C/8] bits out
+            float* ws, uint8_t* relu_mask, unsigned* counters,
+            hipStream_t s);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused coefs)
 void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
             const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
             bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask,
-            hipStream_t s);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate
+            unsigned* counters, hipStream_t s);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate
 void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,
             long g_cs, int K, long rows_per_client, int C, float eps, int rep, hipStream_t s);
 void ln_bwd(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd, const bf16_t* gamma,

@@ -89,6 +89,51 @@ __global__ void pool_bwd_kernel(const bf16_t* __restrict__ dy, const int* __rest
   dx[i] = f2bf(acc);
 }
 
+// 8-channel form (C % 8 == 0): one thread per (input pixel, 8 channels) — 16-B dy loads and dx
+// stores, 2 × 16-B index loads per window, one window-range computation per 8 channels (the
+// scalar form is integer-divide and 2-B-access bound: ResNet-50's 112² stem pool, 12 ms/call)
+__global__ void __launch_bounds__(256) pool_bwd8_kernel(const bf16_t* __restrict__ dy, const int* __restrict__ idx,
+                                                        bf16_t* __restrict__ dx, long total8, int H, int W, int C,
+                                                        int OH, int OW, int k, int stride, int pad, int mode) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total8) return;
+  const int C8 = C >> 3;
+  const int c0 = (int)(i % C8) * 8;
+  const long pix = i / C8;  // (img, ih, iw)
+  const int iw = (int)(pix % W);
+  const long t = pix / W;
+  const int ih = (int)(t % H);
+  const long img = t / H;
+  const long obase = img * OH * OW * C + c0;
+  const int me = ih * W + iw;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int oh_lo = max(0, (ih + pad - k + stride) / stride), oh_hi = min(OH - 1, (ih + pad) / stride);
+  const int ow_lo = max(0, (iw + pad - k + stride) / stride), ow_hi = min(OW - 1, (iw + pad) / stride);
+  const float inv = 1.f / (float)(k * k);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    if (ih + pad - oh * stride < 0 || ih + pad - oh * stride >= k) continue;
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      if (iw + pad - ow * stride < 0 || iw + pad - ow * stride >= k) continue;
+      const long o = obase + ((long)oh * OW + ow) * C;
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+      if (mode == 0) {
+        const int4 a = *reinterpret_cast<const int4*>(idx + o);
+        const int4 b = *reinterpret_cast<const int4*>(idx + o + 4);
+        const int id[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += id[j] == me ? g[j] : 0.f;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += g[j] * inv;
+      }
+    }
+  }
+  *reinterpret_cast<uint4*>(dx + pix * C + c0) = pack8(acc);
+}
+
 // global average pool: [KB][HW][C] -> [KB][C]
 __global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int HW, int C, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -515,6 +560,11 @@ void pool_fwd(const bf16_t* x, bf16_t* y, int* idx, int K, int B, int H, int W, 
 void pool_bwd(const bf16_t* dy, const int* idx, bf16_t* dx, int K, int B, int H, int W, int C, int OH, int OW,
               int k, int stride, int pad, int mode, hipStream_t s) {
   const long total = (long)K * B * H * W * C;
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(pool_bwd8_kernel, dim3(cdiv(total / 8, 256)), dim3(256), 0, s, dy, idx, dx, total / 8, H, W, C,
+                       OH, OW, k, stride, pad, mode);
+    return;
+  }
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, idx, dx, total, H, W, C, OH, OW,
                      k, stride, pad, mode);
 }

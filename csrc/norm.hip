@@ -55,6 +55,54 @@ static int rows_per_block(long R, int K) {
   return (int)std::min<long>(ROWS_PER_BLOCK, (R + bpc - 1) / bpc);
 }
 
+// Arguments of the per-(client, channel) coefficient stage (see bn_coef_kernel for the math).
+// When `counters` is set, the reduction kernel computes the coefficients itself: the last of a
+// client's workgroups to publish its partial sums (agent-scope release → counter ticket →
+// agent-scope acquire) reduces them in fixed order and resets the ticket — one launch less per
+// BN pass and no separate tiny coefficient kernel.
+struct BNCoefArgs {
+  const bf16_t* gamma;
+  const bf16_t* beta;
+  const float* mean_in;
+  const float* rstd_in;
+  float* mean_out;
+  float* rstd_out;
+  float* coef;
+  float* dgamma;
+  float* dbeta;
+  long dg_cs, g_cs;
+  float eps;
+  int rep, bwd;
+  unsigned* counters;  // [K], zero at launch; reset by the last workgroup of each client
+};
+
+__device__ __forceinline__ void bn_coef_math(float s0, float s1, int k, int c, int C, float n, const BNCoefArgs& a) {
+  const long i = (long)k * C + c;
+  const float g = bf2f(a.gamma[(long)(k / a.rep) * a.g_cs + c]);
+  if (!a.bwd) {
+    const float mu = s0 / n;
+    const float var = fmaxf(s1 / n - mu * mu, 0.f);
+    const float rs = rsqrtf(var + a.eps);
+    const float sc = g * rs;
+    a.mean_out[i] = mu;
+    a.rstd_out[i] = rs;
+    a.coef[2 * i] = sc;
+    a.coef[2 * i + 1] = bf2f(a.beta[(long)(k / a.rep) * a.g_cs + c]) - mu * sc;
+  } else {
+    const float mu = a.mean_in[i], rs = a.rstd_in[i];
+    const float aa = g * rs;
+    const float e = -aa * rs * s1 / n;
+    const float d = -aa * s0 / n - e * mu;
+    a.coef[3 * i] = aa;
+    a.coef[3 * i + 1] = d;
+    a.coef[3 * i + 2] = e;
+    if (a.dgamma) {
+      a.dbeta[(long)k * a.dg_cs + c] = s0;
+      a.dgamma[(long)k * a.dg_cs + c] = s1;
+    }
+  }
+}
+
 // Generic per-(client, channel) double reduction over rows [0, nrows_valid):
 //   mode 0: s0 += x, s1 += x²                       (BN fwd stats)
 //   mode 1: g = dy*relu'(y); s0 += g, s1 += g*x̂      (BN bwd)
@@ -65,8 +113,9 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
                                                           const float* __restrict__ rstd,
                                                           const int* __restrict__ valid_rows, int R, int C, int relu,
                                                           float* __restrict__ ws, long ws_cs, int rpb,
-                                                          const uint8_t* __restrict__ rmask) {
+                                                          const uint8_t* __restrict__ rmask, BNCoefArgs ca) {
   __shared__ float red[2][256 * V];
+  __shared__ int is_last;
   const int k = blockIdx.y;
   const int CT = C / V;
   const int tid = threadIdx.x;
@@ -153,6 +202,34 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
     }
     __syncthreads();
   }
+  if (MODE == 2 || ca.counters == nullptr) return;
+  // ---- last-arriver coefficient stage (cdna_hip_programming.md Guideline 16 protocol)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's partials issued+done
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (ROCm 7.2: keep the wait after the release)
+    is_last = atomicAdd(&ca.counters[k], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int nvalid2 = valid_rows ? min(valid_rows[k], R) : R;
+  const float n = (float)max(nvalid2, 1);
+  const float* parts = ws + (long)k * gridDim.x * 2 * C;
+  for (int c = tid; c < C; c += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int b = 0; b < (int)gridDim.x; ++b) {  // fixed order: deterministic
+      a0 += parts[(long)b * 2 * C + c];
+      a1 += parts[(long)b * 2 * C + C + c];
+    }
+    bn_coef_math(a0, a1, k, c, C, n, ca);
+  }
+  if (tid == 0) atomicExch(&ca.counters[k], 0u);
 }
 
 // Per-(client, channel) coefficients from the reduced sums (one tiny launch), so the apply
@@ -442,17 +519,19 @@ long bn_workspace_floats(int K, long R, int C) {
 
 void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
             float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
-            float* ws, uint8_t* rmask, hipStream_t s) {
+            float* ws, uint8_t* rmask, unsigned* counters, hipStream_t s) {
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
+  BNCoefArgs ca{gamma, beta, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, eps, rep, 0, counters};
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr));
-  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
-                     valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+                                   nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr, ca));
+  if (!counters)
+    hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
+                       valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
   if (V != 8) rmask = nullptr;  // bit masks need 8-channel vectors
   DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, res, y, valid_rows, coef, R, C,
                                    relu, rpb, rmask));
@@ -460,16 +539,19 @@ void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16
 
 void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
             const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
-            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, hipStream_t s) {
+            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters,
+            hipStream_t s) {
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
+  BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1, counters};
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
-                                   valid_rows, R, C, relu, part, (long)2 * C, rpb, V == 8 ? rmask : nullptr));
-  hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
-                     valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
+                                   valid_rows, R, C, relu, part, (long)2 * C, rpb, V == 8 ? rmask : nullptr, ca));
+  if (!counters)
+    hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
+                       valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
   DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, valid_rows, coef, R, C,
                                    relu, dx, dpre, rpb, V == 8 ? rmask : nullptr));
 }
@@ -480,7 +562,7 @@ void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, 
   dim3 grid(cdiv(rows, rpb), K);
   const int V = vw(C);
   DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 2>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs, rpb, nullptr));
+                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs, rpb, nullptr, BNCoefArgs{}));
 }
 
 void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,

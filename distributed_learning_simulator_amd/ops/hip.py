@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import collections
 import importlib
+import os
 
 import torch
 
@@ -72,6 +73,27 @@ def _workspace(numel: int, device) -> torch.Tensor:
     if t is None or t.numel() < numel:
         t = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
         _ws_cache[key] = t
+    return t
+
+
+_ctr_cache: dict = {}
+# fused BN coefficients (csrc/norm.hip, last-arriver stage) instead of the separate coefficient
+# kernel. Off by default: measured SLOWER on MI355X — every workgroup's agent-scope release
+# (buffer_wbl2) writes back its XCD's dirty L2 lines: FedAvg ResNet-18 round 2.45 -> 2.91 s at
+# 100 clients, 462 -> 529 ms at the 8-rank per-rank load (DLS_BN_FUSED_COEF=1 to A/B)
+bn_fused_coef = os.environ.get("DLS_BN_FUSED_COEF", "0") == "1"
+
+
+def _bn_counters(K: int, device):
+    """Per-(device, stream) zeroed ticket counters of the fused BN coefficient stage; every
+    launch leaves them zero again. Sized once, generously, so graph capture never allocates."""
+    if not bn_fused_coef:
+        return None
+    key = (device, torch.cuda.current_stream().cuda_stream)
+    t = _ctr_cache.get(key)
+    if t is None or t.numel() < K:
+        t = torch.zeros(max(K, 1 << 14), dtype=torch.int32, device=device)
+        _ctr_cache[key] = t
     return t
 
 
@@ -228,7 +250,7 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
     if with_mask and relu and C % 8 == 0:
         mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
-              eps, rep, _p(ws), _p(mask), _s())
+              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _s())
     if with_mask:
         return y, mean, rstd, mask
     return y, mean, rstd
@@ -245,7 +267,7 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     dg_cs = ggamma.stride(0) if ggamma is not None else 0
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
-              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _s())
+              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _s())
     return dx, dpre
 
 

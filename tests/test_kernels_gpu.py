@@ -258,8 +258,9 @@ def test_layernorm(hip):
 
 
 @pytest.mark.parametrize("k,s,pad", [(2, 2, 0), (3, 2, 1)])
-def test_maxpool(hip, k, s, pad):
-    x = _bf(2, 3, 9, 9, 16)
+@pytest.mark.parametrize("C", [16, 6])  # 8-channel vector form and the scalar form
+def test_maxpool(hip, k, s, pad, C):
+    x = _bf(2, 3, 9, 9, C)
     y, idx = hip.maxpool_fwd(x, k, s, pad)
     y2, idx2 = ref.maxpool_fwd(x.float(), k, s, pad)
     _close(y, y2, 1e-6)
