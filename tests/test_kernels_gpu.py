@@ -378,7 +378,7 @@ def test_embedding_gather(hip):
     assert torch.equal(hip.gather_rows(src, idx), src[idx.reshape(-1)])
 
 
-@pytest.mark.parametrize("L,dh,masked", [(300, 20, True), (64, 32, False), (128, 64, True), (37, 16, True)])
+@pytest.mark.parametrize("L,dh,masked", [(300, 20, True), (64, 32, False), (128, 64, True), (37, 16, True), (700, 8, True)])
 def test_attention_fwd_bwd(hip, L, dh, masked):
     K, B, H = 2, 3, 2
     q, k, v = (_bf(K, B, H, L, dh) for _ in range(3))
