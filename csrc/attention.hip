@@ -28,6 +28,21 @@ __device__ __forceinline__ void load_row(const bf16_t* __restrict__ src, float* 
   for (int d = 0; d < DH; ++d) r[d] = bf2f(src[d]);
 }
 
+// one LDS row (broadcast: every lane reads the same address) as 16-B ds_read_b128s — rows are
+// DH·4 B, 16-B aligned for every supported DH; half the LDS read instructions of the b64 form
+template <int DH>
+__device__ __forceinline__ void lds_row(const float* __restrict__ p, float* r) {
+  static_assert(DH % 4 == 0, "rows are read as float4");
+#pragma unroll
+  for (int d = 0; d < DH; d += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p + d);
+    r[d] = v.x;
+    r[d + 1] = v.y;
+    r[d + 2] = v.z;
+    r[d + 3] = v.w;
+  }
+}
+
 // stage rows [0, L) of a [L][DH] bf16 matrix into LDS fp32 [L][DH]
 template <int DH>
 __device__ __forceinline__ void stage(const bf16_t* __restrict__ src, float* dst, int L) {
@@ -39,7 +54,7 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_fwd_kernel(const bf16_t* __rest
                                                          const bf16_t* __restrict__ v, const int* __restrict__ key_valid,
                                                          bf16_t* __restrict__ o, float* __restrict__ lse, int L, int H,
                                                          float scale) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ks = smem;
   float* Vs = smem + L * DH;
   const long head = blockIdx.x;
@@ -66,7 +81,8 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_fwd_kernel(const bf16_t* __rest
     for (int t = 0; t < CHUNK; ++t) {
       float a = -INFINITY;
       if (t < jn) {
-        const float* kr = Ks + (j0 + t) * DH;
+        float kr[DH];
+        lds_row<DH>(Ks + (j0 + t) * DH, kr);
         a = 0.f;
 #pragma unroll
         for (int d = 0; d < DH; ++d) a = fmaf(qi[d], kr[d], a);
@@ -84,7 +100,8 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_fwd_kernel(const bf16_t* __rest
       if (t < jn) {
         const float p = __expf(s[t] - mn);
         l += p;
-        const float* vr = Vs + (j0 + t) * DH;
+        float vr[DH];
+        lds_row<DH>(Vs + (j0 + t) * DH, vr);
 #pragma unroll
         for (int d = 0; d < DH; ++d) acc[d] = fmaf(p, vr[d], acc[d]);
       }
@@ -104,7 +121,7 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dq_kernel(const bf16_t* __r
                                                             const bf16_t* __restrict__ o, const float* __restrict__ lse,
                                                             const int* __restrict__ key_valid, bf16_t* __restrict__ dq,
                                                             float* __restrict__ delta, int L, int H, float scale) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ks = smem;
   float* Vs = smem + L * DH;
   const long head = blockIdx.x;
@@ -132,8 +149,9 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dq_kernel(const bf16_t* __r
   delta[head * L + i] = dl;
   const float li = lse[head * L + i];
   for (int j = 0; j < nk; ++j) {
-    const float* kr = Ks + j * DH;
-    const float* vr = Vs + j * DH;
+    float kr[DH], vr[DH];
+    lds_row<DH>(Ks + j * DH, kr);
+    lds_row<DH>(Vs + j * DH, vr);
     float s = 0.f, dp = 0.f;
 #pragma unroll
     for (int d = 0; d < DH; ++d) {
@@ -156,7 +174,7 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dkv_kernel(const bf16_t* __
                                                              const float* __restrict__ delta,
                                                              const int* __restrict__ key_valid, bf16_t* __restrict__ dk,
                                                              bf16_t* __restrict__ dv, int L, int H, float scale) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Qs = smem;
   float* Ds = smem + L * DH;
   float* Ls = smem + 2 * L * DH;
@@ -189,8 +207,9 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dkv_kernel(const bf16_t* __
     gk[d] = gv[d] = 0.f;
   }
   for (int i = 0; i < L; ++i) {
-    const float* qr = Qs + i * DH;
-    const float* dr = Ds + i * DH;
+    float qr[DH], dr[DH];
+    lds_row<DH>(Qs + i * DH, qr);
+    lds_row<DH>(Ds + i * DH, dr);
     float s = 0.f, dp = 0.f;
 #pragma unroll
     for (int d = 0; d < DH; ++d) {
