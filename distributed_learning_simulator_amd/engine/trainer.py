@@ -444,7 +444,9 @@ class CohortTrainer:
                     torch.cuda.synchronize(self.device)
                     torch.cuda.empty_cache()
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
+                    # thread-local capture: RCCL's watchdog thread keeps polling its events
+                    # while this rank captures (global mode would fail those calls)
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
                         run_parts()
                     sg.graph = g
                     g.replay()
