@@ -19,8 +19,10 @@ PYBIND11_MODULE(_dls_hip, m) {
 
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
-                      int relu, int K, int b_kmajor, int variant, ptr s) {
+                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, ptr s) {
     ConvNTParams p{};
+    p.acc = P<const bf16_t>(acc);
+    p.gate = P<const bf16_t>(gate);
     p.x = P<const bf16_t>(x);
     p.w = P<const bf16_t>(w);
     p.y = P<bf16_t>(y);

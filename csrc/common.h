@@ -49,6 +49,18 @@ __device__ __forceinline__ uint4 add_bf16x8(const uint4& a, const uint4& b) {
   for (int i = 0; i < 8; ++i) fa[i] += fb[i];
   return pack8(fa);
 }
+// keep the 8 bf16 of v where the matching gate value is > 0 (bit-exact select, no arithmetic)
+__device__ __forceinline__ uint4 gate_bf16x8(const uint4& v, const uint4& g) {
+  uint32_t out[4];
+  const uint32_t* vv = reinterpret_cast<const uint32_t*>(&v);
+  const uint32_t* gg = reinterpret_cast<const uint32_t*>(&g);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool lo = __uint_as_float(gg[i] << 16) > 0.f, hi = __uint_as_float(gg[i] & 0xffff0000u) > 0.f;
+    out[i] = (lo ? (vv[i] & 0xffffu) : 0u) | (hi ? (vv[i] & 0xffff0000u) : 0u);
+  }
+  return make_uint4(out[0], out[1], out[2], out[3]);
+}
 __device__ __forceinline__ uint4 pack8(const float* f) {
   uint32_t w[4];
 #pragma unroll

@@ -235,6 +235,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
   // outputs such as the Transformer FFN: 1.9 M rows × 2048)
   bf16_t* __restrict__ y = p.y + (long)client * p.y_cs;
   const bf16_t* accp = p.acc ? p.acc + (long)client * p.y_cs : nullptr;
+  const bf16_t* gatep = p.gate ? p.gate + (long)client * p.y_cs : nullptr;
   const bf16_t* bias = p.bias ? p.bias + (long)(client / p.rep) * p.b_cs : nullptr;
   float bvals[TN];
 #pragma unroll
@@ -271,13 +272,20 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
       }
       bf16_t* dst = y + row * p.N + n;
       const bf16_t* acc_row = accp ? accp + row * p.N + n : nullptr;
+      const bf16_t* gate_row = gatep ? gatep + row * p.N + n : nullptr;
       const bf16_t* src = slab + r * SW + cc;
       if (vec_ok && n + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
+        if (gate_row) v = gate_bf16x8(v, *reinterpret_cast<const uint4*>(gate_row));
         if (acc_row) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(acc_row));
         *reinterpret_cast<uint4*>(dst) = v;
       } else {
-        for (int t = 0; t < 8 && n + t < p.N; ++t) dst[t] = acc_row ? f2bf(bf2f(src[t]) + bf2f(acc_row[t])) : src[t];
+        for (int t = 0; t < 8 && n + t < p.N; ++t) {
+          float o = bf2f(src[t]);
+          if (gate_row && !(bf2f(gate_row[t]) > 0.f)) o = 0.f;
+          if (acc_row) o += bf2f(acc_row[t]);
+          dst[t] = f2bf(o);
+        }
       }
     }
     __syncthreads();  // the slab is rewritten for the next row block

@@ -31,7 +31,8 @@ struct ConvNTParams {
   const bf16_t* w;  // B rows [N][R] per weight row
   bf16_t* y;        // [K][M][N]
   const bf16_t* bias;
-  const bf16_t* acc;  // optional [K][rows][N] (y layout) added to the result in the epilogue
+  const bf16_t* acc;   // optional [K][rows][N] (y layout) added to the result in the epilogue
+  const bf16_t* gate;  // optional, y layout: result zeroed where gate <= 0 (ReLU' of the next layer's input)
   long x_cs, y_cs, w_cs, b_cs;
   int B, H, W, C;
   int OH, OW, KH, KW, stride, pad, dil;

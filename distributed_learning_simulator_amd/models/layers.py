@@ -162,10 +162,11 @@ class Linear(Module):
     def own_params(self):
         return [self.w] + ([self.b] if self.b else [])
 
-    def forward(self, x, ctx):
+    def forward(self, x, ctx, **fuse):
+        """`fuse`: epilogue fusions of Fn.linear (relu, premasked, gate_input, residual)."""
         P = ctx.P
         return Fn.linear(x, ctx.token, P.w(self.w), P.w(self.b) if self.b else None,
-                         P.g(self.w), P.g(self.b) if self.b else None)
+                         P.g(self.w), P.g(self.b) if self.b else None, **fuse)
 
 
 class LayerNorm(Module):

@@ -248,13 +248,14 @@ class MultiheadAttention(Module):
         self.child("in_proj", Linear(d, 3 * d))
         self.child("out_proj", Linear(d, d))
 
-    def forward(self, x, ctx, key_valid):
+    def forward(self, x, ctx, key_valid, residual=None):
+        """Returns out_proj(attention) (+ residual, added in the projection's epilogue)."""
         K, B, L, D = x.shape
         qkv = self.in_proj.forward(x, ctx).reshape(K, B, L, 3, self.h, D // self.h)
         qkv = qkv.permute(3, 0, 1, 4, 2, 5)  # 3,K,B,H,L,dh
         o = Fn.attention(qkv[0].contiguous(), qkv[1].contiguous(), qkv[2].contiguous(), key_valid)
         o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
-        return self.out_proj.forward(o, ctx)
+        return self.out_proj.forward(o, ctx, residual=residual)
 
 
 class TransformerEncoderLayer(Module):
@@ -272,9 +273,10 @@ class TransformerEncoderLayer(Module):
         self.child("norm2", LayerNorm(d))
 
     def forward(self, x, ctx, key_valid):
-        x = self.norm1.forward(x + self.self_attn.forward(x, ctx, key_valid), ctx)
-        f = self.linear2.forward(torch.relu(self.linear1.forward(x, ctx)), ctx)
-        return self.norm2.forward(x + f, ctx)
+        # residual adds and the FFN ReLU (forward and backward) ride in the GEMM epilogues
+        x = self.norm1.forward(self.self_attn.forward(x, ctx, key_valid, residual=x), ctx)
+        h = self.linear1.forward(x, ctx, relu=True, premasked=True)
+        return self.norm2.forward(self.linear2.forward(h, ctx, gate_input=True, residual=x), ctx)
 
 
 class TransformerClassifier(Module):

@@ -92,20 +92,34 @@ def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None, link: ResidualLink
 
 # --------------------------------------------------------------------------- linear
 class _Linear(torch.autograd.Function):
+    """y = x Wᵀ + b with optional epilogue fusions (Transformer FFN / residual branches):
+    relu      — ReLU in the GEMM epilogue (no separate activation pass);
+    premasked — the ReLU gradient is applied by the consumer (the next linear's gate_input),
+                so this backward takes dy as d(pre-activation) directly;
+    gate_input— x is a ReLU output: dX leaves through ReLU' (zeroed where x <= 0) in the dgrad
+                epilogue, one pass instead of a separate threshold-backward;
+    residual  — y += residual in the epilogue (its gradient is dy, passed straight through)."""
+
     @staticmethod
-    def forward(ctx, x, token, w, b, gw, gb):
+    def forward(ctx, x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False):
         be = _be(x)
-        y = be.linear_fwd(x, w, b)
-        ctx.save_for_backward(x, w)
+        y = be.linear_fwd(x, w, b, relu=relu, acc=residual)
+        mask_dy = relu and not premasked
+        ctx.save_for_backward(x, w, y if mask_dy else None)
         ctx.gw, ctx.gb = gw, gb
+        ctx.mask_dy, ctx.gate_input, ctx.has_res = mask_dy, gate_input, residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, y = ctx.saved_tensors
         be = _be(dy)
         dy = dy.contiguous()
-        dx = be.linear_dgrad(dy, w) if ctx.needs_input_grad[0] else None
+        dres = dy if ctx.has_res else None
+        if ctx.mask_dy:
+            dy = dy * (y > 0).to(dy.dtype)
+        gate = x.contiguous() if ctx.gate_input else None
+        dx = be.linear_dgrad(dy, w, gate=gate) if ctx.needs_input_grad[0] else None
         if ctx.gw is not None:
             if be is ref:
                 dw, db = ref.linear_wgrad(dy.float(), x.float(), ctx.gb is not None)
@@ -114,14 +128,17 @@ class _Linear(torch.autograd.Function):
                     ctx.gb.copy_(db)
             else:
                 be.linear_wgrad(dy, x, ctx.gw, ctx.gb)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, dres, None, None, None
 
 
-def linear(x, token, w, b, gw, gb):
-    """x [K, N, Fi] -> [K, N, Fo]; any extra middle dims are flattened."""
+def linear(x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False):
+    """x [K, N, Fi] -> [K, N, Fo]; any extra middle dims are flattened. Epilogue fusions: see
+    _Linear (relu / premasked / gate_input / residual)."""
+    assert not (relu and residual is not None), "ReLU and residual epilogues are not combined"
     shp = x.shape
     x3 = x.reshape(shp[0], -1, shp[-1])
-    y = _Linear.apply(x3, token, w, b, gw, gb)
+    r3 = residual.reshape(shp[0], x3.shape[1], -1).contiguous() if residual is not None else None
+    y = _Linear.apply(x3, token, w, b, gw, gb, r3, relu, premasked, gate_input)
     return y.reshape(*shp[:-1], y.shape[-1])
 
 

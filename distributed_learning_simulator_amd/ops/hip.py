@@ -132,7 +132,7 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
-               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_variant, _s())
+               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_variant, NULL, NULL, _s())
     return y
 
 
@@ -192,7 +192,8 @@ def bias_grad(dy, gb):
 
 
 # --------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b=None):
+def linear_fwd(x, w, b=None, relu=False, acc=None):
+    """y = x Wᵀ + b, optionally ReLU'd and/or + `acc` (a residual branch) in the epilogue."""
     K, N, Fi = x.shape
     x = x.contiguous()
     Kw, Fo, Fi2 = w.shape
@@ -200,20 +201,26 @@ def linear_fwd(x, w, b=None):
     w_cs, rep = _client_view(w, K)
     b_cs = _client_view(b, K)[0] if b is not None else 0
     y = torch.empty((K, N, Fo), dtype=BF16, device=x.device)
+    if acc is not None:
+        assert acc.shape == y.shape and acc.dtype == BF16 and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               0, K, 0, nt_variant, _s())
+               int(relu), K, 0, nt_variant, _p(acc), NULL, _s())
     return y
 
 
-def linear_dgrad(dy, w):
+def linear_dgrad(dy, w, gate=None):
+    """dX = dY W, zeroed where `gate` <= 0 when given (gate = the ReLU output this layer read:
+    the gradient then leaves already through the ReLU)."""
     K, N, Fo = dy.shape
     dy = dy.contiguous()
     Kw, Fo2, Fi = w.shape
     w_cs, rep = _client_view(w, K)
     dx = torch.empty((K, N, Fi), dtype=BF16, device=dy.device)
+    if gate is not None:
+        assert gate.shape == dx.shape and gate.dtype == BF16 and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
-               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_variant, _s())
+               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_variant, NULL, _p(gate), _s())
     return dx
 
 

@@ -75,20 +75,25 @@ def conv_wgrad(dy, x, w_shape, stride: int, pad: int):
 
 
 # ---------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b=None):
+def linear_fwd(x, w, b=None, relu=False, acc=None):
     K = x.shape[0]
     w = _match(w, K)
     y = torch.bmm(x, w.transpose(1, 2))
     if b is not None:
         b = _match(b, K)
         y = y + b[:, None, :]
+    if relu:
+        y = torch.relu(y)
+    if acc is not None:
+        y = y.to(acc.dtype) + acc
     return y
 
 
-def linear_dgrad(dy, w):
+def linear_dgrad(dy, w, gate=None):
     K = dy.shape[0]
     w = _match(w, K)
-    return torch.bmm(dy, w)
+    dx = torch.bmm(dy, w)
+    return dx if gate is None else dx * (gate > 0).to(dx.dtype)
 
 
 def linear_wgrad(dy, x, with_bias: bool):

@@ -190,6 +190,23 @@ def test_conv_large_wgrad_splitk(hip):
     _close(gw, ref.conv_wgrad(dy.float(), x.float(), (K, Co, 3, 3, Ci), 1, 1))
 
 
+@pytest.mark.parametrize("N,Fi,Fo", [(96, 100, 300), (64, 2048, 100), (40, 24, 36)])
+def test_linear_epilogue_fusions(hip, N, Fi, Fo):
+    """ReLU / residual epilogues of the forward and the ReLU' gate of the dgrad (Transformer FFN)."""
+    K = 3
+    x = _bf(K, N, Fi)
+    w = _bf(K, Fo, Fi, scale=0.1)
+    b = _bf(K, Fo, scale=0.1)
+    res = _bf(K, N, Fo)
+    _close(hip.linear_fwd(x, w, b, relu=True), ref.linear_fwd(x.float(), w.float(), b.float(), relu=True))
+    _close(hip.linear_fwd(x, w, b, acc=res), ref.linear_fwd(x.float(), w.float(), b.float(), acc=res.float()))
+    dy = _bf(K, N, Fo)
+    gate = torch.relu(_bf(K, N, Fi))
+    out = hip.linear_dgrad(dy, w, gate=gate)
+    _close(out, ref.linear_dgrad(dy.float(), w.float(), gate=gate.float()))
+    assert torch.all(out[gate <= 0] == 0)
+
+
 @pytest.mark.parametrize("N,Fi,Fo", [(64, 512, 10), (33, 100, 300), (128, 784, 200), (5, 84, 10)])
 def test_linear(hip, N, Fi, Fo):
     K = 3

@@ -138,3 +138,30 @@ def test_residual_link_gradients_equal_autograd_sum(name, ds, monkeypatch):
     loss_a, grad_a = _run(model, x, y, 1, theta.clone())
     torch.testing.assert_close(loss_l, loss_a)
     torch.testing.assert_close(grad_l, grad_a, rtol=1e-4, atol=1e-6 * grad_a.abs().max().item())
+
+
+def test_transformer_epilogue_fusions_match_unfused(monkeypatch):
+    """FFN ReLU (fwd + bwd gate) and residual adds fused into the linear epilogues give the same
+    loss and gradients as the plain composition (torch.relu, separate adds)."""
+    from distributed_learning_simulator_amd.models import zoo
+
+    torch.manual_seed(0)
+    spec = get_spec("imdb", {"max_len": 16})
+    model = build_model("TransformerClassificationModel", spec,
+                        {"d_model": 16, "nhead": 2, "num_encoder_layer": 2, "max_len": 16, "dim_feedforward": 64})
+    g = torch.Generator().manual_seed(3)
+    theta = model.layout.init_flat(g).unsqueeze(0)
+    tokens = torch.randint(1, spec.vocab_size if hasattr(spec, "vocab_size") else 100, (1, 3, 16))
+    lengths = torch.tensor([[16, 9, 4]])
+    y = torch.randint(0, spec.num_classes, (1, 3))
+    fused = _run(model, (tokens, lengths), y, 1, theta.clone())
+
+    def plain(self, x, ctx, key_valid):
+        x = self.norm1.forward(x + self.self_attn.forward(x, ctx, key_valid), ctx)
+        f = self.linear2.forward(torch.relu(self.linear1.forward(x, ctx)), ctx)
+        return self.norm2.forward(x + f, ctx)
+
+    monkeypatch.setattr(zoo.TransformerEncoderLayer, "forward", plain)
+    ref_ = _run(model, (tokens, lengths), y, 1, theta.clone())
+    torch.testing.assert_close(fused[0], ref_[0])
+    torch.testing.assert_close(fused[1], ref_[1], rtol=1e-4, atol=1e-6)
