@@ -46,6 +46,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--cohort", type=int, default=0)
+    ap.add_argument("--amp", action="store_true",
+                    help="bf16 fast mode (use_amp: true). Default: fp32, the reference's precision "
+                         "(conf/global.yaml use_amp: false) — split-bf16 MFMA GEMMs, fp32 storage/accumulate")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: time rank 0's share of an N-rank round alone on one GPU "
                          "(collectives are no-ops; not the benchmark contract)")
@@ -125,6 +128,9 @@ def main() -> None:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16" if sess.compute_dtype == torch.bfloat16 else "fp32",
+            # fp32: activations/weights/gradients fp32; GEMMs as split-bf16 (hi+lo) MFMA with fp32
+            # accumulation (≤1e-5 relative vs fp64, tests/test_kernels_f32_gpu.py)
+            "matmul": "bf16 MFMA" if sess.compute_dtype == torch.bfloat16 else "split-bf16x3 MFMA, fp32 accumulate",
             "data": wl["data"],
             "comm_bytes_per_round": bytes_per_round,
             "test_accuracy_last_round": acc,
@@ -146,6 +152,7 @@ def main() -> None:
 
 def workload_config(args, rounds: int) -> dict:
     common = {"round": rounds + 1000, "save_models": False, "log_level": "WARNING", "cohort_size": args.cohort,
+              "use_amp": bool(args.amp),
               "save_dir": os.path.join("/tmp", f"dls_bench_{os.getpid()}")}
 
     def shard_samples(sess):

@@ -22,10 +22,10 @@ namespace {
 constexpr int MAX_ROWS = 512;  // query / key rows per workgroup (one per lane): see attn_rows()
 constexpr int CHUNK = 16;   // keys per online-softmax rescale
 
-template <int DH>
-__device__ __forceinline__ void load_row(const bf16_t* __restrict__ src, float* r) {
+template <int DH, typename T>
+__device__ __forceinline__ void load_row(const T* __restrict__ src, float* r) {
 #pragma unroll
-  for (int d = 0; d < DH; ++d) r[d] = bf2f(src[d]);
+  for (int d = 0; d < DH; ++d) r[d] = ldf(src + d);
 }
 
 // one LDS row (broadcast: every lane reads the same address) as 16-B ds_read_b128s — rows are
@@ -44,15 +44,15 @@ __device__ __forceinline__ void lds_row(const float* __restrict__ p, float* r) {
 }
 
 // stage rows [0, L) of a [L][DH] bf16 matrix into LDS fp32 [L][DH]
-template <int DH>
-__device__ __forceinline__ void stage(const bf16_t* __restrict__ src, float* dst, int L) {
-  for (int e = threadIdx.x; e < L * DH; e += blockDim.x) dst[e] = bf2f(src[e]);
+template <int DH, typename T>
+__device__ __forceinline__ void stage(const T* __restrict__ src, float* dst, int L) {
+  for (int e = threadIdx.x; e < L * DH; e += blockDim.x) dst[e] = ldf(src + e);
 }
 
-template <int DH>
-__global__ void __launch_bounds__(MAX_ROWS) attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
-                                                         const bf16_t* __restrict__ v, const int* __restrict__ key_valid,
-                                                         bf16_t* __restrict__ o, float* __restrict__ lse, int L, int H,
+template <int DH, typename T>
+__global__ void __launch_bounds__(MAX_ROWS) attn_fwd_kernel(const T* __restrict__ q, const T* __restrict__ k,
+                                                         const T* __restrict__ v, const int* __restrict__ key_valid,
+                                                         T* __restrict__ o, float* __restrict__ lse, int L, int H,
                                                          float scale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ks = smem;
@@ -109,17 +109,17 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_fwd_kernel(const bf16_t* __rest
     m = mn;
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16_t* orow = o + base + (long)i * DH;
+  T* orow = o + base + (long)i * DH;
 #pragma unroll
-  for (int d = 0; d < DH; ++d) orow[d] = f2bf(acc[d] * inv);
+  for (int d = 0; d < DH; ++d) stf(orow + d, acc[d] * inv);
   lse[head * L + i] = l > 0.f ? m + __logf(l) : 0.f;
 }
 
-template <int DH>
-__global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dq_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ q,
-                                                            const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-                                                            const bf16_t* __restrict__ o, const float* __restrict__ lse,
-                                                            const int* __restrict__ key_valid, bf16_t* __restrict__ dq,
+template <int DH, typename T>
+__global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dq_kernel(const T* __restrict__ dout, const T* __restrict__ q,
+                                                            const T* __restrict__ k, const T* __restrict__ v,
+                                                            const T* __restrict__ o, const float* __restrict__ lse,
+                                                            const int* __restrict__ key_valid, T* __restrict__ dq,
                                                             float* __restrict__ delta, int L, int H, float scale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ks = smem;
@@ -162,18 +162,18 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dq_kernel(const bf16_t* __r
 #pragma unroll
     for (int d = 0; d < DH; ++d) g[d] = fmaf(ds, kr[d], g[d]);
   }
-  bf16_t* out = dq + base + (long)i * DH;
+  T* out = dq + base + (long)i * DH;
 #pragma unroll
-  for (int d = 0; d < DH; ++d) out[d] = f2bf(g[d] * scale);
+  for (int d = 0; d < DH; ++d) stf(out + d, g[d] * scale);
 }
 
-template <int DH>
-__global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dkv_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ q,
-                                                             const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+template <int DH, typename T>
+__global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dkv_kernel(const T* __restrict__ dout, const T* __restrict__ q,
+                                                             const T* __restrict__ k, const T* __restrict__ v,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta,
-                                                             const int* __restrict__ key_valid, bf16_t* __restrict__ dk,
-                                                             bf16_t* __restrict__ dv, int L, int H, float scale) {
+                                                             const int* __restrict__ key_valid, T* __restrict__ dk,
+                                                             T* __restrict__ dv, int L, int H, float scale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Qs = smem;
   float* Ds = smem + L * DH;
@@ -191,11 +191,14 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dkv_kernel(const bf16_t* __
   __syncthreads();
   const int j = blockIdx.y * blockDim.x + threadIdx.x;
   if (j >= L) return;
-  bf16_t* dkr = dk + base + (long)j * DH;
-  bf16_t* dvr = dv + base + (long)j * DH;
+  T* dkr = dk + base + (long)j * DH;
+  T* dvr = dv + base + (long)j * DH;
   if (j >= nk) {  // padded key: no probability mass, no gradient
 #pragma unroll
-    for (int d = 0; d < DH; ++d) dkr[d] = dvr[d] = f2bf(0.f);
+    for (int d = 0; d < DH; ++d) {
+      stf(dkr + d, 0.f);
+      stf(dvr + d, 0.f);
+    }
     return;
   }
   float kj[DH], vj[DH], gk[DH], gv[DH];
@@ -226,8 +229,8 @@ __global__ void __launch_bounds__(MAX_ROWS) attn_bwd_dkv_kernel(const bf16_t* __
   }
 #pragma unroll
   for (int d = 0; d < DH; ++d) {
-    dkr[d] = f2bf(gk[d] * scale);
-    dvr[d] = f2bf(gv[d]);
+    stf(dkr + d, gk[d] * scale);
+    stf(dvr + d, gv[d]);
   }
 }
 
@@ -261,21 +264,32 @@ bool attn_supported(int L, int DH) {
   return (2L * L * DH + 2L * L) * 4 <= 160L * 1024;
 }
 
-bool attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const int* key_valid, bf16_t* o, float* lse, long KBH,
-              int H, int L, int DH, hipStream_t s) {
+#define DISPATCH_T(F32, ...) \
+  if (F32) {                 \
+    typedef float TT;        \
+    __VA_ARGS__;             \
+  } else {                   \
+    typedef bf16_t TT;       \
+    __VA_ARGS__;             \
+  }
+#define CP(p) static_cast<const TT*>(p)
+#define MP(p) static_cast<TT*>(p)
+
+bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
+              int L, int DH, int f32, hipStream_t s) {
   if (!attn_supported(L, DH)) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));
   const size_t sh = (size_t)2 * L * DH * sizeof(float);
   const float scale = 1.0f / sqrtf((float)DH);
-  ATTN_DISPATCH(DH, big_lds((const void*)attn_fwd_kernel<D>, sh);
-                hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(rows), sh, s, q, k, v, key_valid, o, lse, L, H,
-                                   scale));
+  DISPATCH_T(f32, ATTN_DISPATCH(DH, big_lds((const void*)attn_fwd_kernel<D, TT>, sh);
+                                hipLaunchKernelGGL((attn_fwd_kernel<D, TT>), grid, dim3(rows), sh, s, CP(q), CP(k),
+                                                   CP(v), key_valid, MP(o), lse, L, H, scale)));
   return true;
 }
 
-bool attn_bwd(const bf16_t* dout, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const float* lse,
-              const int* key_valid, bf16_t* dq, bf16_t* dk, bf16_t* dv, float* delta, long KBH, int H, int L, int DH,
+bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
+              const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
               hipStream_t s) {
   if (!attn_supported(L, DH)) return false;
   const int rows = attn_rows(L);
@@ -283,53 +297,56 @@ bool attn_bwd(const bf16_t* dout, const bf16_t* q, const bf16_t* k, const bf16_t
   const float scale = 1.0f / sqrtf((float)DH);
   const size_t sh1 = (size_t)2 * L * DH * sizeof(float);
   const size_t sh2 = ((size_t)2 * L * DH + 2 * L) * sizeof(float);
-  ATTN_DISPATCH(DH, big_lds((const void*)attn_bwd_dq_kernel<D>, sh1);
-                hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, grid, dim3(rows), sh1, s, dout, q, k, v, o, lse,
-                                   key_valid, dq, delta, L, H, scale));
-  ATTN_DISPATCH(DH, big_lds((const void*)attn_bwd_dkv_kernel<D>, sh2);
-                hipLaunchKernelGGL(attn_bwd_dkv_kernel<D>, grid, dim3(rows), sh2, s, dout, q, k, v, lse, delta,
-                                   key_valid, dk, dv, L, H, scale));
+  DISPATCH_T(f32, ATTN_DISPATCH(DH, big_lds((const void*)attn_bwd_dq_kernel<D, TT>, sh1);
+                                hipLaunchKernelGGL((attn_bwd_dq_kernel<D, TT>), grid, dim3(rows), sh1, s, CP(dout),
+                                                   CP(q), CP(k), CP(v), CP(o), lse, key_valid, MP(dq), delta, L, H,
+                                                   scale)));
+  DISPATCH_T(f32, ATTN_DISPATCH(DH, big_lds((const void*)attn_bwd_dkv_kernel<D, TT>, sh2);
+                                hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, TT>), grid, dim3(rows), sh2, s, CP(dout),
+                                                   CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk), MP(dv), L, H,
+                                                   scale)));
   return true;
 }
 
 // ------------------------------------------------------------------------ SpMM (GCN)
 // y[k][i][:] = Σ_{e ∈ row i} val[e] · x[k][col[e]][:]   (CSR graph shared by all K clients)
 // One wave per (row, client); lanes own 8-feature chunks (16-B loads), fp32 accumulation.
+template <typename T>
 __global__ void __launch_bounds__(256) spmm_kernel(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                                   const float* __restrict__ val, const bf16_t* __restrict__ x,
-                                                   bf16_t* __restrict__ y, int N, int Nx, int F, long x_cs, long y_cs) {
+                                                   const float* __restrict__ val, const T* __restrict__ x,
+                                                   T* __restrict__ y, int N, int Nx, int F, long x_cs, long y_cs) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + wave;
   if (i >= N) return;
   const int kc = blockIdx.y;
-  const bf16_t* xk = x + (long)kc * x_cs;
-  bf16_t* yk = y + (long)kc * y_cs + (long)i * F;
+  const T* xk = x + (long)kc * x_cs;
+  T* yk = y + (long)kc * y_cs + (long)i * F;
   const int e0 = rowptr[i], e1 = rowptr[i + 1];
   for (int f0 = lane * 8; f0 < F; f0 += 64 * 8) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const bool vec = f0 + 8 <= F && (F % 8 == 0);
     for (int e = e0; e < e1; ++e) {
       const float a = val[e];
-      const bf16_t* xr = xk + (long)col[e] * F + f0;
+      const T* xr = xk + (long)col[e] * F + f0;
       if (vec) {
-        const uint4 u = *reinterpret_cast<const uint4*>(xr);
         float t[8];
-        unpack8(u, t);
+        load_vec<8>(xr, t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(a, t[j], acc[j]);
       } else {
-        for (int j = 0; j < 8 && f0 + j < F; ++j) acc[j] = fmaf(a, bf2f(xr[j]), acc[j]);
+        for (int j = 0; j < 8 && f0 + j < F; ++j) acc[j] = fmaf(a, ldf(xr + j), acc[j]);
       }
     }
     if (vec) {
-      *reinterpret_cast<uint4*>(yk + f0) = pack8(acc);
+      store_vec<8>(yk + f0, acc);
     } else {
-      for (int j = 0; j < 8 && f0 + j < F; ++j) yk[f0 + j] = f2bf(acc[j]);
+      for (int j = 0; j < 8 && f0 + j < F; ++j) stf(yk + f0 + j, acc[j]);
     }
   }
 }
 
-void spmm(const int* rowptr, const int* col, const float* val, const bf16_t* x, bf16_t* y, int K, int N, int Nx, int F,
-          long x_cs, long y_cs, hipStream_t s) {
-  hipLaunchKernelGGL(spmm_kernel, dim3(cdiv(N, 4), K), dim3(256), 0, s, rowptr, col, val, x, y, N, Nx, F, x_cs, y_cs);
+void spmm(const int* rowptr, const int* col, const float* val, const void* x, void* y, int K, int N, int Nx, int F,
+          long x_cs, long y_cs, int f32, hipStream_t s) {
+  DISPATCH_T(f32, hipLaunchKernelGGL(spmm_kernel<TT>, dim3(cdiv(N, 4), K), dim3(256), 0, s, rowptr, col, val, CP(x),
+                                     MP(y), N, Nx, F, x_cs, y_cs));
 }

@@ -19,8 +19,9 @@ PYBIND11_MODULE(_dls_hip, m) {
 
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
-                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, ptr s) {
+                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s) {
     ConvNTParams p{};
+    p.f32 = f32;
     p.acc = P<const bf16_t>(acc);
     p.gate = P<const bf16_t>(gate);
     p.x = P<const bf16_t>(x);
@@ -34,9 +35,9 @@ PYBIND11_MODULE(_dls_hip, m) {
     conv_nt(p, K, variant, S(s));
   });
   m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, ptr acc, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
-                         int W, int Ci, int KH, int KW, int stride, int pad, int variant, ptr s) {
+                         int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, ptr s) {
     conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), P<const bf16_t>(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
-               stride, pad, variant, S(s));
+               stride, pad, variant, f32, S(s));
   });
   m.def("conv_gl_wanted", &conv_gl_wanted);
   m.def("conv_gl_fwd", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int K, int rep,
@@ -56,8 +57,10 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt_num_variants", &conv_nt_num_variants);
   m.def("conv_nt_default_variant", &conv_nt_default_variant);
   m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,
-                      int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, int variant, ptr s) {
+                      int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, int variant, int f32,
+                      ptr s) {
     ConvTNParams p{};
+    p.f32 = f32;
     p.dy = P<const bf16_t>(dy);
     p.x = P<const bf16_t>(x);
     p.dw = P<float>(dw);
@@ -68,53 +71,59 @@ PYBIND11_MODULE(_dls_hip, m) {
   });
   m.def("conv_tn_splitk", &conv_tn_splitk);
   m.def("conv_tn_num_variants", &conv_tn_num_variants);
+  m.def("conv_nt_f32_num_variants", &conv_nt_f32_num_variants);
+  m.def("conv_tn_f32_num_variants", &conv_tn_f32_num_variants);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
-                     int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, ptr s) {
-    bn_fwd(P<const bf16_t>(x), P<const bf16_t>(gamma), P<const bf16_t>(beta), P<const bf16_t>(res), P<bf16_t>(y),
-           P<float>(mean), P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws),
-           P<uint8_t>(mask), P<unsigned>(counters), S(s));
+                     int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, int f32, ptr s) {
+    bn_fwd(P<const void>(x), P<const void>(gamma), P<const void>(beta), P<const void>(res), P<void>(y), P<float>(mean),
+           P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws), P<uint8_t>(mask),
+           P<unsigned>(counters), f32, S(s));
   });
   m.def("bn_bwd", [](ptr dy, ptr x, ptr y, ptr mean, ptr rstd, ptr gamma, ptr valid, long g_cs, int K, int R, int C,
                      int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr mask, ptr counters,
-                     ptr s) {
-    bn_bwd(P<const bf16_t>(dy), P<const bf16_t>(x), P<const bf16_t>(y), P<const float>(mean), P<const float>(rstd),
-           P<const bf16_t>(gamma), P<const int>(valid), g_cs, K, R, C, relu, P<bf16_t>(dx), P<bf16_t>(dpre),
-           P<float>(dgamma), P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), P<unsigned>(counters),
-           S(s));
+                     int f32, ptr s) {
+    bn_bwd(P<const void>(dy), P<const void>(x), P<const void>(y), P<const float>(mean), P<const float>(rstd),
+           P<const void>(gamma), P<const int>(valid), g_cs, K, R, C, relu, P<void>(dx), P<void>(dpre), P<float>(dgamma),
+           P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), P<unsigned>(counters), f32, S(s));
   });
   m.def("ln_fwd", [](ptr x, ptr gamma, ptr beta, ptr y, ptr mean, ptr rstd, long g_cs, int K, long rpc, int C,
-                     float eps, int rep, ptr s) {
-    ln_fwd(P<const bf16_t>(x), P<const bf16_t>(gamma), P<const bf16_t>(beta), P<bf16_t>(y), P<float>(mean),
-           P<float>(rstd), g_cs, K, rpc, C, eps, rep, S(s));
+                     float eps, int rep, int f32, ptr s) {
+    ln_fwd(P<const void>(x), P<const void>(gamma), P<const void>(beta), P<void>(y), P<float>(mean), P<float>(rstd),
+           g_cs, K, rpc, C, eps, rep, f32, S(s));
   });
   m.def("ln_bwd", [](ptr dy, ptr x, ptr mean, ptr rstd, ptr gamma, long g_cs, int K, long rpc, int C, ptr dx,
-                     ptr dgamma, ptr dbeta, long dg_cs, ptr s) {
-    ln_bwd(P<const bf16_t>(dy), P<const bf16_t>(x), P<const float>(mean), P<const float>(rstd),
-           P<const bf16_t>(gamma), g_cs, K, rpc, C, P<bf16_t>(dx), P<float>(dgamma), P<float>(dbeta), dg_cs, nullptr,
-           S(s));
+                     ptr dgamma, ptr dbeta, long dg_cs, int f32, ptr s) {
+    ln_bwd(P<const void>(dy), P<const void>(x), P<const float>(mean), P<const float>(rstd), P<const void>(gamma), g_cs,
+           K, rpc, C, P<void>(dx), P<float>(dgamma), P<float>(dbeta), dg_cs, nullptr, f32, S(s));
   });
-  m.def("col_sum", [](ptr x, ptr out, long out_cs, int K, long rows, int C, ptr s) {
-    col_sum(P<const bf16_t>(x), P<float>(out), out_cs, K, rows, C, S(s));
+  m.def("col_sum", [](ptr x, ptr out, long out_cs, int K, long rows, int C, int f32, ptr s) {
+    col_sum(P<const void>(x), P<float>(out), out_cs, K, rows, C, f32, S(s));
   });
 
   m.def("pool_fwd", [](ptr x, ptr y, ptr idx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
-                       int pad, int mode, ptr s) {
-    pool_fwd(P<const bf16_t>(x), P<bf16_t>(y), P<int>(idx), K, B, H, W, C, OH, OW, k, stride, pad, mode, S(s));
+                       int pad, int mode, int f32, ptr s) {
+    pool_fwd(P<const void>(x), P<void>(y), P<int>(idx), K, B, H, W, C, OH, OW, k, stride, pad, mode, f32, S(s));
   });
   m.def("pool_bwd", [](ptr dy, ptr idx, ptr dx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
-                       int pad, int mode, ptr s) {
-    pool_bwd(P<const bf16_t>(dy), P<const int>(idx), P<bf16_t>(dx), K, B, H, W, C, OH, OW, k, stride, pad, mode, S(s));
+                       int pad, int mode, int f32, ptr s) {
+    pool_bwd(P<const void>(dy), P<const int>(idx), P<void>(dx), K, B, H, W, C, OH, OW, k, stride, pad, mode, f32, S(s));
   });
-  m.def("gap_fwd", [](ptr x, ptr y, int KB, int HW, int C, ptr s) { gap_fwd(P<const bf16_t>(x), P<bf16_t>(y), KB, HW, C, S(s)); });
-  m.def("gap_bwd", [](ptr dy, ptr dx, int KB, int HW, int C, ptr s) { gap_bwd(P<const bf16_t>(dy), P<bf16_t>(dx), KB, HW, C, S(s)); });
+  m.def("gap_fwd", [](ptr x, ptr y, int KB, int HW, int C, int f32, ptr s) {
+    gap_fwd(P<const void>(x), P<void>(y), KB, HW, C, f32, S(s));
+  });
+  m.def("gap_bwd", [](ptr dy, ptr dx, int KB, int HW, int C, int f32, ptr s) {
+    gap_bwd(P<const void>(dy), P<void>(dx), KB, HW, C, f32, S(s));
+  });
   m.def("ce_fwd_bwd", [](ptr logits, ptr labels, ptr valid, ptr loss, ptr correct, ptr dlogits, int K, int B, int NC,
-                         ptr s) {
-    ce_fwd_bwd(P<const bf16_t>(logits), P<const int>(labels), P<const int>(valid), P<float>(loss), P<float>(correct),
-               P<bf16_t>(dlogits), K, B, NC, S(s));
+                         int f32, ptr s) {
+    ce_fwd_bwd(P<const void>(logits), P<const int>(labels), P<const int>(valid), P<float>(loss), P<float>(correct),
+               P<void>(dlogits), K, B, NC, f32, S(s));
   });
-  m.def("relu_bwd", [](ptr dy, ptr y, ptr dx, long n, ptr s) { relu_bwd(P<const bf16_t>(dy), P<const bf16_t>(y), P<bf16_t>(dx), n, S(s)); });
+  m.def("relu_bwd", [](ptr dy, ptr y, ptr dx, long n, int f32, ptr s) {
+    relu_bwd(P<const void>(dy), P<const void>(y), P<void>(dx), n, f32, S(s));
+  });
 
   m.def("sgd_step", [](ptr theta, ptr grad, ptr mom, ptr shadow, ptr lr, ptr active, ptr first, int K, long Pn, long ld,
                        float wd, float momentum, float dampening, int nesterov, ptr s) {
@@ -135,8 +144,8 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("weighted_sum", [](ptr x, ptr w, ptr out, int K, long Pn, long ld, ptr s) {
     weighted_sum(P<const float>(x), P<const float>(w), P<float>(out), K, Pn, ld, S(s));
   });
-  m.def("mix_rows", [](ptr x, ptr w, ptr out, int K, int M, long Pn, long ld, long ld_out, ptr s) {
-    mix_rows(P<const float>(x), P<const float>(w), P<bf16_t>(out), K, M, Pn, ld, ld_out, S(s));
+  m.def("mix_rows", [](ptr x, ptr w, ptr out, int K, int M, long Pn, long ld, long ld_out, int f32, ptr s) {
+    mix_rows(P<const float>(x), P<const float>(w), P<void>(out), K, M, Pn, ld, ld_out, f32, S(s));
   });
   m.def("masked_weighted_sum", [](ptr x, ptr mask, ptr w, ptr num, ptr den, int K, long Pn, long ld, ptr s) {
     masked_weighted_sum(P<const float>(x), P<const uint8_t>(mask), P<const float>(w), P<float>(num), P<float>(den), K, Pn,
@@ -161,33 +170,33 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("sign_vote", [](ptr packed, ptr active, ptr votes, int K, long Pn, ptr s) {
     sign_vote(P<const uint8_t>(packed), P<const uint8_t>(active), P<int>(votes), K, Pn, S(s));
   });
-  m.def("embedding_fwd", [](ptr tok, ptr table, ptr out, int K, long n_tok, int D, long t_cs, int rep, ptr s) {
-    embedding_fwd(P<const int>(tok), P<const bf16_t>(table), P<bf16_t>(out), K, n_tok, D, t_cs, rep, S(s));
+  m.def("embedding_fwd", [](ptr tok, ptr table, ptr out, int K, long n_tok, int D, long t_cs, int rep, int f32, ptr s) {
+    embedding_fwd(P<const int>(tok), P<const void>(table), P<void>(out), K, n_tok, D, t_cs, rep, f32, S(s));
   });
-  m.def("embedding_bwd", [](ptr tok, ptr dy, ptr dtable, int K, long n_tok, int D, long t_cs, ptr s) {
-    embedding_bwd(P<const int>(tok), P<const bf16_t>(dy), P<float>(dtable), K, n_tok, D, t_cs, S(s));
+  m.def("embedding_bwd", [](ptr tok, ptr dy, ptr dtable, int K, long n_tok, int D, long t_cs, int f32, ptr s) {
+    embedding_bwd(P<const int>(tok), P<const void>(dy), P<float>(dtable), K, n_tok, D, t_cs, f32, S(s));
   });
   m.def("attn_supported", &attn_supported);
-  m.def("attn_fwd", [](ptr q, ptr k, ptr v, ptr kv, ptr o, ptr lse, long KBH, int H, int L, int DH, ptr s) {
-    return attn_fwd(P<const bf16_t>(q), P<const bf16_t>(k), P<const bf16_t>(v), P<const int>(kv), P<bf16_t>(o),
-                    P<float>(lse), KBH, H, L, DH, S(s));
+  m.def("attn_fwd", [](ptr q, ptr k, ptr v, ptr kv, ptr o, ptr lse, long KBH, int H, int L, int DH, int f32, ptr s) {
+    return attn_fwd(P<const void>(q), P<const void>(k), P<const void>(v), P<const int>(kv), P<void>(o), P<float>(lse),
+                    KBH, H, L, DH, f32, S(s));
   });
   m.def("attn_bwd", [](ptr dout, ptr q, ptr k, ptr v, ptr o, ptr lse, ptr kv, ptr dq, ptr dk, ptr dv, ptr delta,
-                       long KBH, int H, int L, int DH, ptr s) {
-    return attn_bwd(P<const bf16_t>(dout), P<const bf16_t>(q), P<const bf16_t>(k), P<const bf16_t>(v),
-                    P<const bf16_t>(o), P<const float>(lse), P<const int>(kv), P<bf16_t>(dq), P<bf16_t>(dk),
-                    P<bf16_t>(dv), P<float>(delta), KBH, H, L, DH, S(s));
+                       long KBH, int H, int L, int DH, int f32, ptr s) {
+    return attn_bwd(P<const void>(dout), P<const void>(q), P<const void>(k), P<const void>(v), P<const void>(o),
+                    P<const float>(lse), P<const int>(kv), P<void>(dq), P<void>(dk), P<void>(dv), P<float>(delta), KBH,
+                    H, L, DH, f32, S(s));
   });
   m.def("spmm", [](ptr rowptr, ptr col, ptr val, ptr x, ptr y, int K, int N, int Nx, int F, long x_cs, long y_cs,
-                   ptr s) {
-    spmm(P<const int>(rowptr), P<const int>(col), P<const float>(val), P<const bf16_t>(x), P<bf16_t>(y), K, N, Nx, F,
-         x_cs, y_cs, S(s));
+                   int f32, ptr s) {
+    spmm(P<const int>(rowptr), P<const int>(col), P<const float>(val), P<const void>(x), P<void>(y), K, N, Nx, F, x_cs,
+         y_cs, f32, S(s));
   });
   m.def("nnadq_qdq", [](ptr x, ptr seg, ptr lo, ptr scale, ptr levels, int K, long Pn, long ld, int nseg, ptr s) {
     nnadq_qdq(P<float>(x), P<const int>(seg), P<const float>(lo), P<const float>(scale), P<const float>(levels), K, Pn,
               ld, nseg, S(s));
   });
-  m.def("gather_rows", [](ptr src, ptr idx, ptr dst, long n, long row_elems, ptr s) {
-    gather_rows(P<const bf16_t>(src), P<const int>(idx), P<bf16_t>(dst), n, row_elems, S(s));
+  m.def("gather_rows", [](ptr src, ptr idx, ptr dst, long n, long row_bytes, ptr s) {
+    gather_rows(P<const void>(src), P<const int>(idx), P<void>(dst), n, row_bytes, S(s));
   });
 }

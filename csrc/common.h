@@ -68,6 +68,92 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// ---- element-type-generic access: every activation kernel is instantiated for bf16 storage
+// (fast mode) and fp32 storage (reference precision, the reference trains in fp32:
+// conf/global.yaml `use_amp: false`). Arithmetic is always fp32.
+__device__ __forceinline__ float ldf(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float ldf(const float* p) { return *p; }
+__device__ __forceinline__ void stf(bf16_t* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void stf(float* p, float v) { *p = v; }
+// the value a store of v to T would read back (bf16 rounding only for bf16 storage)
+template <typename T>
+__device__ __forceinline__ float rt(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v)); else return v;
+}
+
+template <int V>
+__device__ __forceinline__ void load_vec(const bf16_t* p, float* f) {
+  if constexpr (V == 8) {
+    unpack8(*reinterpret_cast<const uint4*>(p), f);
+  } else if constexpr (V == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    f[0] = __uint_as_float(u.x << 16);
+    f[1] = __uint_as_float(u.x & 0xffff0000u);
+    f[2] = __uint_as_float(u.y << 16);
+    f[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) f[i] = bf2f(p[i]);
+  }
+}
+template <int V>
+__device__ __forceinline__ void load_vec(const float* p, float* f) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V; i += 4) {
+      const float4 u = *reinterpret_cast<const float4*>(p + i);
+      f[i] = u.x;
+      f[i + 1] = u.y;
+      f[i + 2] = u.z;
+      f[i + 3] = u.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) f[i] = p[i];
+  }
+}
+template <int V>
+__device__ __forceinline__ void store_vec(bf16_t* p, const float* f) {
+  if constexpr (V == 8) {
+    *reinterpret_cast<uint4*>(p) = pack8(f);
+  } else if constexpr (V == 4) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+    u.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = u;
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = f2bf(f[i]);
+  }
+}
+template <int V>
+__device__ __forceinline__ void store_vec(float* p, const float* f) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V; i += 4) *reinterpret_cast<float4*>(p + i) = make_float4(f[i], f[i + 1], f[i + 2], f[i + 3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = f[i];
+  }
+}
+
+// ---- split-bf16 ("bf16x3") operands of the fp32-accurate GEMMs: x = hi + lo with
+// hi = bf16(x), lo = bf16(x − hi) (both RNE) ⇒ |x − hi − lo| ≤ 2⁻¹⁷|x|. A·B is then
+// Ah·Bh + Al·Bh + Ah·Bl on the bf16 MFMA (fp32 accumulate); the dropped Al·Bl term is
+// ≤ 2⁻¹⁸|A||B|. Three bf16 MFMAs cost 3/16 of one f32 MFMA's time for the same tile.
+__device__ __forceinline__ void split2(float x, bf16_t& hi, bf16_t& lo) {
+  const __bf16 h = (__bf16)x;  // RNE; hipcc emits v_cvt_pk_bf16_f32 for pairs
+  const __bf16 l = (__bf16)(x - (float)h);
+  hi = __builtin_bit_cast(bf16_t, h);
+  lo = __builtin_bit_cast(bf16_t, l);
+}
+// V consecutive floats → V hi + V lo bf16 (V = 4: 8-B halves, V = 8: 16-B halves)
+template <int V>
+__device__ __forceinline__ void split_vec(const float* f, bf16_t* hi, bf16_t* lo) {
+#pragma unroll
+  for (int i = 0; i < V; ++i) split2(f[i], hi[i], lo[i]);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

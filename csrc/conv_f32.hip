@@ -1,0 +1,647 @@
+// fp32-accurate client-batched implicit-GEMM convolution / linear for gfx950 (MI355X, CDNA4).
+//
+// The reference trains in fp32 (conf/global.yaml `use_amp: false`). gfx950 has no xf32/TF32 and
+// its f32-input MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of the bf16 rate, so these kernels
+// compute every product as split bf16 ("bf16x3"):
+//
+//   a = ah + al, b = bh + bl  (ah = bf16(a), al = bf16(a − ah), RNE)
+//   a·b ≈ ah·bh + al·bh + ah·bl      (three v_mfma_f32_32x32x16_bf16, fp32 accumulate)
+//
+// |a − ah − al| ≤ 2⁻¹⁷|a| and the dropped al·bl ≤ 2⁻¹⁸|a||b|, so each product carries ≤ ~2⁻¹⁶
+// relative error (fp32-level results: the GPU tests compare against fp64 at ≤ 1e-5 relative) at
+// 3/16 of the f32-MFMA time. Operands are stored fp32 in HBM; the split happens ONCE per element
+// per workgroup, when the register-staged tile is written to LDS as two bf16 planes (hi, lo) —
+// the fragment reads and MFMA inner loop are the bf16 kernel's, with twice the fragments.
+//
+//   conv_nt_f32 : Y[m][n] = Σ_r A[m][r] B[n][r]  (forward, dgrad with B read from the forward
+//                 weight in place — k-major LDS image + ds_read_b64_tr_b16, as conv_nt.hip)
+//   conv_tn_f32 : dW[co][r] = Σ_m dY[m][co] X̃[m][r]  (weight gradient, split-K fp32 atomics)
+#include "dls.h"
+#include "gemm_common.h"
+
+namespace {
+
+template <int V>
+struct FV {
+  float v[V];
+};
+
+template <int V>
+__device__ __forceinline__ void fzero(FV<V>& f) {
+#pragma unroll
+  for (int i = 0; i < V; ++i) f.v[i] = 0.f;
+}
+
+template <int V>
+__device__ __forceinline__ void fload(FV<V>& f, const float* p) {
+  load_vec<V>(p, f.v);
+}
+
+// V floats → V bf16 hi at `hi`, V bf16 lo at `lo` (one 2/8/16-B LDS store per plane)
+template <int V>
+__device__ __forceinline__ void st_split(bf16_t* hi, bf16_t* lo, const FV<V>& f) {
+  typedef typename VecT<V>::T TV;
+  union {
+    TV v;
+    bf16_t e[V];
+  } h, l;
+#pragma unroll
+  for (int i = 0; i < V; ++i) split2(f.v[i], h.e[i], l.e[i]);
+  *reinterpret_cast<TV*>(hi) = h.v;
+  *reinterpret_cast<TV*>(lo) = l.v;
+}
+
+// ------------------------------------------------------------------------- NT (fwd / dgrad)
+template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int NBUF>
+__global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p) {
+  constexpr int T = WM * WN * 64;
+  constexpr int TM = BM / (WM * 32);
+  constexpr int TN = BN / (WN * 32);
+  constexpr int LDA = BK + 8;
+  constexpr int KCA = BK / VA, RPA = T / KCA, PA = BM / RPA;
+  constexpr int KCB = BK / VB, RPB = T / KCB, PB = BN / RPB;  // B row-major [n][k]
+  constexpr int CCB = BN / VB, RPK = T / CCB, PK = BK / RPK;  // B k-major [k][n]
+  constexpr int LDBK = BN + 32;                                // row bytes ≡ 64 (mod 256)
+  constexpr int NB = BKM ? PK : PB;
+  static_assert(PA >= 1 && NB >= 1, "tile too small for thread count");
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int B_ROWS = BKM ? BK : BN, B_COLS = BKM ? LDBK : LDA;
+  constexpr int A_PLANE = NBUF * BM * LDA, B_PLANE = NBUF * B_ROWS * B_COLS;  // bf16 elements
+  constexpr int LOOP_BYTES = 2 * (A_PLANE + B_PLANE) * 2;
+  constexpr int SW = TN * 32 + 4;                   // epilogue slab row (fp32), 16-B aligned
+  constexpr int EPI_BYTES = WM * WN * 32 * SW * 4;  // one 32-row slab per wave
+  constexpr int SMEM = LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  bf16_t* const As = reinterpret_cast<bf16_t*>(smem);  // [plane hi/lo][NBUF][BM][LDA]
+  bf16_t* const Bs = As + 2 * A_PLANE;                 // [plane][NBUF][B_ROWS][B_COLS]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
+  const int per_client = tilesM * tilesN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int client = bid / per_client;
+  const int t = bid % per_client;
+  const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BN;
+  const float* __restrict__ x = reinterpret_cast<const float*>(p.x) + (long)client * p.x_cs;
+  const float* __restrict__ w = reinterpret_cast<const float*>(p.w) + (long)(client / p.rep) * p.w_cs;
+
+  // --- A loader: PA rows per thread, one fixed K sub-chunk, incremental im2col state
+  const int kca = tid % KCA;
+  int a_ih0[PA], a_iw0[PA];
+  const float* a_ptr[PA];
+  bool a_ok[PA];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int m = m0 + tid / KCA + j * RPA;
+    a_ok[j] = m < p.M;
+    const uint32_t mm = a_ok[j] ? m : 0;
+    const uint32_t b = fdiv(mm, p.fd_ohw);
+    const uint32_t rem = mm - b * p.OH * p.OW;
+    const uint32_t oh = fdiv(rem, p.fd_ow);
+    const uint32_t ow = rem - oh * p.OW;
+    a_ih0[j] = (int)oh * p.stride - p.pad;
+    a_iw0[j] = (int)ow * p.stride - p.pad_w;
+    a_ptr[j] = x + (long)b * p.H * p.W * p.C;
+  }
+  int r_cur = kca * VA;
+  int kh, kw, c;
+  {
+    kh = (int)fdiv(r_cur, p.fd_kwc);
+    const int rr = r_cur - kh * p.KW * p.C;
+    kw = (int)fdiv(rr, p.fd_c);
+    c = rr - kw * p.C;
+  }
+  const int kcb = tid % (BKM ? CCB : KCB);
+  const int nk = (p.R + BK - 1) / BK;
+  int k_next = 0;
+
+  FV<VA> ra[PA];
+  FV<VB> rb[NB];
+
+  auto load = [&]() {
+    const int k0 = k_next;
+    k_next += BK;
+    const bool rok = r_cur < p.R;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      fzero(ra[j]);
+      if (!(rok && a_ok[j])) continue;
+      int qh = a_ih0[j] + kh, qw = a_iw0[j] + kw;
+      if (p.dil > 1) {
+        if ((qh % p.dil) != 0 || (qw % p.dil) != 0) continue;
+        qh /= p.dil;
+        qw /= p.dil;
+      }
+      if (qh < 0 || qh >= p.H || qw < 0 || qw >= p.W) continue;
+      fload(ra[j], a_ptr[j] + ((long)qh * p.W + qw) * p.C + c);
+    }
+    if constexpr (!BKM) {
+      const int rB = k0 + kcb * VB;
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int n = n0 + tid / KCB + j * RPB;
+        fzero(rb[j]);
+        if (n < p.N && rB < p.R) fload(rb[j], w + (long)n * p.R + rB);
+      }
+    } else {
+      const int nb = n0 + kcb * VB;
+#pragma unroll
+      for (int j = 0; j < PK; ++j) {
+        const int k = k0 + tid / CCB + j * RPK;
+        fzero(rb[j]);
+        if (k >= p.R || nb >= p.N) continue;
+        const int kh2 = (int)fdiv(k, p.fd_kwc);
+        const int rr = k - kh2 * p.KW * p.C;
+        const int kw2 = (int)fdiv(rr, p.fd_c);
+        const int co = rr - kw2 * p.C;
+        const int khh = p.kh_off - p.kh_step * kh2, kww = p.kw_off - p.kw_step * kw2;
+        fload(rb[j], w + (((long)co * p.wKH + khh) * p.wKW + kww) * p.N + nb);
+      }
+    }
+    r_cur += BK;
+    c += BK;
+    while (c >= p.C) {
+      c -= p.C;
+      if (++kw == p.KW) {
+        kw = 0;
+        ++kh;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int off = (buf * BM + tid / KCA + j * RPA) * LDA + kca * VA;
+      st_split(As + off, As + A_PLANE + off, ra[j]);
+    }
+    if constexpr (!BKM) {
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int off = (buf * B_ROWS + tid / KCB + j * RPB) * B_COLS + kcb * VB;
+        st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PK; ++j) {
+        const int off = (buf * B_ROWS + tid / CCB + j * RPK) * B_COLS + kcb * VB;
+        st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const int wm0 = (wid / WN) * (TM * 32), wn0 = (wid % WN) * (TN * 32);
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int off = (buf * BM + wm0 + i * 32 + (lane & 31)) * LDA + ks * 16 + 8 * h;
+        ah[i] = *reinterpret_cast<const bf16x8*>(As + off);
+        al[i] = *reinterpret_cast<const bf16x8*>(As + A_PLANE + off);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (!BKM) {
+          const int off = (buf * B_ROWS + wn0 + j * 32 + (lane & 31)) * B_COLS + ks * 16 + 8 * h;
+          bh[j] = *reinterpret_cast<const bf16x8*>(Bs + off);
+          bl[j] = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + off);
+        } else {
+          const int col = wn0 + j * 32 + 16 * (g & 1) + 4 * pp;
+          const int o0 = (buf * B_ROWS + ks * 16 + 8 * h + q) * B_COLS + col;
+          const int o1 = o0 + 4 * B_COLS;
+          bh[j] = tr_frag(Bs + o0, Bs + o1);
+          bl[j] = tr_frag(Bs + B_PLANE + o0, Bs + B_PLANE + o1);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  if constexpr (NBUF == 1) {
+    load();
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load();
+      compute(0);
+      if (kt + 1 < nk) {
+        __syncthreads();
+        store(0);
+        __syncthreads();
+      }
+    }
+  } else {
+    load();
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load();
+      compute(buf);
+      if (kt + 1 < nk) store(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // --- epilogue: bias (+ReLU) → per-wave 32-row fp32 LDS slab → 16-B coalesced stores, with the
+  // optional gate (ReLU' of the next layer's input) and accumulate (second gradient branch)
+  float* __restrict__ y = reinterpret_cast<float*>(p.y) + (long)client * p.y_cs;
+  const float* accp = p.acc ? reinterpret_cast<const float*>(p.acc) + (long)client * p.y_cs : nullptr;
+  const float* gatep = p.gate ? reinterpret_cast<const float*>(p.gate) + (long)client * p.y_cs : nullptr;
+  const float* bias = p.bias ? reinterpret_cast<const float*>(p.bias) + (long)(client / p.rep) * p.b_cs : nullptr;
+  float bvals[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + j * 32 + (lane & 31);
+    bvals[j] = (bias && n < p.N) ? bias[n] : 0.f;
+  }
+  float* slab = reinterpret_cast<float*>(smem) + wid * 32 * SW;
+  const bool vec_ok = (p.N % 4) == 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float v = acc[i][j][e] + bvals[j];
+        if (p.relu) v = fmaxf(v, 0.f);
+        slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = v;
+      }
+    }
+    __syncthreads();
+    for (int qd = lane; qd < 32 * TN * 8; qd += 64) {
+      const int r = qd / (TN * 8), cc = (qd % (TN * 8)) * 4;
+      const int m = m0 + wm0 + i * 32 + r, n = n0 + wn0 + cc;
+      if (m >= p.M || n >= p.N) continue;
+      long row = m;
+      if (p.out_s > 1) {
+        const uint32_t b = fdiv(m, p.fd_ohw);
+        const uint32_t rem = m - b * p.OH * p.OW;
+        const uint32_t oh = fdiv(rem, p.fd_ow);
+        const uint32_t ow = rem - oh * p.OW;
+        row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
+      }
+      float* dst = y + row * p.N + n;
+      const float* src = slab + r * SW + cc;
+      if (vec_ok && n + 4 <= p.N) {
+        float4 v = *reinterpret_cast<const float4*>(src);
+        if (gatep) {
+          const float4 gv = *reinterpret_cast<const float4*>(gatep + row * p.N + n);
+          v.x = gv.x > 0.f ? v.x : 0.f;
+          v.y = gv.y > 0.f ? v.y : 0.f;
+          v.z = gv.z > 0.f ? v.z : 0.f;
+          v.w = gv.w > 0.f ? v.w : 0.f;
+        }
+        if (accp) {
+          const float4 av = *reinterpret_cast<const float4*>(accp + row * p.N + n);
+          v.x += av.x;
+          v.y += av.y;
+          v.z += av.z;
+          v.w += av.w;
+        }
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        for (int t2 = 0; t2 < 4 && n + t2 < p.N; ++t2) {
+          float o = src[t2];
+          if (gatep && !(gatep[row * p.N + n + t2] > 0.f)) o = 0.f;
+          if (accp) o += accp[row * p.N + n + t2];
+          dst[t2] = o;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// VSET 0: the 32-B (8, 8) gathers of wide layers; 1: + 16-B (4, ·) widths (d_model = 100,
+// DenseNet's 12-channel growth); 2: every combination incl. scalar (stems, LeNet, tiny linears)
+template <int BM, int BN, int BK, int WM, int WN, int NBUF, int VSET>
+bool launch_nt_f32_cfg(const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStream_t s) {
+  const int grid = K * cdiv(p.M, BM) * cdiv(p.N, BN);
+#define NTF_CASE(A, B)                                                                                       \
+  if (va == A && vb == B) {                                                                                  \
+    if (bkm)                                                                                                 \
+      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, A, B, true, NBUF>), dim3(grid),             \
+                         dim3(WM * WN * 64), 0, s, p);                                                       \
+    else                                                                                                     \
+      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, A, B, false, NBUF>), dim3(grid),            \
+                         dim3(WM * WN * 64), 0, s, p);                                                       \
+    return true;                                                                                             \
+  }
+  NTF_CASE(8, 8)
+  if constexpr (VSET >= 1) { NTF_CASE(4, 4) NTF_CASE(8, 4) NTF_CASE(4, 8) }
+  if constexpr (VSET >= 2) { NTF_CASE(8, 1) NTF_CASE(4, 1) NTF_CASE(1, 8) NTF_CASE(1, 4) NTF_CASE(1, 1) }
+#undef NTF_CASE
+  return false;
+}
+
+// variant ids are stable (bench/kernel_bench.py --f32 sweeps them)
+bool launch_nt_f32_variant(int v, const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStream_t s) {
+  switch (v) {
+    case 0: return launch_nt_f32_cfg<128, 128, 32, 2, 2, 2, 1>(p, K, va, vb, bkm, s);  // 80 KB: 2 blocks/CU
+    case 1: return launch_nt_f32_cfg<128, 128, 32, 2, 2, 1, 0>(p, K, va, vb, bkm, s);  // 40 KB
+    case 2: return launch_nt_f32_cfg<256, 128, 32, 4, 2, 1, 0>(p, K, va, vb, bkm, s);  // 60 KB
+    case 3: return launch_nt_f32_cfg<64, 64, 32, 2, 2, 2, 2>(p, K, va, vb, bkm, s);    // 40 KB, any width
+    case 4: return launch_nt_f32_cfg<128, 64, 32, 4, 1, 2, 1>(p, K, va, vb, bkm, s);   // 60 KB, N <= 64
+    case 5: return launch_nt_f32_cfg<128, 128, 64, 2, 2, 1, 0>(p, K, va, vb, bkm, s);  // 72 KB
+    case 6: return launch_nt_f32_cfg<256, 64, 32, 4, 1, 1, 0>(p, K, va, vb, bkm, s);   // 50 KB, N <= 64
+    case 7: return launch_nt_f32_cfg<64, 64, 32, 2, 2, 1, 1>(p, K, va, vb, bkm, s);    // 20 KB
+    default: return false;
+  }
+}
+
+int vw(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
+
+// --------------------------------------------------------------------------- TN (wgrad)
+template <int BMc, int BNr, int BKT, int WM, int WN, int VA, int VB, int NBUF>
+__global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p) {
+  constexpr int T = WM * WN * 64;
+  constexpr int TM = BMc / (WM * 32), TN = BNr / (WN * 32);
+  constexpr int LDA = BMc + 32;
+  constexpr int LDB = BNr + 32;
+  constexpr int CCA = BMc / VA, RPA = T / CCA, PA = BKT / RPA;
+  constexpr int CCB = BNr / VB, RPB = T / CCB, PB = BKT / RPB;
+  static_assert(PA >= 1 && PB >= 1, "tile too small");
+  constexpr int A_PLANE = NBUF * BKT * LDA, B_PLANE = NBUF * BKT * LDB;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (A_PLANE + B_PLANE)];
+  bf16_t* const As = smem;               // [plane][NBUF][BKT][LDA]
+  bf16_t* const Bs = smem + 2 * A_PLANE;  // [plane][NBUF][BKT][LDB]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tilesM = (p.Co + BMc - 1) / BMc, tilesN = (p.R + BNr - 1) / BNr;
+  const int per_client = tilesM * tilesN * p.splitk;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int client = bid / per_client;
+  int t = bid % per_client;
+  const int split = t % p.splitk;
+  t /= p.splitk;
+  const int co0 = (t / tilesN) * BMc, r0 = (t % tilesN) * BNr;
+  const int mbeg = split * p.m_per_split;
+  const int mend = min(p.M, mbeg + p.m_per_split);
+
+  const float* __restrict__ dy = reinterpret_cast<const float*>(p.dy) + (long)client * p.dy_cs;
+  const float* __restrict__ x = reinterpret_cast<const float*>(p.x) + (long)client * p.x_cs;
+
+  const int cb = tid % CCB;
+  const int rcol = r0 + cb * VB;
+  const bool rok = rcol < p.R;
+  int kh = 0, kw = 0, c = 0;
+  if (rok) {
+    kh = rcol / (p.KW * p.C);
+    const int rr = rcol - kh * p.KW * p.C;
+    kw = rr / p.C;
+    c = rr - kw * p.C;
+  }
+  const int ca = tid % CCA;
+  const int cocol = co0 + ca * VA;
+  const bool cok = cocol < p.Co;
+
+  FV<VA> ra[PA];
+  FV<VB> rb[PB];
+  int k_next = mbeg;
+  auto load = [&]() {
+    const int k0 = k_next;
+    k_next += BKT;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int m = k0 + tid / CCA + j * RPA;
+      fzero(ra[j]);
+      if (cok && m < mend) fload(ra[j], dy + (long)m * p.Co + cocol);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int m = k0 + tid / CCB + j * RPB;
+      fzero(rb[j]);
+      if (!(rok && m < mend)) continue;
+      const uint32_t b = fdiv(m, p.fd_ohw);
+      const uint32_t rem = m - b * p.OH * p.OW;
+      const uint32_t oh = fdiv(rem, p.fd_ow);
+      const uint32_t ow = rem - oh * p.OW;
+      const int ih = (int)oh * p.stride - p.pad + kh, iw = (int)ow * p.stride - p.pad + kw;
+      if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
+      fload(rb[j], x + (((long)b * p.H + ih) * p.W + iw) * p.C + c);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int off = (buf * BKT + tid / CCA + j * RPA) * LDA + ca * VA;
+      st_split(As + off, As + A_PLANE + off, ra[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int off = (buf * BKT + tid / CCB + j * RPB) * LDB + cb * VB;
+      st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const int wm0 = (wid / WN) * (TM * 32), wn0 = (wid % WN) * (TN * 32);
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int ks = 0; ks < BKT / 16; ++ks) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+      const int krow = buf * BKT + ks * 16 + 8 * h + q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int o0 = krow * LDA + wm0 + i * 32 + 16 * (g & 1) + 4 * pp, o1 = o0 + 4 * LDA;
+        ah[i] = tr_frag(As + o0, As + o1);
+        al[i] = tr_frag(As + A_PLANE + o0, As + A_PLANE + o1);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int o0 = krow * LDB + wn0 + j * 32 + 16 * (g & 1) + 4 * pp, o1 = o0 + 4 * LDB;
+        bh[j] = tr_frag(Bs + o0, Bs + o1);
+        bl[j] = tr_frag(Bs + B_PLANE + o0, Bs + B_PLANE + o1);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  const int nk = (mend - mbeg + BKT - 1) / BKT;
+  if (nk <= 0) return;
+  if constexpr (NBUF == 1) {
+    load();
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load();
+      compute(0);
+      if (kt + 1 < nk) {
+        __syncthreads();
+        store(0);
+        __syncthreads();
+      }
+    }
+  } else {
+    load();
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load();
+      compute(buf);
+      if (kt + 1 < nk) store(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  float* __restrict__ dw = p.dw + (long)client * p.dw_cs;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int r = r0 + wn0 + j * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wm0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (co < p.Co && r < p.R) {
+          float* dst = dw + (long)co * p.R + r;
+          if (p.splitk > 1)
+            atomicAdd(dst, acc[i][j][e]);
+          else
+            *dst = acc[i][j][e];
+        }
+      }
+    }
+  }
+}
+
+template <int BMc, int BNr, int BKT, int WM, int WN, int NBUF, bool ALLV>
+bool launch_tn_f32_cfg(const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
+#define TNF_CASE(A, B)                                                                                          \
+  if (va == A && vb == B) {                                                                                     \
+    hipLaunchKernelGGL((conv_tn_f32_kernel<BMc, BNr, BKT, WM, WN, A, B, NBUF>), dim3(grid), dim3(WM * WN * 64), \
+                       0, s, p);                                                                                \
+    return true;                                                                                                \
+  }
+  TNF_CASE(8, 8)
+  if constexpr (ALLV) {
+    TNF_CASE(4, 4) TNF_CASE(8, 4) TNF_CASE(4, 8) TNF_CASE(1, 1) TNF_CASE(8, 1) TNF_CASE(1, 8) TNF_CASE(4, 1)
+    TNF_CASE(1, 4)
+  }
+#undef TNF_CASE
+  return false;
+}
+
+struct TnTile {
+  int bm, bn;
+};
+constexpr TnTile kTnF32Tiles[] = {{128, 128}, {64, 128}, {128, 128}, {256, 128}, {128, 256}, {64, 64}};
+constexpr int kTnF32Variants = sizeof(kTnF32Tiles) / sizeof(kTnF32Tiles[0]);
+constexpr int TN_BKT_MAX = 32;
+
+bool launch_tn_f32_variant(int v, const ConvTNParams& p, int va, int vb, int grid, hipStream_t s) {
+  switch (v) {
+    case 0: return launch_tn_f32_cfg<128, 128, 32, 2, 2, 2, true>(p, va, vb, grid, s);  // 80 KB
+    case 1: return launch_tn_f32_cfg<64, 128, 32, 2, 2, 2, true>(p, va, vb, grid, s);   // 60 KB
+    case 2: return launch_tn_f32_cfg<128, 128, 32, 2, 2, 1, false>(p, va, vb, grid, s);  // 40 KB
+    case 3: return launch_tn_f32_cfg<256, 128, 32, 4, 2, 1, false>(p, va, vb, grid, s);  // 60 KB
+    case 4: return launch_tn_f32_cfg<128, 256, 32, 2, 4, 1, false>(p, va, vb, grid, s);  // 60 KB
+    case 5: return launch_tn_f32_cfg<64, 64, 32, 2, 2, 2, true>(p, va, vb, grid, s);    // 40 KB
+    default: return false;
+  }
+}
+
+int tn_f32_default_variant(int K, int Co, int R) {
+  auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
+  if (Co <= 32 || R <= 64) return 5;
+  if (Co <= 64) return 1;
+  if (Co >= 256 && tiles(256, 128) >= 1024) return 3;
+  return 0;
+}
+
+int resolve_tn_f32_variant(int variant, int K, int Co, int R, int va, int vb) {
+  if (variant < 0 || variant >= kTnF32Variants) variant = tn_f32_default_variant(K, Co, R);
+  if ((va != 8 || vb != 8) && !(variant == 0 || variant == 1 || variant == 5)) variant = Co <= 64 ? 1 : 0;
+  return variant;
+}
+
+void tn_f32_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
+  const TnTile t = kTnF32Tiles[variant];
+  const long tiles = (long)K * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  splitk = 1;
+  const int target = 1024;  // >= 4 blocks per CU
+  if (tiles < target) {
+    splitk = (int)((target + tiles - 1) / tiles);
+    splitk = min(splitk, max(1, M / (4 * TN_BKT_MAX)));
+  }
+  mps = cdiv(M, splitk);
+  mps = ((mps + TN_BKT_MAX - 1) / TN_BKT_MAX) * TN_BKT_MAX;
+  splitk = cdiv(M, mps);
+}
+
+}  // namespace
+
+int conv_nt_f32_num_variants() { return 8; }
+
+void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
+  const bool bkm = p.b_kmajor != 0;
+  const int va = vw(p.C);
+  int vb = bkm ? vw(p.N) : vw(p.R);
+  if (variant < 0) {
+    if (p.N <= 64)
+      variant = bkm ? 6 : 4;
+    else
+      variant = 0;
+  }
+  // variants without the requested vector widths fall back to the all-widths 64x64 tile
+  const bool v88 = va == 8 && vb == 8;
+  const bool v84 = (va == 8 || va == 4) && (vb == 8 || vb == 4);
+  if (!v88) {
+    if (!v84 && variant != 3) variant = 3;
+    if (v84 && !(variant == 0 || variant == 3 || variant == 4 || variant == 7)) variant = p.N <= 64 ? 4 : 0;
+  }
+  if (!launch_nt_f32_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt_f32: bad variant %d\n", variant);
+}
+
+int conv_tn_f32_num_variants() { return kTnF32Variants; }
+
+void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s) {
+  const int va = vw(p.Co);
+  const int vb = vw(p.C);
+  variant = resolve_tn_f32_variant(variant, K, p.Co, p.R, va, vb);
+  tn_f32_split(K, p.Co, p.R, p.M, variant, p.splitk, p.m_per_split);
+  const TnTile t = kTnF32Tiles[variant];
+  const long tiles = (long)K * cdiv(p.Co, t.bm) * cdiv(p.R, t.bn);
+  const int grid = (int)(tiles * p.splitk);
+  if (!launch_tn_f32_variant(variant, p, va, vb, grid, s)) fprintf(stderr, "conv_tn_f32: bad variant %d\n", variant);
+}
+
+int conv_tn_f32_splitk(int K, int Co, int R, int M, int C, int variant) {
+  int splitk, mps;
+  variant = resolve_tn_f32_variant(variant, K, Co, R, vw(Co), vw(C));
+  tn_f32_split(K, Co, R, M, variant, splitk, mps);
+  return splitk;
+}

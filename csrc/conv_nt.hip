@@ -374,6 +374,10 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   p.fd_ow = make_fastdiv((uint32_t)p.OW);
   p.fd_kwc = make_fastdiv((uint32_t)(p.KW * p.C));
   p.fd_c = make_fastdiv((uint32_t)p.C);
+  if (p.f32) {  // reference precision: split-bf16 MFMA kernels (conv_f32.hip)
+    conv_nt_f32(p, K, variant, s);
+    return;
+  }
   const bool bkm = p.b_kmajor != 0;
   int va = vec_width(p.C);
   int vb = bkm ? vec_width(p.N) : vec_width(p.R);
@@ -396,8 +400,9 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
 }
 
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
-                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, hipStream_t s) {
+                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s) {
   ConvNTParams p{};
+  p.f32 = f32;
   p.x = dy;
   p.w = w;
   p.y = dx;
@@ -436,7 +441,7 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
     // N <= 64 full-correlation dgrad (ResNet l1): the 256x64 BK32 single-buffer tile streams the
     // k-major weight rows best — l1 dgrad 420-435 vs 377-385 TFLOP/s for the 64x64 tile at 13 and
     // 100 clients (bench/kernel_bench.py --sweep); the stride-2 parity classes keep the 64x64 tile
-    if (variant < 0 && Ci <= 64 && vec_width(Ci) == 8 && vec_width(Co) == 8) variant = 14;
+    if (variant < 0 && !f32 && Ci <= 64 && vec_width(Ci) == 8 && vec_width(Co) == 8) variant = 14;
     conv_nt(p, K, variant, s);
     return;
   }

@@ -273,6 +273,10 @@ int conv_tn_num_variants() { return kTnVariants; }
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s) {
   p.fd_ohw = make_fastdiv((uint32_t)(p.OH * p.OW));
   p.fd_ow = make_fastdiv((uint32_t)p.OW);
+  if (p.f32) {  // reference precision: split-bf16 MFMA kernel (conv_f32.hip)
+    conv_tn_f32(p, K, variant, s);
+    return;
+  }
   const int va = vec_width(p.Co);
   const int vb = vec_width(p.C);
   variant = resolve_tn_variant(variant, K, p.Co, p.R, va, vb);
@@ -283,7 +287,8 @@ void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s) {
   if (!launch_tn_variant(variant, p, va, vb, grid, s)) fprintf(stderr, "conv_tn: bad variant %d\n", variant);
 }
 
-int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant) {
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32) {
+  if (f32) return conv_tn_f32_splitk(K, Co, R, M, C, variant);
   int splitk, mps;
   variant = resolve_tn_variant(variant, K, Co, R, vec_width(Co), vec_width(C));
   tn_split(K, Co, R, M, variant, splitk, mps);

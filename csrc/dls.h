@@ -46,6 +46,9 @@ struct ConvNTParams {
   // output row remap (sub-pixel dgrad): GEMM row (b, oh, ow) → dx pixel (oh·out_s+out_ph, ow·out_s+out_pw)
   int out_s, out_ph, out_pw, out_H, out_W;
   FastDiv fd_ohw, fd_ow, fd_kwc, fd_c;  // filled by conv_nt()
+  // 1: every tensor pointer above is fp32 (reference precision); the GEMM runs as split-bf16
+  // ("bf16x3") on the MFMA with fp32 accumulation (conv_f32.hip)
+  int f32;
 };
 
 struct ConvTNParams {
@@ -57,6 +60,7 @@ struct ConvTNParams {
   int M, Co, R;
   int splitk, m_per_split;
   FastDiv fd_ohw, fd_ow;  // filled by conv_tn()
+  int f32;                // 1: dy / x are fp32 (split-bf16 GEMM, conv_f32.hip)
 };
 
 // Large-tile conv GEMM fed by the LDS-DMA (conv_gl.hip): K loop over a tap table × 64-channel
@@ -99,39 +103,47 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // dX of a conv (any stride): stride-1 → one flipped-weight NT GEMM; stride s > 1 → s² parity
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
-                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, hipStream_t s);
+                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s);
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
-int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant);
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32);
+// fp32 (split-bf16 MFMA) GEMMs, conv_f32.hip; reached through conv_nt / conv_tn with p.f32 = 1
+void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s);
+int conv_nt_f32_num_variants();
+void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s);
+int conv_tn_f32_num_variants();
+int conv_tn_f32_splitk(int K, int Co, int R, int M, int C, int variant);
 
 // ---------------------------------------------------------------- normalisation
+// Activation / γ / β pointers are the compute dtype: bf16 (f32 = 0) or fp32 (f32 = 1, the
+// reference precision); statistics, coefficients and parameter gradients are always fp32.
 long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd
-void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
-            float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
-            float* ws, uint8_t* relu_mask, unsigned* counters,
+void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
+            const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
+            uint8_t* relu_mask, unsigned* counters, int f32,
             hipStream_t s);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused coefs)
-void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
-            const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
-            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask,
-            unsigned* counters, hipStream_t s);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate
-void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,
-            long g_cs, int K, long rows_per_client, int C, float eps, int rep, hipStream_t s);
-void ln_bwd(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd, const bf16_t* gamma,
-            long g_cs, int K, long rows_per_client, int C, bf16_t* dx, float* dgamma, float* dbeta, long dg_cs,
-            float* ws, hipStream_t s);
-void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s);
+void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
+            const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
+            float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, unsigned* counters, int f32,
+            hipStream_t s);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate
+void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
+            long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s);
+void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,
+            long rows_per_client, int C, void* dx, float* dgamma, float* dbeta, long dg_cs, float* ws, int f32,
+            hipStream_t s);
+void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, int f32, hipStream_t s);
 
 // ------------------------------------------------------------------- elementwise
-void pool_fwd(const bf16_t* x, bf16_t* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k,
-              int stride, int pad, int mode, hipStream_t s);
-void pool_bwd(const bf16_t* dy, const int* idx, bf16_t* dx, int K, int B, int H, int W, int C, int OH, int OW,
-              int k, int stride, int pad, int mode, hipStream_t s);
-void gap_fwd(const bf16_t* x, bf16_t* y, int KB, int HW, int C, hipStream_t s);
-void gap_bwd(const bf16_t* dy, bf16_t* dx, int KB, int HW, int C, hipStream_t s);
-void ce_fwd_bwd(const bf16_t* logits, const int* labels, const int* valid, float* loss, float* correct,
-                bf16_t* dlogits, int K, int B, int NC, hipStream_t s);
-void relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s);
+void pool_fwd(const void* x, void* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
+              int pad, int mode, int f32, hipStream_t s);
+void pool_bwd(const void* dy, const int* idx, void* dx, int K, int B, int H, int W, int C, int OH, int OW, int k,
+              int stride, int pad, int mode, int f32, hipStream_t s);
+void gap_fwd(const void* x, void* y, int KB, int HW, int C, int f32, hipStream_t s);
+void gap_bwd(const void* dy, void* dx, int KB, int HW, int C, int f32, hipStream_t s);
+void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* loss, float* correct, void* dlogits,
+                int K, int B, int NC, int f32, hipStream_t s);
+void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStream_t s);
 
 // ------------------------------------------------------------- FL / optimiser
 void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
@@ -143,7 +155,7 @@ void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shad
 void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s);
 void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s);
 void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s);
-void mix_rows(const float* x, const float* w, bf16_t* out, int K, int M, long P, long ld, long ld_out,
+void mix_rows(const float* x, const float* w, void* out, int K, int M, long P, long ld, long ld_out, int f32,
               hipStream_t s);
 void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
                          long ld, hipStream_t s);
@@ -158,17 +170,17 @@ void nnadq_qdq(float* x, const int* seg, const float* lo, const float* scale, co
                long ld, int nseg, hipStream_t s);
 void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s);
 void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, long P, hipStream_t s);
-void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, long n_tok, int D, long t_cs,
-                   int rep, hipStream_t s);
-void embedding_bwd(const int* tokens, const bf16_t* dy, float* dtable, int K, long n_tok, int D, long t_cs,
+void embedding_fwd(const int* tokens, const void* table, void* out, int K, long n_tok, int D, long t_cs, int rep,
+                   int f32, hipStream_t s);
+void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long n_tok, int D, long t_cs, int f32,
                    hipStream_t s);
 // --------------------------------------------------------------- attention / graph
 bool attn_supported(int L, int DH);
-bool attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const int* key_valid, bf16_t* o, float* lse, long KBH,
-              int H, int L, int DH, hipStream_t s);
-bool attn_bwd(const bf16_t* dout, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const float* lse,
-              const int* key_valid, bf16_t* dq, bf16_t* dk, bf16_t* dv, float* delta, long KBH, int H, int L, int DH,
+bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
+              int L, int DH, int f32, hipStream_t s);
+bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
+              const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
               hipStream_t s);
-void spmm(const int* rowptr, const int* col, const float* val, const bf16_t* x, bf16_t* y, int K, int N, int Nx, int F,
-          long x_cs, long y_cs, hipStream_t s);
-void gather_rows(const bf16_t* src, const int* idx, bf16_t* dst, long n, long row_elems, hipStream_t s);
+void spmm(const int* rowptr, const int* col, const float* val, const void* x, void* y, int K, int N, int Nx, int F,
+          long x_cs, long y_cs, int f32, hipStream_t s);
+void gather_rows(const void* src, const int* idx, void* dst, long n, long row_bytes, hipStream_t s);

@@ -19,7 +19,8 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t seed) {
 
 // ------------------------------------------------------------------ pooling (NHWC)
 // mode 0 = max (records argmax as flat input spatial index), 1 = average
-__global__ void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int* __restrict__ idx,
+template <typename T>
+__global__ void pool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int* __restrict__ idx,
                                 long total, int H, int W, int C, int OH, int OW, int k, int stride, int pad,
                                 int mode) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -30,7 +31,7 @@ __global__ void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict
   t /= OW;
   const int oh = t % OH;
   const long img = t / OH;
-  const bf16_t* xi = x + img * H * W * C;
+  const T* xi = x + img * H * W * C;
   float best = -INFINITY, acc = 0.f;
   int bi = -1;
   for (int a = 0; a < k; ++a) {
@@ -39,7 +40,7 @@ __global__ void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict
     for (int b = 0; b < k; ++b) {
       const int iw = ow * stride - pad + b;
       if (iw < 0 || iw >= W) continue;
-      const float v = bf2f(xi[((long)ih * W + iw) * C + c]);
+      const float v = ldf(xi + ((long)ih * W + iw) * C + c);
       if (mode == 0) {
         if (v > best) {
           best = v;
@@ -51,15 +52,16 @@ __global__ void pool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict
     }
   }
   if (mode == 0) {
-    y[i] = f2bf(best);
+    stf(y + i, best);
     idx[i] = bi;
   } else {
-    y[i] = f2bf(acc / (float)(k * k));
+    stf(y + i, acc / (float)(k * k));
   }
 }
 
 // gather-form backward (no atomics): each input element sums the windows that cover it
-__global__ void pool_bwd_kernel(const bf16_t* __restrict__ dy, const int* __restrict__ idx, bf16_t* __restrict__ dx,
+template <typename T>
+__global__ void pool_bwd_kernel(const T* __restrict__ dy, const int* __restrict__ idx, T* __restrict__ dx,
                                 long total, int H, int W, int C, int OH, int OW, int k, int stride, int pad,
                                 int mode) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -80,20 +82,21 @@ __global__ void pool_bwd_kernel(const bf16_t* __restrict__ dy, const int* __rest
       if (iw + pad - ow * stride < 0 || iw + pad - ow * stride >= k) continue;
       const long o = obase + ((long)oh * OW + ow) * C + c;
       if (mode == 0) {
-        if (idx[o] == ih * W + iw) acc += bf2f(dy[o]);
+        if (idx[o] == ih * W + iw) acc += ldf(dy + o);
       } else {
-        acc += bf2f(dy[o]) / (float)(k * k);
+        acc += ldf(dy + o) / (float)(k * k);
       }
     }
   }
-  dx[i] = f2bf(acc);
+  stf(dx + i, acc);
 }
 
 // 8-channel form (C % 8 == 0): one thread per (input pixel, 8 channels) — 16-B dy loads and dx
 // stores, 2 × 16-B index loads per window, one window-range computation per 8 channels (the
 // scalar form is integer-divide and 2-B-access bound: ResNet-50's 112² stem pool, 12 ms/call)
-__global__ void __launch_bounds__(256) pool_bwd8_kernel(const bf16_t* __restrict__ dy, const int* __restrict__ idx,
-                                                        bf16_t* __restrict__ dx, long total8, int H, int W, int C,
+template <typename T>
+__global__ void __launch_bounds__(256) pool_bwd8_kernel(const T* __restrict__ dy, const int* __restrict__ idx,
+                                                        T* __restrict__ dx, long total8, int H, int W, int C,
                                                         int OH, int OW, int k, int stride, int pad, int mode) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total8) return;
@@ -118,7 +121,7 @@ __global__ void __launch_bounds__(256) pool_bwd8_kernel(const bf16_t* __restrict
       if (iw + pad - ow * stride < 0 || iw + pad - ow * stride >= k) continue;
       const long o = obase + ((long)oh * OW + ow) * C;
       float g[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+      load_vec<8>(dy + o, g);
       if (mode == 0) {
         const int4 a = *reinterpret_cast<const int4*>(idx + o);
         const int4 b = *reinterpret_cast<const int4*>(idx + o + 4);
@@ -131,34 +134,37 @@ __global__ void __launch_bounds__(256) pool_bwd8_kernel(const bf16_t* __restrict
       }
     }
   }
-  *reinterpret_cast<uint4*>(dx + pix * C + c0) = pack8(acc);
+  store_vec<8>(dx + pix * C + c0, acc);
 }
 
 // global average pool: [KB][HW][C] -> [KB][C]
-__global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int HW, int C, long total) {
+template <typename T>
+__global__ void gap_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int HW, int C, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const long img = i / C;
   const int c = i % C;
-  const bf16_t* p = x + img * HW * C + c;
+  const T* p = x + img * HW * C + c;
   float s = 0.f;
-  for (int j = 0; j < HW; ++j) s += bf2f(p[(long)j * C]);
-  y[i] = f2bf(s / HW);
+  for (int j = 0; j < HW; ++j) s += ldf(p + (long)j * C);
+  stf(y + i, s / HW);
 }
 
-__global__ void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int HW, int C, long total) {
+template <typename T>
+__global__ void gap_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int HW, int C, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = i % C;
   const long img = i / ((long)HW * C);
-  dx[i] = f2bf(bf2f(dy[img * C + c]) / HW);
+  stf(dx + i, ldf(dy + img * C + c) / HW);
 }
 
 // fused softmax cross-entropy: one wave per sample row; per-client mean over valid rows.
 // Writes loss[K] (mean), correct[K] and dlogits = (softmax - onehot)/n_k (0 on padded rows).
-__global__ void __launch_bounds__(256) ce_kernel(const bf16_t* __restrict__ logits, const int* __restrict__ labels,
+template <typename T>
+__global__ void __launch_bounds__(256) ce_kernel(const T* __restrict__ logits, const int* __restrict__ labels,
                                                  const int* __restrict__ valid, float* __restrict__ loss,
-                                                 float* __restrict__ correct, bf16_t* __restrict__ dlogits, int B,
+                                                 float* __restrict__ correct, T* __restrict__ dlogits, int B,
                                                  int NC) {
   const int k = blockIdx.y;
   const int lane = threadIdx.x & 63;
@@ -167,14 +173,14 @@ __global__ void __launch_bounds__(256) ce_kernel(const bf16_t* __restrict__ logi
   const int nv = valid ? valid[k] : B;
   const long off = ((long)k * B + row) * NC;
   if (row >= nv) {
-    for (int c = lane; c < NC; c += 64) dlogits[off + c] = 0;
+    for (int c = lane; c < NC; c += 64) stf(dlogits + off + c, 0.f);
     return;
   }
   const float inv_n = 1.f / (float)max(nv, 1);
   float mx = -INFINITY;
   int amax = 0;
   for (int c = lane; c < NC; c += 64) {
-    const float v = bf2f(logits[off + c]);
+    const float v = ldf(logits + off + c);
     if (v > mx) {
       mx = v;
       amax = c;
@@ -190,25 +196,25 @@ __global__ void __launch_bounds__(256) ce_kernel(const bf16_t* __restrict__ logi
     }
   }
   float se = 0.f;
-  for (int c = lane; c < NC; c += 64) se += __expf(bf2f(logits[off + c]) - mx);
+  for (int c = lane; c < NC; c += 64) se += expf(ldf(logits + off + c) - mx);
   se = wave_sum(se);
-  const float lse = mx + __logf(se);
+  const float lse = mx + logf(se);
   const int lab = labels[(long)k * B + row];
   for (int c = lane; c < NC; c += 64) {
-    const float pr = __expf(bf2f(logits[off + c]) - lse);
-    dlogits[off + c] = f2bf((pr - (c == lab ? 1.f : 0.f)) * inv_n);
+    const float pr = expf(ldf(logits + off + c) - lse);
+    stf(dlogits + off + c, (pr - (c == lab ? 1.f : 0.f)) * inv_n);
   }
   if (lane == 0) {
-    const float nll = lse - bf2f(logits[off + lab]);
+    const float nll = lse - ldf(logits + off + lab);
     atomicAdd(&loss[k], nll * inv_n);
     if (amax == lab) atomicAdd(&correct[k], 1.f);
   }
 }
 
-__global__ void relu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, bf16_t* __restrict__ dx,
-                                long n) {
+template <typename T>
+__global__ void relu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dx[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
+  if (i < n) dx[i] = ldf(y + i) > 0.f ? dy[i] : (T)0;
 }
 
 // ------------------------------------------------------------- optimiser steps
@@ -329,8 +335,9 @@ __global__ void __launch_bounds__(256) weighted_sum_kernel(const float* __restri
 // sum re-reads all K rows for every model); fp32 accumulation, W staged in LDS.
 constexpr int MIX_M = 32;
 constexpr int MIX_KMAX = 256;
+template <typename T>
 __global__ void __launch_bounds__(256) mix_rows_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                       bf16_t* __restrict__ out, int K, int M, long P4, long ld,
+                                                       T* __restrict__ out, int K, int M, long P4, long ld,
                                                        long ld_out) {
   __shared__ float wl[MIX_M * MIX_KMAX];
   const int m0 = blockIdx.y * MIX_M;
@@ -354,12 +361,7 @@ __global__ void __launch_bounds__(256) mix_rows_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int m = 0; m < MIX_M; ++m) {
-      if (m < mn) {
-        uint2 u;
-        u.x = (uint32_t)f2bf(acc[m][0]) | ((uint32_t)f2bf(acc[m][1]) << 16);
-        u.y = (uint32_t)f2bf(acc[m][2]) | ((uint32_t)f2bf(acc[m][3]) << 16);
-        reinterpret_cast<uint2*>(out + (long)(m0 + m) * ld_out)[i] = u;
-      }
+      if (m < mn) store_vec<4>(out + (long)(m0 + m) * ld_out + 4 * i, acc[m]);
     }
   }
 }
@@ -518,8 +520,9 @@ __global__ void sign_vote_kernel(const uint8_t* __restrict__ packed, const uint8
   }
 }
 
-__global__ void embedding_fwd_kernel(const int* __restrict__ tok, const bf16_t* __restrict__ table,
-                                     bf16_t* __restrict__ out, long n_tok, int D, long t_cs, int rep, long total) {
+template <typename T>
+__global__ void embedding_fwd_kernel(const int* __restrict__ tok, const T* __restrict__ table,
+                                     T* __restrict__ out, long n_tok, int D, long t_cs, int rep, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const long row = i / D;
@@ -528,67 +531,82 @@ __global__ void embedding_fwd_kernel(const int* __restrict__ tok, const bf16_t* 
   out[i] = table[(long)(k / rep) * t_cs + (long)tok[row] * D + d];
 }
 
-__global__ void embedding_bwd_kernel(const int* __restrict__ tok, const bf16_t* __restrict__ dy,
+template <typename T>
+__global__ void embedding_bwd_kernel(const int* __restrict__ tok, const T* __restrict__ dy,
                                      float* __restrict__ dtable, long n_tok, int D, long t_cs, long total) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const long row = i / D;
   const int d = i % D;
   const int k = (int)(row / n_tok);
-  atomicAdd(&dtable[(long)k * t_cs + (long)tok[row] * D + d], bf2f(dy[i]));
+  atomicAdd(&dtable[(long)k * t_cs + (long)tok[row] * D + d], ldf(dy + i));
 }
 
-__global__ void gather_rows_kernel(const bf16_t* __restrict__ src, const int* __restrict__ idx,
-                                   bf16_t* __restrict__ dst, long n, long row_vec8) {
+__global__ void gather_rows_kernel(const uint4* __restrict__ src, const int* __restrict__ idx,
+                                   uint4* __restrict__ dst, long n, long row_vec8) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * row_vec8) return;
   const long r = i / row_vec8, c = i % row_vec8;
-  reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[(long)idx[r] * row_vec8 + c];
+  dst[i] = src[(long)idx[r] * row_vec8 + c];
 }
 
 int grid_for(long n, int per_block = 256, int cap = 4096) { return (int)max(1L, min((long)cap, (n + per_block - 1) / per_block)); }
 
 }  // namespace
 
-void pool_fwd(const bf16_t* x, bf16_t* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k,
-              int stride, int pad, int mode, hipStream_t s) {
+#define DISPATCH_T(F32, ...) \
+  if (F32) {                 \
+    typedef float TT;        \
+    __VA_ARGS__;             \
+  } else {                   \
+    typedef bf16_t TT;       \
+    __VA_ARGS__;             \
+  }
+#define CP(p) static_cast<const TT*>(p)
+#define MP(p) static_cast<TT*>(p)
+
+void pool_fwd(const void* x, void* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
+              int pad, int mode, int f32, hipStream_t s) {
   const long total = (long)K * B * OH * OW * C;
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, idx, total, H, W, C, OH, OW, k,
-                     stride, pad, mode);
+  DISPATCH_T(f32, hipLaunchKernelGGL(pool_fwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, CP(x), MP(y), idx,
+                                     total, H, W, C, OH, OW, k, stride, pad, mode));
 }
 
-void pool_bwd(const bf16_t* dy, const int* idx, bf16_t* dx, int K, int B, int H, int W, int C, int OH, int OW,
-              int k, int stride, int pad, int mode, hipStream_t s) {
+void pool_bwd(const void* dy, const int* idx, void* dx, int K, int B, int H, int W, int C, int OH, int OW, int k,
+              int stride, int pad, int mode, int f32, hipStream_t s) {
   const long total = (long)K * B * H * W * C;
   if (C % 8 == 0) {
-    hipLaunchKernelGGL(pool_bwd8_kernel, dim3(cdiv(total / 8, 256)), dim3(256), 0, s, dy, idx, dx, total / 8, H, W, C,
-                       OH, OW, k, stride, pad, mode);
+    DISPATCH_T(f32, hipLaunchKernelGGL(pool_bwd8_kernel<TT>, dim3(cdiv(total / 8, 256)), dim3(256), 0, s, CP(dy), idx,
+                                       MP(dx), total / 8, H, W, C, OH, OW, k, stride, pad, mode));
     return;
   }
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, idx, dx, total, H, W, C, OH, OW,
-                     k, stride, pad, mode);
+  DISPATCH_T(f32, hipLaunchKernelGGL(pool_bwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, CP(dy), idx, MP(dx),
+                                     total, H, W, C, OH, OW, k, stride, pad, mode));
 }
 
-void gap_fwd(const bf16_t* x, bf16_t* y, int KB, int HW, int C, hipStream_t s) {
+void gap_fwd(const void* x, void* y, int KB, int HW, int C, int f32, hipStream_t s) {
   const long total = (long)KB * C;
-  hipLaunchKernelGGL(gap_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, HW, C, total);
+  DISPATCH_T(f32, hipLaunchKernelGGL(gap_fwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, CP(x), MP(y), HW, C,
+                                     total));
 }
 
-void gap_bwd(const bf16_t* dy, bf16_t* dx, int KB, int HW, int C, hipStream_t s) {
+void gap_bwd(const void* dy, void* dx, int KB, int HW, int C, int f32, hipStream_t s) {
   const long total = (long)KB * HW * C;
-  hipLaunchKernelGGL(gap_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, dx, HW, C, total);
+  DISPATCH_T(f32, hipLaunchKernelGGL(gap_bwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, CP(dy), MP(dx), HW,
+                                     C, total));
 }
 
-void ce_fwd_bwd(const bf16_t* logits, const int* labels, const int* valid, float* loss, float* correct,
-                bf16_t* dlogits, int K, int B, int NC, hipStream_t s) {
+void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* loss, float* correct, void* dlogits,
+                int K, int B, int NC, int f32, hipStream_t s) {
   DLS_CHECK(hipMemsetAsync(loss, 0, sizeof(float) * K, s));
   DLS_CHECK(hipMemsetAsync(correct, 0, sizeof(float) * K, s));
-  hipLaunchKernelGGL(ce_kernel, dim3(cdiv(B, 4), K), dim3(256), 0, s, logits, labels, valid, loss, correct, dlogits,
-                     B, NC);
+  DISPATCH_T(f32, hipLaunchKernelGGL(ce_kernel<TT>, dim3(cdiv(B, 4), K), dim3(256), 0, s, CP(logits), labels, valid,
+                                     loss, correct, MP(dlogits), B, NC));
 }
 
-void relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t s) {
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, dy, y, dx, n);
+void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStream_t s) {
+  DISPATCH_T(f32, hipLaunchKernelGGL(relu_bwd_kernel<TT>, dim3(cdiv(n, 256)), dim3(256), 0, s, CP(dy), CP(y), MP(dx),
+                                     n));
 }
 
 void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
@@ -622,14 +640,15 @@ void weighted_sum(const float* x, const float* w, float* out, int K, long P, lon
   hipLaunchKernelGGL(weighted_sum_kernel, dim3(grid_for(P / 4, 256, 8192)), dim3(256), 0, s, x, w, out, K, P / 4, ld);
 }
 
-void mix_rows(const float* x, const float* w, bf16_t* out, int K, int M, long P, long ld, long ld_out,
+void mix_rows(const float* x, const float* w, void* out, int K, int M, long P, long ld, long ld_out, int f32,
               hipStream_t s) {
   if (K > MIX_KMAX || M <= 0) {  // the wrapper (ops/hip.py) routes larger K elsewhere
     DLS_CHECK(hipErrorInvalidValue);
     return;
   }
   dim3 grid(grid_for(P / 4, 256, 2048), cdiv(M, MIX_M));
-  hipLaunchKernelGGL(mix_rows_kernel, grid, dim3(256), 0, s, x, w, out, K, M, P / 4, ld, ld_out);
+  DISPATCH_T(f32, hipLaunchKernelGGL(mix_rows_kernel<TT>, grid, dim3(256), 0, s, x, w, MP(out), K, M, P / 4, ld,
+                                     ld_out));
 }
 
 void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
@@ -679,21 +698,22 @@ void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, 
                      (P + 7) / 8);
 }
 
-void embedding_fwd(const int* tokens, const bf16_t* table, bf16_t* out, int K, long n_tok, int D, long t_cs, int rep,
-                   hipStream_t s) {
+void embedding_fwd(const int* tokens, const void* table, void* out, int K, long n_tok, int D, long t_cs, int rep,
+                   int f32, hipStream_t s) {
   const long total = (long)K * n_tok * D;
-  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, table, out, n_tok, D,
-                     t_cs, rep, total);
+  DISPATCH_T(f32, hipLaunchKernelGGL(embedding_fwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens,
+                                     CP(table), MP(out), n_tok, D, t_cs, rep, total));
 }
 
-void embedding_bwd(const int* tokens, const bf16_t* dy, float* dtable, int K, long n_tok, int D, long t_cs,
+void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long n_tok, int D, long t_cs, int f32,
                    hipStream_t s) {
   const long total = (long)K * n_tok * D;
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, dy, dtable, n_tok, D,
-                     t_cs, total);
+  DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, CP(dy),
+                                     dtable, n_tok, D, t_cs, total));
 }
 
-void gather_rows(const bf16_t* src, const int* idx, bf16_t* dst, long n, long row_elems, hipStream_t s) {
-  const long v8 = row_elems / 8;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(n * v8, 256)), dim3(256), 0, s, src, idx, dst, n, v8);
+void gather_rows(const void* src, const int* idx, void* dst, long n, long row_bytes, hipStream_t s) {
+  const long v16 = row_bytes / 16;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(n * v16, 256)), dim3(256), 0, s, static_cast<const uint4*>(src), idx,
+                     static_cast<uint4*>(dst), n, v16);
 }

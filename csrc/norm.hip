@@ -13,37 +13,6 @@
 
 namespace {
 
-template <int V>
-__device__ __forceinline__ void load_vec(const bf16_t* p, float* f) {
-  if constexpr (V == 8) {
-    unpack8(*reinterpret_cast<const uint4*>(p), f);
-  } else if constexpr (V == 4) {
-    const uint2 u = *reinterpret_cast<const uint2*>(p);
-    f[0] = __uint_as_float(u.x << 16);
-    f[1] = __uint_as_float(u.x & 0xffff0000u);
-    f[2] = __uint_as_float(u.y << 16);
-    f[3] = __uint_as_float(u.y & 0xffff0000u);
-  } else {
-#pragma unroll
-    for (int i = 0; i < V; ++i) f[i] = bf2f(p[i]);
-  }
-}
-
-template <int V>
-__device__ __forceinline__ void store_vec(bf16_t* p, const float* f) {
-  if constexpr (V == 8) {
-    *reinterpret_cast<uint4*>(p) = pack8(f);
-  } else if constexpr (V == 4) {
-    uint2 u;
-    u.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-    u.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-    *reinterpret_cast<uint2*>(p) = u;
-  } else {
-#pragma unroll
-    for (int i = 0; i < V; ++i) p[i] = f2bf(f[i]);
-  }
-}
-
 constexpr int ROWS_PER_BLOCK = 512;  // upper bound; launches pick rows per block for >= ~2048 blocks
 
 // Rows per workgroup for a (clients × rows) channel pass: enough workgroups to fill 256 CUs
@@ -61,8 +30,8 @@ static int rows_per_block(long R, int K) {
 // agent-scope acquire) reduces them in fixed order and resets the ticket — one launch less per
 // BN pass and no separate tiny coefficient kernel.
 struct BNCoefArgs {
-  const bf16_t* gamma;
-  const bf16_t* beta;
+  const void* gamma;  // T (bf16 or fp32, the compute dtype)
+  const void* beta;
   const float* mean_in;
   const float* rstd_in;
   float* mean_out;
@@ -76,9 +45,10 @@ struct BNCoefArgs {
   unsigned* counters;  // [K], zero at launch; reset by the last workgroup of each client
 };
 
+template <typename T>
 __device__ __forceinline__ void bn_coef_math(float s0, float s1, int k, int c, int C, float n, const BNCoefArgs& a) {
   const long i = (long)k * C + c;
-  const float g = bf2f(a.gamma[(long)(k / a.rep) * a.g_cs + c]);
+  const float g = ldf(static_cast<const T*>(a.gamma) + (long)(k / a.rep) * a.g_cs + c);
   if (!a.bwd) {
     const float mu = s0 / n;
     const float var = fmaxf(s1 / n - mu * mu, 0.f);
@@ -87,7 +57,7 @@ __device__ __forceinline__ void bn_coef_math(float s0, float s1, int k, int c, i
     a.mean_out[i] = mu;
     a.rstd_out[i] = rs;
     a.coef[2 * i] = sc;
-    a.coef[2 * i + 1] = bf2f(a.beta[(long)(k / a.rep) * a.g_cs + c]) - mu * sc;
+    a.coef[2 * i + 1] = ldf(static_cast<const T*>(a.beta) + (long)(k / a.rep) * a.g_cs + c) - mu * sc;
   } else {
     const float mu = a.mean_in[i], rs = a.rstd_in[i];
     const float aa = g * rs;
@@ -107,9 +77,9 @@ __device__ __forceinline__ void bn_coef_math(float s0, float s1, int k, int c, i
 //   mode 0: s0 += x, s1 += x²                       (BN fwd stats)
 //   mode 1: g = dy*relu'(y); s0 += g, s1 += g*x̂      (BN bwd)
 //   mode 2: s0 += x                                  (column sums, bias grads)
-template <int V, int MODE>
-__global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
-                                                          const bf16_t* __restrict__ yv, const float* __restrict__ mean,
+template <typename T, int V, int MODE>
+__global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                          const T* __restrict__ yv, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd,
                                                           const int* __restrict__ valid_rows, int R, int C, int relu,
                                                           float* __restrict__ ws, long ws_cs, int rpb,
@@ -227,7 +197,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
       a0 += parts[(long)b * 2 * C + c];
       a1 += parts[(long)b * 2 * C + C + c];
     }
-    bn_coef_math(a0, a1, k, c, C, n, ca);
+    bn_coef_math<T>(a0, a1, k, c, C, n, ca);
   }
   if (tid == 0) atomicExch(&ca.counters[k], 0u);
 }
@@ -239,9 +209,10 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const bf16_t* __restri
 //        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
 // grid (cdiv(C, 32), K), 256 threads = 32 channels × 8 part-groups: the per-workgroup partial
 // sums of a client are reduced in a fixed order (deterministic) by 8 lanes per channel.
+template <typename T>
 __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ ws, int nparts,
-                                                      const bf16_t* __restrict__ gamma,
-                                                      const bf16_t* __restrict__ beta, const int* __restrict__ valid_rows,
+                                                      const T* __restrict__ gamma,
+                                                      const T* __restrict__ beta, const int* __restrict__ valid_rows,
                                                       const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                       float* __restrict__ coef, float* __restrict__ dgamma,
@@ -271,7 +242,7 @@ __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ 
   const long i = (long)k * C + c;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const float n = (float)max(nvalid, 1);
-  const float g = bf2f(gamma[(long)(k / rep) * g_cs + c]);
+  const float g = ldf(gamma + (long)(k / rep) * g_cs + c);
   if (!bwd) {
     const float mu = s0 / n;
     const float var = fmaxf(s1 / n - mu * mu, 0.f);
@@ -280,7 +251,7 @@ __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ 
     mean_out[i] = mu;
     rstd_out[i] = rs;
     coef[2 * i] = sc;
-    coef[2 * i + 1] = bf2f(beta[(long)(k / rep) * g_cs + c]) - mu * sc;
+    coef[2 * i + 1] = ldf(beta + (long)(k / rep) * g_cs + c) - mu * sc;
   } else {
     const float mu = mean_in[i], rs = rstd_in[i];
     const float a = g * rs;
@@ -297,9 +268,9 @@ __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ 
 }
 
 // thread owns one V-channel chunk and strides over rows; grid (row-blocks, K)
-template <int V>
-__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                                       bf16_t* __restrict__ y, const int* __restrict__ valid_rows,
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                       T* __restrict__ y, const int* __restrict__ valid_rows,
                                                        const float* __restrict__ coef, int R, int C, int relu,
                                                        int rpb, uint8_t* __restrict__ rmask) {
   const int k = blockIdx.y;
@@ -341,10 +312,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int j = 0; j < V; ++j) out[j] = 0.f;
       }
-      if (rmask) {  // bit j = (bf16(out_j) > 0): exactly the mask the backward would read from y
+      if (rmask) {  // bit j = (stored out_j > 0): exactly the mask the backward would read from y
         uint32_t m = 0;
 #pragma unroll
-        for (int j = 0; j < V; ++j) m |= (bf2f(f2bf(out[j])) > 0.f ? 1u : 0u) << j;
+        for (int j = 0; j < V; ++j) m |= (rt<T>(out[j]) > 0.f ? 1u : 0u) << j;
         rmask[((long)k * R + r) * (C / 8) + c0 / 8] = (uint8_t)m;
       }
       store_vec<V>(y + off, out);
@@ -352,12 +323,12 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-template <int V>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                           const bf16_t* __restrict__ y,
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                           const T* __restrict__ y,
                                                            const int* __restrict__ valid_rows,
                                                            const float* __restrict__ coef, int R, int C, int relu,
-                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre,
+                                                           T* __restrict__ dx, T* __restrict__ dpre,
                                                            int rpb, const uint8_t* __restrict__ rmask) {
   const int k = blockIdx.y;
   const int CT = C / V;
@@ -413,18 +384,19 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
 int vw(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : 1; }
 
 // ------------------------------------------------------------------ LayerNorm
-__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
-                                                     const bf16_t* __restrict__ beta, bf16_t* __restrict__ y,
+template <typename T>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ gamma,
+                                                     const T* __restrict__ beta, T* __restrict__ y,
                                                      float* __restrict__ mean, float* __restrict__ rstd, long g_cs,
                                                      long nrows, long rpc, int C, float eps, int rep) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
   const int k = (int)(row / rpc);
-  const bf16_t* xr = x + row * C;
+  const T* xr = x + row * C;
   float s = 0.f, sq = 0.f;
   for (int c = lane; c < C; c += 64) {
-    const float v = bf2f(xr[c]);
+    const float v = ldf(xr + c);
     s += v;
     sq += v * v;
   }
@@ -432,9 +404,9 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
   sq = wave_sum(sq);
   const float mu = s / C;
   const float rs = rsqrtf(fmaxf(sq / C - mu * mu, 0.f) + eps);
-  const bf16_t* g = gamma + (long)(k / rep) * g_cs;
-  const bf16_t* b = beta + (long)(k / rep) * g_cs;
-  for (int c = lane; c < C; c += 64) y[row * C + c] = f2bf((bf2f(xr[c]) - mu) * rs * bf2f(g[c]) + bf2f(b[c]));
+  const T* g = gamma + (long)(k / rep) * g_cs;
+  const T* b = beta + (long)(k / rep) * g_cs;
+  for (int c = lane; c < C; c += 64) stf(y + row * C + c, (ldf(xr + c) - mu) * rs * ldf(g + c) + ldf(b + c));
   if (lane == 0) {
     mean[row] = mu;
     rstd[row] = rs;
@@ -442,10 +414,11 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 }
 
 constexpr int LN_MAXC = 16;  // C <= 1024
-__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+template <typename T>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const bf16_t* __restrict__ gamma, long g_cs, long rpc, int C,
-                                                     bf16_t* __restrict__ dx, float* __restrict__ dgamma,
+                                                     const T* __restrict__ gamma, long g_cs, long rpc, int C,
+                                                     T* __restrict__ dx, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta, long dg_cs, int rows_per_wave) {
   // grid: (row-groups, K); each wave handles rows_per_wave rows of client k
   const int k = blockIdx.y;
@@ -453,7 +426,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long rbeg = wave * rows_per_wave;
   const long rend = min(rpc, rbeg + rows_per_wave);
-  const bf16_t* g = gamma + (long)k * g_cs;
+  const T* g = gamma + (long)k * g_cs;
   float dg[LN_MAXC], db[LN_MAXC];
 #pragma unroll
   for (int i = 0; i < LN_MAXC; ++i) dg[i] = db[i] = 0.f;
@@ -465,9 +438,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int i = 0; i < LN_MAXC; ++i) {
       const int c = lane + 64 * i;
       if (c < C) {
-        const float gy = bf2f(dy[row * C + c]);
-        const float xh = (bf2f(x[row * C + c]) - mu) * rs;
-        const float gg = gy * bf2f(g[c]);
+        const float gy = ldf(dy + row * C + c);
+        const float xh = (ldf(x + row * C + c) - mu) * rs;
+        const float gg = gy * ldf(g + c);
         a += gg;
         b += gg * xh;
         dg[i] += gy * xh;
@@ -480,9 +453,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     for (int i = 0; i < LN_MAXC; ++i) {
       const int c = lane + 64 * i;
       if (c < C) {
-        const float gy = bf2f(dy[row * C + c]);
-        const float xh = (bf2f(x[row * C + c]) - mu) * rs;
-        dx[row * C + c] = f2bf(rs * (gy * bf2f(g[c]) - a - xh * b));
+        const float gy = ldf(dy + row * C + c);
+        const float xh = (ldf(x + row * C + c) - mu) * rs;
+        stf(dx + row * C + c, rs * (gy * ldf(g + c) - a - xh * b));
       }
     }
   }
@@ -511,15 +484,26 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     constexpr int VV = 1;           \
     __VA_ARGS__;                    \
   }
+// element type of the activations / γ β: bf16 (f32 = 0) or fp32 (f32 = 1)
+#define DISPATCH_T(F32, ...)        \
+  if (F32) {                        \
+    typedef float TT;               \
+    __VA_ARGS__;                    \
+  } else {                          \
+    typedef bf16_t TT;              \
+    __VA_ARGS__;                    \
+  }
+#define CP(p) static_cast<const TT*>(p)
+#define MP(p) static_cast<TT*>(p)
 
 long bn_workspace_floats(int K, long R, int C) {
   const long parts = (R + rows_per_block(R, K) - 1) / rows_per_block(R, K);
   return (long)K * 3 * C + (long)K * parts * 2 * C;
 }
 
-void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16_t* res, bf16_t* y, float* mean,
-            float* rstd, const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep,
-            float* ws, uint8_t* rmask, unsigned* counters, hipStream_t s) {
+void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
+            const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
+            uint8_t* rmask, unsigned* counters, int f32, hipStream_t s) {
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
@@ -527,57 +511,63 @@ void bn_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, const bf16
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
   BNCoefArgs ca{gamma, beta, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, eps, rep, 0, counters};
-  DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 0>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr, ca));
-  if (!counters)
-    hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, beta,
-                       valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
   if (V != 8) rmask = nullptr;  // bit masks need 8-channel vectors
-  DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<VV>), grid, dim3(256), 0, s, x, res, y, valid_rows, coef, R, C,
-                                   relu, rpb, rmask));
+  DISPATCH_T(f32, {
+    DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 0>), grid, dim3(256), 0, s, CP(x), nullptr, nullptr,
+                                     nullptr, nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr, ca));
+    if (!counters)
+      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, CP(gamma),
+                         CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C,
+                         eps, rep, 0);
+    DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
+                                     valid_rows, coef, R, C, relu, rpb, rmask));
+  });
 }
 
-void bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean, const float* rstd,
-            const bf16_t* gamma, const int* valid_rows, long g_cs, int K, int R, int C, int relu, bf16_t* dx,
-            bf16_t* dpre, float* dgamma, float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters,
-            hipStream_t s) {
+void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
+            const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
+            float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s) {
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(C);
+  if (V != 8) rmask = nullptr;
   BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1, counters};
-  DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 1>), grid, dim3(256), 0, s, dy, x, y, mean, rstd,
-                                   valid_rows, R, C, relu, part, (long)2 * C, rpb, V == 8 ? rmask : nullptr, ca));
-  if (!counters)
-    hipLaunchKernelGGL(bn_coef_kernel, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, gamma, nullptr,
-                       valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K, R, C, 0.f, 1, 1);
-  DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<VV>), grid, dim3(256), 0, s, dy, x, y, valid_rows, coef, R, C,
-                                   relu, dx, dpre, rpb, V == 8 ? rmask : nullptr));
+  DISPATCH_T(f32, {
+    DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
+                                     mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca));
+    if (!counters)
+      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, CP(gamma),
+                         (const TT*)nullptr, valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs,
+                         g_cs, K, R, C, 0.f, 1, 1);
+    DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
+                                     valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask));
+  });
 }
 
-void col_sum(const bf16_t* x, float* out, long out_cs, int K, long rows, int C, hipStream_t s) {
+void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, int f32, hipStream_t s) {
   // out must be zeroed by the caller (it is a strided view of the grad buffer)
   const int rpb = rows_per_block(rows, K);
   dim3 grid(cdiv(rows, rpb), K);
   const int V = vw(C);
-  DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<VV, 2>), grid, dim3(256), 0, s, x, nullptr, nullptr, nullptr,
-                                   nullptr, nullptr, (int)rows, C, 0, out, out_cs, rpb, nullptr, BNCoefArgs{}));
+  DISPATCH_T(f32, DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 2>), grid, dim3(256), 0, s, CP(x),
+                                                   nullptr, nullptr, nullptr, nullptr, nullptr, (int)rows, C, 0, out,
+                                                   out_cs, rpb, nullptr, BNCoefArgs{})));
 }
 
-void ln_fwd(const bf16_t* x, const bf16_t* gamma, const bf16_t* beta, bf16_t* y, float* mean, float* rstd,
-            long g_cs, int K, long rpc, int C, float eps, int rep, hipStream_t s) {
+void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
+            long rpc, int C, float eps, int rep, int f32, hipStream_t s) {
   const long nrows = (long)K * rpc;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(nrows, 4)), dim3(256), 0, s, x, gamma, beta, y, mean, rstd, g_cs,
-                     nrows, rpc, C, eps, rep);
+  DISPATCH_T(f32, hipLaunchKernelGGL(ln_fwd_kernel<TT>, dim3(cdiv(nrows, 4)), dim3(256), 0, s, CP(x), CP(gamma),
+                                     CP(beta), MP(y), mean, rstd, g_cs, nrows, rpc, C, eps, rep));
 }
 
-void ln_bwd(const bf16_t* dy, const bf16_t* x, const float* mean, const float* rstd, const bf16_t* gamma,
-            long g_cs, int K, long rpc, int C, bf16_t* dx, float* dgamma, float* dbeta, long dg_cs, float* ws,
-            hipStream_t s) {
+void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,
+            long rpc, int C, void* dx, float* dgamma, float* dbeta, long dg_cs, float* ws, int f32, hipStream_t s) {
   const int rows_per_wave = 16;
   const long waves = (rpc + rows_per_wave - 1) / rows_per_wave;
   dim3 grid(cdiv(waves, 4), K);
-  hipLaunchKernelGGL(ln_bwd_kernel, grid, dim3(256), 0, s, dy, x, mean, rstd, gamma, g_cs, rpc, C, dx, dgamma, dbeta,
-                     dg_cs, rows_per_wave);
+  DISPATCH_T(f32, hipLaunchKernelGGL(ln_bwd_kernel<TT>, grid, dim3(256), 0, s, CP(dy), CP(x), mean, rstd, CP(gamma),
+                                     g_cs, rpc, C, MP(dx), dgamma, dbeta, dg_cs, rows_per_wave));
 }

@@ -72,7 +72,7 @@ class DistributedTrainingConfig:
     debug: bool = False
     # --- MI355X-native knobs ---
     seed: int = 0
-    compute_dtype: str = "auto"  # auto => bf16 on GPU, fp32 on CPU
+    compute_dtype: str = "auto"  # auto => fp32 unless use_amp (then bf16 on GPU)
     backend: str = "auto"  # auto => hip kernels on GPU, torch oracle on CPU
     cohort_size: int = 0  # max clients resident per rank (0 => all of them)
     eval_batch_size: int = 0  # 0 => batch_size (BN uses batch stats, so it matters)

@@ -148,7 +148,7 @@ class ImageDataset:
         if self.data is not None:
             from ..ops import backend
 
-            if backend.using_hip(self.data) and self.data[0].numel() % 8 == 0:
+            if backend.using_hip(self.data) and (self.data[0].numel() * self.data.element_size()) % 16 == 0:
                 from ..ops import hip
 
                 return hip.gather_rows(self.data, idx).reshape(*idx.shape, *self.shape)

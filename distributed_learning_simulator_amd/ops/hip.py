@@ -24,7 +24,16 @@ except ImportError as e:  # pragma: no cover - exercised only on a GPU box witho
     ) from e
 
 BF16 = torch.bfloat16
+F32 = torch.float32
 NULL = 0
+_DTYPES = (BF16, F32)
+
+
+def _f32(t: torch.Tensor) -> int:
+    """Kernel element-type flag of an activation tensor: bf16 (fast mode) or fp32 (reference
+    precision: the GEMMs then run as split-bf16 MFMA, csrc/conv_f32.hip)."""
+    assert t.dtype in _DTYPES, f"unsupported activation dtype {t.dtype}"
+    return int(t.dtype == F32)
 
 
 def _s() -> int:
@@ -115,24 +124,26 @@ def _gl(K: int, M: int, N: int, C: int, taps: int) -> bool:
 def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
     K, B, H, W, C = x.shape
     x = x.contiguous()
-    _check(x, BF16, name="x")
-    _check(w, BF16, contiguous=False, name="w")
+    f32 = _f32(x)
+    _check(x, x.dtype, name="x")
+    _check(w, x.dtype, contiguous=False, name="w")
     Kw, Co, KH, KW, Ci = w.shape
     assert Ci == C, (Ci, C)
     w_cs, rep = _client_view(w, K)
     OH = (H + 2 * pad - KH) // stride + 1
     OW = (W + 2 * pad - KW) // stride + 1
-    y = torch.empty((K, B, OH, OW, Co), dtype=BF16, device=x.device)
+    y = torch.empty((K, B, OH, OW, Co), dtype=x.dtype, device=x.device)
     b_cs = 0
     if bias is not None:
+        assert bias.dtype == x.dtype
         b_cs, _ = _client_view(bias, K)
     M = B * OH * OW
-    if _gl(K, M, Co, C, KH * KW):
+    if not f32 and _gl(K, M, Co, C, KH * KW):
         _C.conv_gl_fwd(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, K, rep, B, H, W, C, OH, OW,
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
-               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_variant, NULL, NULL, _s())
+               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, -1 if f32 else nt_variant, NULL, NULL, f32, _s())
     return y
 
 
@@ -141,15 +152,16 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
     residual branch of a ResNet block, so autograd never materialises the sum separately)."""
     K, B, OH, OW, Co = dy.shape
     dy = dy.contiguous()
-    _check(dy, BF16, name="dy")
+    f32 = _f32(dy)
+    _check(w, dy.dtype, contiguous=False, name="w")
     Kw, Co2, KH, KW, Ci = w.shape
     assert Co2 == Co
     w_cs, rep = _client_view(w, K)
     H, W = int(in_hw[0]), int(in_hw[1])
-    dx = torch.empty((K, B, H, W, Ci), dtype=BF16, device=dy.device)
+    dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
     if acc is not None:
-        assert stride == 1 and acc.shape == dx.shape and acc.dtype == BF16 and acc.is_contiguous(), acc.shape
-    if (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
+        assert stride == 1 and acc.shape == dx.shape and acc.dtype == dy.dtype and acc.is_contiguous(), acc.shape
+    if not f32 and (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
         # (strided dgrad splits into stride² short-K parity classes: conv_nt's smaller tiles win
         # there, l3a dgrad 447 vs 396 TFLOP/s). Large tiles want a k-contiguous B: one flip+transpose pass over the weight rows
         # (weights are small next to the activations), then stride² parity-class launches
@@ -159,8 +171,8 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
         return dx
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
-    _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad, nt_variant,
-                  _s())
+    _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
+                  -1 if f32 else nt_variant, f32, _s())
     return dx
 
 
@@ -169,17 +181,18 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int):
     _, _, H, W, C = x.shape
     dy = dy.contiguous()
     x = x.contiguous()
-    _check(dy, BF16, name="dy")
-    _check(x, BF16, name="x")
+    f32 = _f32(dy)
+    _check(x, dy.dtype, name="x")
     assert gw.dtype == torch.float32 and gw.shape[0] == K and gw[0].is_contiguous()
     _, Co2, KH, KW, Ci = gw.shape
     assert Co2 == Co and Ci == C
     M = B * OH * OW
     R = KH * KW * C
-    if _C.conv_tn_splitk(K, Co, R, M, C, tn_variant) > 1:
+    tv = -1 if f32 else tn_variant
+    if _C.conv_tn_splitk(K, Co, R, M, C, tv, f32) > 1:
         gw.zero_()
     _C.conv_tn(_p(dy), _p(x), _p(gw), M * Co, B * H * W * C, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M,
-               Co, R, K, tn_variant, _s())
+               Co, R, K, tv, f32, _s())
 
 
 def bias_grad(dy, gb):
@@ -188,7 +201,7 @@ def bias_grad(dy, gb):
     C = dy.shape[-1]
     rows = dy.numel() // (K * C)
     gb.zero_()
-    _C.col_sum(_p(dy.contiguous()), _p(gb), gb.stride(0), K, rows, C, _s())
+    _C.col_sum(_p(dy.contiguous()), _p(gb), gb.stride(0), K, rows, C, _f32(dy), _s())
 
 
 # --------------------------------------------------------------------------- linear
@@ -196,15 +209,16 @@ def linear_fwd(x, w, b=None, relu=False, acc=None):
     """y = x Wᵀ + b, optionally ReLU'd and/or + `acc` (a residual branch) in the epilogue."""
     K, N, Fi = x.shape
     x = x.contiguous()
+    f32 = _f32(x)
     Kw, Fo, Fi2 = w.shape
-    assert Fi2 == Fi
+    assert Fi2 == Fi and w.dtype == x.dtype
     w_cs, rep = _client_view(w, K)
     b_cs = _client_view(b, K)[0] if b is not None else 0
-    y = torch.empty((K, N, Fo), dtype=BF16, device=x.device)
+    y = torch.empty((K, N, Fo), dtype=x.dtype, device=x.device)
     if acc is not None:
-        assert acc.shape == y.shape and acc.dtype == BF16 and acc.is_contiguous()
+        assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               int(relu), K, 0, nt_variant, _p(acc), NULL, _s())
+               int(relu), K, 0, -1 if f32 else nt_variant, _p(acc), NULL, f32, _s())
     return y
 
 
@@ -213,14 +227,16 @@ def linear_dgrad(dy, w, gate=None):
     the gradient then leaves already through the ReLU)."""
     K, N, Fo = dy.shape
     dy = dy.contiguous()
+    f32 = _f32(dy)
     Kw, Fo2, Fi = w.shape
+    assert w.dtype == dy.dtype
     w_cs, rep = _client_view(w, K)
-    dx = torch.empty((K, N, Fi), dtype=BF16, device=dy.device)
+    dx = torch.empty((K, N, Fi), dtype=dy.dtype, device=dy.device)
     if gate is not None:
-        assert gate.shape == dx.shape and gate.dtype == BF16 and gate.is_contiguous()
+        assert gate.shape == dx.shape and gate.dtype == dy.dtype and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
-               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_variant, NULL, _p(gate), _s())
+               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, -1 if f32 else nt_variant, NULL, _p(gate), f32, _s())
     return dx
 
 
@@ -229,14 +245,17 @@ def linear_wgrad(dy, x, gw, gb=None):
     Fi = x.shape[-1]
     dy = dy.contiguous()
     x = x.contiguous()
+    f32 = _f32(dy)
+    assert x.dtype == dy.dtype
     assert gw.shape == (K, Fo, Fi) and gw[0].is_contiguous()
-    if _C.conv_tn_splitk(K, Fo, Fi, N, Fi, tn_variant) > 1:
+    tv = -1 if f32 else tn_variant
+    if _C.conv_tn_splitk(K, Fo, Fi, N, Fi, tv, f32) > 1:
         gw.zero_()
     _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K,
-               tn_variant, _s())
+               tv, f32, _s())
     if gb is not None:
         gb.zero_()
-        _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, _s())
+        _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, f32, _s())
 
 
 # ------------------------------------------------------------------------ batchnorm
@@ -256,8 +275,9 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
     mask = None
     if with_mask and relu and C % 8 == 0:
         mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
+    assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
-              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _s())
+              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s())
     if with_mask:
         return y, mean, rstd, mask
     return y, mean, rstd
@@ -273,8 +293,9 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     dg_cs = ggamma.stride(0) if ggamma is not None else 0
+    assert dy.dtype == x.dtype == gamma.dtype
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
-              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _s())
+              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s())
     return dx, dpre
 
 
@@ -288,7 +309,8 @@ def ln_fwd(x, gamma, beta, eps=1e-5):
     y = torch.empty_like(x)
     mean = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
     rstd = torch.empty_like(mean)
-    _C.ln_fwd(_p(x), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), g_cs, K, rpc, C, eps, rep, _s())
+    assert gamma.dtype == x.dtype
+    _C.ln_fwd(_p(x), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), g_cs, K, rpc, C, eps, rep, _f32(x), _s())
     return y, mean, rstd
 
 
@@ -302,7 +324,7 @@ def ln_bwd(dy, x, mean, rstd, gamma):
     dgamma = torch.zeros((K, C), dtype=torch.float32, device=x.device)
     dbeta = torch.zeros((K, C), dtype=torch.float32, device=x.device)
     _C.ln_bwd(_p(dy.contiguous()), _p(x), _p(mean), _p(rstd), _p(gamma), g_cs, K, rpc, C, _p(dx), _p(dgamma),
-              _p(dbeta), C, _s())
+              _p(dbeta), C, _f32(x), _s())
     return dx, dgamma, dbeta
 
 
@@ -312,9 +334,9 @@ def _pool_fwd(x, k, s, pad, mode):
     x = x.contiguous()
     OH = (H + 2 * pad - k) // s + 1
     OW = (W + 2 * pad - k) // s + 1
-    y = torch.empty((K, B, OH, OW, C), dtype=BF16, device=x.device)
+    y = torch.empty((K, B, OH, OW, C), dtype=x.dtype, device=x.device)
     idx = torch.empty((K, B, OH, OW, C), dtype=torch.int32, device=x.device) if mode == 0 else None
-    _C.pool_fwd(_p(x), _p(y), _p(idx), K, B, H, W, C, OH, OW, k, s, pad, mode, _s())
+    _C.pool_fwd(_p(x), _p(y), _p(idx), K, B, H, W, C, OH, OW, k, s, pad, mode, _f32(x), _s())
     return y, idx
 
 
@@ -325,8 +347,8 @@ def maxpool_fwd(x, k, s, pad=0):
 def maxpool_bwd(dy, idx, x_shape, k, s, pad=0):
     K, B, H, W, C = x_shape
     _, _, OH, OW, _ = dy.shape
-    dx = torch.empty(x_shape, dtype=BF16, device=dy.device)
-    _C.pool_bwd(_p(dy.contiguous()), _p(idx), _p(dx), K, B, H, W, C, OH, OW, k, s, pad, 0, _s())
+    dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    _C.pool_bwd(_p(dy.contiguous()), _p(idx), _p(dx), K, B, H, W, C, OH, OW, k, s, pad, 0, _f32(dy), _s())
     return dx
 
 
@@ -337,23 +359,23 @@ def avgpool_fwd(x, k, s):
 def avgpool_bwd(dy, x_shape, k, s):
     K, B, H, W, C = x_shape
     _, _, OH, OW, _ = dy.shape
-    dx = torch.empty(x_shape, dtype=BF16, device=dy.device)
-    _C.pool_bwd(_p(dy.contiguous()), NULL, _p(dx), K, B, H, W, C, OH, OW, k, s, 0, 1, _s())
+    dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    _C.pool_bwd(_p(dy.contiguous()), NULL, _p(dx), K, B, H, W, C, OH, OW, k, s, 0, 1, _f32(dy), _s())
     return dx
 
 
 def gap_fwd(x):
     K, B, H, W, C = x.shape
     x = x.contiguous()
-    y = torch.empty((K, B, C), dtype=BF16, device=x.device)
-    _C.gap_fwd(_p(x), _p(y), K * B, H * W, C, _s())
+    y = torch.empty((K, B, C), dtype=x.dtype, device=x.device)
+    _C.gap_fwd(_p(x), _p(y), K * B, H * W, C, _f32(x), _s())
     return y
 
 
 def gap_bwd(dy, x_shape):
     K, B, H, W, C = x_shape
-    dx = torch.empty(x_shape, dtype=BF16, device=dy.device)
-    _C.gap_bwd(_p(dy.contiguous()), _p(dx), K * B, H * W, C, _s())
+    dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device)
+    _C.gap_bwd(_p(dy.contiguous()), _p(dx), K * B, H * W, C, _f32(dy), _s())
     return dx
 
 
@@ -366,7 +388,7 @@ def ce_fwd_bwd(logits, labels, valid=None):
     loss = torch.empty(K, dtype=torch.float32, device=logits.device)
     correct = torch.empty(K, dtype=torch.float32, device=logits.device)
     dlogits = torch.empty_like(logits)
-    _C.ce_fwd_bwd(_p(logits), _p(lab), _p(v), _p(loss), _p(correct), _p(dlogits), K, B, NC, _s())
+    _C.ce_fwd_bwd(_p(logits), _p(lab), _p(v), _p(loss), _p(correct), _p(dlogits), K, B, NC, _f32(logits), _s())
     return loss, correct, dlogits
 
 
@@ -377,8 +399,8 @@ def embedding_fwd(tokens, table):
     t_cs, rep = _client_view(table, K)
     D = table.shape[-1]
     n_tok = tok.numel() // K
-    out = torch.empty((*tokens.shape, D), dtype=BF16, device=table.device)
-    _C.embedding_fwd(_p(tok), _p(table), _p(out), K, n_tok, D, t_cs, rep, _s())
+    out = torch.empty((*tokens.shape, D), dtype=table.dtype, device=table.device)
+    _C.embedding_fwd(_p(tok), _p(table), _p(out), K, n_tok, D, t_cs, rep, _f32(table), _s())
     return out
 
 
@@ -387,7 +409,7 @@ def embedding_bwd(dy, tokens, gtable):
     tok = tokens.to(torch.int32).contiguous()
     D = dy.shape[-1]
     gtable.zero_()
-    _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _s())
+    _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _f32(dy), _s())
 
 
 # ------------------------------------------------------------------------ attention
@@ -408,14 +430,15 @@ def attn_fwd(q, k, v, key_valid=None):
     """q,k,v [K,B,Hh,L,dh] bf16 → (o [K,B,Hh,L,dh] bf16, lse [K,B,Hh,L] fp32); flash-style
     kernel (csrc/attention.hip), never materialising the L×L scores."""
     q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
-    _check(q, BF16, name="q")
+    _check(q, q.dtype, name="q")
+    assert k.dtype == v.dtype == q.dtype
     KBH, H, L, DH = _attn_shape(q)
     if not _C.attn_supported(L, DH):
         raise NotImplementedError(f"attention kernel: unsupported L={L} dh={DH}")
     kv = _key_valid(key_valid, q)
     o = torch.empty_like(q)
     lse = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
-    _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _s())
+    _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _f32(q), _s())
     return o, lse
 
 
@@ -426,22 +449,22 @@ def attn_bwd(do, q, k, v, o, lse, key_valid=None):
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     delta = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
     _C.attn_bwd(_p(do), _p(q), _p(k), _p(v), _p(o), _p(lse.contiguous()), _p(kv), _p(dq), _p(dk), _p(dv), _p(delta),
-                KBH, H, L, DH, _s())
+                KBH, H, L, DH, _f32(q), _s())
     return dq, dk, dv
 
 
 # ----------------------------------------------------------------------------- SpMM
 def spmm(rowptr, col, val, x):
-    """CSR (shared graph, fp32 values) times per-client dense x [K,Nx,F] → [K,N,F] bf16."""
+    """CSR (shared graph, fp32 values) times per-client dense x [K,Nx,F] → [K,N,F] (x's dtype)."""
     x = x.contiguous()
-    _check(x, BF16, name="x")
+    f32 = _f32(x)
     K, Nx, F = x.shape
     N = rowptr.numel() - 1
-    y = torch.empty((K, N, F), dtype=BF16, device=x.device)
+    y = torch.empty((K, N, F), dtype=x.dtype, device=x.device)
     rp = rowptr.to(torch.int32).contiguous()
     cl = col.to(torch.int32).contiguous()
     vl = val.to(torch.float32).contiguous()
-    _C.spmm(_p(rp), _p(cl), _p(vl), _p(x), _p(y), K, N, Nx, F, Nx * F, N * F, _s())
+    _C.spmm(_p(rp), _p(cl), _p(vl), _p(x), _p(y), K, N, Nx, F, Nx * F, N * F, f32, _s())
     return y
 
 
@@ -494,17 +517,22 @@ def weighted_sum(x, w):
 
 
 def mix_rows(x, w, out_dtype=BF16):
-    """[M, P] = W[M, K] · x[K, P]: subset models for Shapley utilities, emitted in bf16 (the
-    eval compute dtype) by one native pass that reads each x row once per 32 models."""
+    """[M, P] = W[M, K] · x[K, P]: subset models for Shapley utilities, emitted in the eval
+    compute dtype (bf16 or fp32) by one native pass that reads each x row once per 32 models;
+    K > 256 is split into 256-row chunks (fp32 partial sums, one rounding at the end)."""
     K, P, ld = _row_args(x)
     M = w.shape[0]
-    assert w.shape == (M, K)
-    if out_dtype != BF16 or K > 256:
-        return (w.float().to(x.device) @ x).to(out_dtype)  # plain library GEMM
+    assert w.shape == (M, K) and out_dtype in _DTYPES
     w = w.float().to(x.device).contiguous()
-    out = torch.empty((M, P), dtype=BF16, device=x.device)
+    if K > 256:
+        acc = None
+        for k0 in range(0, K, 256):
+            part = mix_rows(x[k0:k0 + 256], w[:, k0:k0 + 256].contiguous(), F32)
+            acc = part if acc is None else acc.add_(part)
+        return acc.to(out_dtype)
+    out = torch.empty((M, P), dtype=out_dtype, device=x.device)
     if M:
-        _C.mix_rows(_p(x), _p(w), _p(out), K, M, P, ld, P, _s())
+        _C.mix_rows(_p(x), _p(w), _p(out), K, M, P, ld, P, int(out_dtype == F32), _s())
     return out
 
 
@@ -594,10 +622,10 @@ def sign_vote(packed, P, active=None):
 
 
 def gather_rows(src, idx):
-    """src [N, ...] bf16 contiguous, idx int -> [len(idx), ...]"""
-    row = src[0].numel()
-    assert row % 8 == 0 and src.is_contiguous()
+    """src [N, ...] contiguous (rows a multiple of 16 B), idx int -> [len(idx), ...]"""
+    row_bytes = src[0].numel() * src.element_size()
+    assert row_bytes % 16 == 0 and src.is_contiguous()
     i32 = idx.reshape(-1).to(torch.int32).contiguous()
     out = torch.empty((i32.numel(), *src.shape[1:]), dtype=src.dtype, device=src.device)
-    _C.gather_rows(_p(src), _p(i32), _p(out), i32.numel(), row, _s())
+    _C.gather_rows(_p(src), _p(i32), _p(out), i32.numel(), row_bytes, _s())
     return out

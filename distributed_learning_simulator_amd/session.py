@@ -38,9 +38,15 @@ from .utils.logging import get_logger
 
 
 def resolve_dtype(config, device) -> torch.dtype:
+    """Compute dtype of activations and of the parameter views the kernels read.
+
+    `auto` follows the reference's own switch: `use_amp: false` (its default,
+    `conf/global.yaml:7`) trains in fp32 — on the GPU the GEMMs then run as split-bf16 MFMA
+    with fp32 storage and accumulation (csrc/conv_f32.hip) — and `use_amp: true` selects the
+    bf16 fast mode. An explicit `compute_dtype` (bf16 / fp32) overrides both."""
     name = (config.compute_dtype or "auto").lower()
     if name == "auto":
-        return torch.bfloat16 if device.type == "cuda" else torch.float32
+        return torch.bfloat16 if (device.type == "cuda" and config.use_amp) else torch.float32
     return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
             "float32": torch.float32}[name]
 

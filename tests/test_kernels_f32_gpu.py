@@ -1,0 +1,232 @@
+"""Reference-precision (fp32) kernels vs a float64 CPU oracle at <= 1e-5 relative error.
+
+The reference trains in fp32 (`/root/reference/conf/global.yaml:7` `use_amp: false`). On gfx950
+the GEMMs of this mode run as split-bf16 ("bf16x3") MFMA with fp32 storage and accumulation
+(csrc/conv_f32.hip); every other kernel computes in fp32 on fp32 storage. Error metric: max
+|out - exact| over max |exact| (the scale of the output), as in tests/test_kernels_gpu.py.
+"""
+
+import pytest
+import torch
+
+from distributed_learning_simulator_amd.ops import ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOL = 1e-5
+
+
+def _f(*shape, scale=1.0):
+    return torch.randn(*shape, device=DEV) * scale
+
+
+def _d(t):
+    return t.detach().cpu().double()
+
+
+def _close(out, exp, tol=TOL):
+    out = out.detach().cpu().double()
+    exp = exp.detach().cpu().double()
+    assert out.shape == exp.shape, (out.shape, exp.shape)
+    err = (out - exp).abs().max().item()
+    mag = exp.abs().max().item() + 1e-12
+    assert err <= tol * mag, f"rel err {err / mag:.3g} > {tol}"
+
+
+CONV_CASES = [
+    # K, B, H, W, Ci, Co, k, stride, pad
+    (3, 4, 8, 8, 16, 32, 3, 1, 1),
+    (2, 2, 8, 8, 64, 64, 3, 1, 1),
+    (2, 3, 9, 9, 64, 128, 3, 2, 1),
+    (2, 2, 8, 8, 64, 128, 1, 2, 0),
+    (3, 2, 8, 8, 3, 64, 3, 1, 1),       # stem: Ci=3 scalar path
+    (2, 2, 8, 8, 8, 64, 3, 1, 1),       # stem with RGB zero-padded to 8 channels
+    (2, 2, 6, 6, 36, 12, 3, 1, 1),      # DenseNet-like: Ci%8==4, Co=12
+    (2, 2, 12, 12, 1, 6, 5, 1, 2),      # LeNet conv1
+    (2, 2, 7, 7, 128, 256, 3, 1, 1),
+    (2, 2, 9, 7, 16, 32, 3, 3, 1),      # stride 3, non-square: 9 parity classes
+    (2, 8, 16, 16, 64, 64, 3, 1, 1),    # long pixel reduction (split-K wgrad)
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_f32(hip, case):
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(0)
+    x = _f(K, B, H, W, Ci)
+    w = _f(K, Co, k, k, Ci, scale=0.2)
+    y = hip.conv_fwd(x, w, s, p)
+    assert y.dtype == torch.float32
+    _close(y, ref.conv_fwd(_d(x), _d(w), s, p))
+    dy = _f(*y.shape)
+    dx = hip.conv_dgrad(dy, w, (H, W), s, p)
+    _close(dx, ref.conv_dgrad(_d(dy), _d(w), (H, W), s, p))
+    P = Co * k * k * Ci + 16
+    gbuf = torch.full((K, P), 7.0, device=DEV)
+    gw = gbuf[:, 8 : 8 + Co * k * k * Ci].unflatten(1, (Co, k, k, Ci))
+    hip.conv_wgrad(dy, x, gw, s, p)
+    _close(gw, ref.conv_wgrad(_d(dy), _d(x), (K, Co, k, k, Ci), s, p))
+    assert torch.all(gbuf[:, :8] == 7.0) and torch.all(gbuf[:, 8 + Co * k * k * Ci :] == 7.0)
+
+
+@pytest.mark.parametrize("case", [(2, 2, 9, 9, 64, 128, 3, 2, 1), (2, 3, 8, 8, 128, 64, 3, 1, 1),
+                                  (2, 2, 6, 6, 24, 40, 3, 1, 1)])
+def test_conv_f32_every_variant(hip, case):
+    """Every fp32 NT and TN tile configuration (the driver's fp32 `--variant` sweep ids)."""
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(3)
+    x = _f(K, B, H, W, Ci)
+    w = _f(K, Co, k, k, Ci, scale=0.2)
+    OH = (H + 2 * p - k) // s + 1
+    dy = _f(K, B, OH, (W + 2 * p - k) // s + 1, Co)
+    y_ref = ref.conv_fwd(_d(x), _d(w), s, p)
+    dx_ref = ref.conv_dgrad(_d(dy), _d(w), (H, W), s, p)
+    dw_ref = ref.conv_wgrad(_d(dy), _d(x), (K, Co, k, k, Ci), s, p)
+    stream = torch.cuda.current_stream().cuda_stream
+    M = B * OH * ((W + 2 * p - k) // s + 1)
+    for v in range(hip._C.conv_nt_f32_num_variants()):
+        y = torch.empty_like(dy)
+        hip._C.conv_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, B * H * W * Ci, M * Co, w.stride(0), 0, B, H, W,
+                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream)
+        _close(y, y_ref)
+        dx = torch.empty_like(x)
+        hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
+                          W, Ci, k, k, s, p, v, 1, stream)
+        _close(dx, dx_ref)
+    for v in range(hip._C.conv_tn_f32_num_variants()):
+        gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
+        hip._C.conv_tn(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M * Co, B * H * W * Ci, gw.stride(0), B, H, W, Ci,
+                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream)
+        _close(gw, dw_ref)
+
+
+@pytest.mark.parametrize("N,Fi,Fo", [(64, 512, 10), (33, 100, 300), (128, 784, 200), (5, 84, 10), (96, 512, 2048)])
+def test_linear_f32(hip, N, Fi, Fo):
+    K = 3
+    torch.manual_seed(1)
+    x = _f(K, N, Fi)
+    w = _f(K, Fo, Fi, scale=0.1)
+    b = _f(K, Fo)
+    _close(hip.linear_fwd(x, w, b), ref.linear_fwd(_d(x), _d(w), _d(b)))
+    res = _f(K, N, Fo)
+    _close(hip.linear_fwd(x, w, b, acc=res), ref.linear_fwd(_d(x), _d(w), _d(b), acc=_d(res)))
+    _close(hip.linear_fwd(x, w, b, relu=True), ref.linear_fwd(_d(x), _d(w), _d(b), relu=True))
+    dy = _f(K, N, Fo)
+    _close(hip.linear_dgrad(dy, w), ref.linear_dgrad(_d(dy), _d(w)))
+    gate = torch.relu(_f(K, N, Fi))
+    _close(hip.linear_dgrad(dy, w, gate=gate), ref.linear_dgrad(_d(dy), _d(w), gate=_d(gate)))
+    gw = torch.empty((K, Fo, Fi), device=DEV)
+    gb = torch.empty((K, Fo), device=DEV)
+    hip.linear_wgrad(dy, x, gw, gb)
+    dw_ref, db_ref = ref.linear_wgrad(_d(dy), _d(x), True)
+    _close(gw, dw_ref)
+    _close(gb, db_ref)
+
+
+def test_conv_f32_dgrad_accumulate_and_bias(hip):
+    K, B, H, W, Ci, Co = 2, 3, 8, 8, 64, 64
+    w = _f(K, Co, 3, 3, Ci, scale=0.2)
+    dy = _f(K, B, H, W, Co)
+    acc = _f(K, B, H, W, Ci)
+    _close(hip.conv_dgrad(dy, w, (H, W), 1, 1, acc=acc), ref.conv_dgrad(_d(dy), _d(w), (H, W), 1, 1, acc=_d(acc)))
+    x = _f(K, B, H, W, Ci)
+    b = _f(K, Co)
+    _close(hip.conv_fwd(x, w, 1, 1, bias=b), ref.conv_fwd(_d(x), _d(w), 1, 1, bias=_d(b)))
+    gb = torch.empty((K, Co), device=DEV)
+    hip.bias_grad(dy, gb)
+    _close(gb, _d(dy).sum(dim=(1, 2, 3)))
+
+
+@pytest.mark.parametrize("C", [64, 12, 3])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
+def test_batchnorm_f32(hip, C, relu, res):
+    K, R = 3, 300
+    torch.manual_seed(2)
+    x = _f(K, R, C, scale=2.0) + 0.5
+    g = _f(K, C) + 1
+    b = _f(K, C)
+    valid = torch.tensor([300, 150, 7], dtype=torch.int32, device=DEV)
+    r = _f(K, R, C) if res else None
+    y, mean, rstd = hip.bn_fwd(x, g, b, valid, relu, r)
+    y2, mean2, rstd2 = ref.bn_fwd(_d(x), _d(g), _d(b), valid.cpu(), relu, _d(r) if res else None)
+    _close(mean, mean2, 1e-5)
+    _close(rstd, rstd2, 1e-5)
+    _close(y, y2)
+    dy = _f(K, R, C)
+    gg = torch.zeros((K, C), device=DEV)
+    gbeta = torch.zeros((K, C), device=DEV)
+    dx, dpre = hip.bn_bwd(dy, x, y, mean, rstd, g, valid, relu, gg, gbeta, res)
+    dx2, dg2, db2, dpre2 = ref.bn_bwd(_d(dy), _d(x), y2, mean2, rstd2, _d(g), valid.cpu(), relu)
+    _close(dx, dx2, 2e-5)
+    _close(gg, dg2)
+    _close(gbeta, db2)
+    if res:
+        _close(dpre, dpre2)
+
+
+def test_layernorm_f32(hip):
+    K, N, C = 2, 37, 100
+    x, g, b = _f(K, N, C), _f(K, C) + 1, _f(K, C)
+    y, mean, rstd = hip.ln_fwd(x, g, b)
+    y2, m2, r2 = ref.ln_fwd(_d(x), _d(g), _d(b))
+    _close(y, y2)
+    dy = _f(K, N, C)
+    dx, dg, db = hip.ln_bwd(dy, x, mean, rstd, g)
+    dx2, dg2, db2 = ref.ln_bwd(_d(dy), _d(x), m2, r2, _d(g))
+    _close(dx, dx2, 2e-5)
+    _close(dg, dg2)
+    _close(db, db2)
+
+
+def test_pool_gap_ce_f32(hip):
+    x = _f(2, 3, 9, 9, 16)
+    y, idx = hip.maxpool_fwd(x, 3, 2, 1)
+    y2, idx2 = ref.maxpool_fwd(_d(x), 3, 2, 1)
+    _close(y, y2)
+    dy = _f(*y.shape)
+    _close(hip.maxpool_bwd(dy, idx, x.shape, 3, 2, 1), ref.maxpool_bwd(_d(dy), idx2, x.shape, 3, 2, 1))
+    x = _f(2, 3, 8, 8, 24)
+    _close(hip.avgpool_fwd(x, 2, 2), ref.avgpool_fwd(_d(x), 2, 2))
+    dy = _f(2, 3, 4, 4, 24)
+    _close(hip.avgpool_bwd(dy, x.shape, 2, 2), ref.avgpool_bwd(_d(dy), x.shape, 2, 2))
+    _close(hip.gap_fwd(x), _d(x).mean(dim=(2, 3)))
+    K, B, NC = 3, 64, 100
+    logits = _f(K, B, NC, scale=3)
+    labels = torch.randint(0, NC, (K, B), device=DEV)
+    valid = torch.tensor([64, 30, 1], dtype=torch.int32, device=DEV)
+    l, c, d = hip.ce_fwd_bwd(logits, labels, valid)
+    l2, c2, d2 = ref.ce_fwd_bwd(_d(logits), labels.cpu(), valid.cpu())
+    _close(l, l2)
+    assert torch.equal(c.cpu(), c2.float())
+    _close(d, d2)
+
+
+@pytest.mark.parametrize("L,dh", [(300, 20), (128, 64)])
+def test_attention_embedding_f32(hip, L, dh):
+    K, B, H = 2, 2, 2
+    q, k, v = (_f(K, B, H, L, dh) for _ in range(3))
+    kv = torch.randint(1, L + 1, (K, B), device=DEV, dtype=torch.int32)
+    o, lse = hip.attn_fwd(q, k, v, kv)
+    o2, lse2 = ref.attn_fwd(_d(q), _d(k), _d(v), kv.cpu())
+    _close(o, o2, 3e-5)
+    do = _f(K, B, H, L, dh)
+    dq, dk, dv = hip.attn_bwd(do, q, k, v, o, lse, kv)
+    rq, rk, rv = ref.attn_bwd(_d(do), _d(q), _d(k), _d(v), o2, lse2, kv.cpu())
+    _close(dq, rq, 3e-5)
+    _close(dk, rk, 3e-5)
+    _close(dv, rv, 3e-5)
+    table = _f(K, 50, 16)
+    tok = torch.randint(0, 50, (K, 3, 7), device=DEV)
+    assert torch.equal(hip.embedding_fwd(tok, table), ref.embedding_fwd(tok, table))
+
+
+def test_mix_rows_f32_and_gather(hip):
+    K, M, P = 300, 40, 4096 + 48  # K > 256: chunked native passes
+    x = torch.randn(K, P, device=DEV)
+    w = torch.rand(M, K, device=DEV)
+    out = hip.mix_rows(x, w, torch.float32)
+    assert out.dtype == torch.float32
+    _close(out, _d(w) @ _d(x))
+    src = _f(100, 4, 4, 4)
+    idx = torch.randint(0, 100, (3, 5), device=DEV)
+    assert torch.equal(hip.gather_rows(src, idx), src[idx.reshape(-1)])
