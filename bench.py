@@ -38,7 +38,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="fedavg_resnet18",
-                    choices=["fedavg_resnet18", "fedobd_transformer", "signsgd_resnet50", "gtg_resnet18"])
+                    choices=["fedavg_resnet18", "fedobd_transformer", "signsgd_resnet50", "gtg_resnet18",
+                             "fedavg_mlp_mnist"])
     ap.add_argument("--algo", default="fed_avg", choices=["fed_avg", "fed_obd"])
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--clients", type=int, default=100)
@@ -56,6 +57,11 @@ def main() -> None:
     if args.emulate_world and args.workload != "fedavg_resnet18":
         ap.error("--emulate-world supports the fedavg_resnet18 workload only")
 
+    from distributed_learning_simulator_amd.parallel import launch
+
+    if args.gpus > 1 and not launch.under_launcher():
+        # one rank per GPU, spawned before anything touches the GPU; rank 0 prints the line
+        sys.exit(launch.spawn_ranks(args.gpus))
     if args.backend == "torch":
         os.environ["DLS_BACKEND"] = "torch"
     os.environ.setdefault("DLS_LOG_LEVEL", "WARNING")
@@ -159,6 +165,13 @@ def workload_config(args, rounds: int) -> dict:
         name = sess.dc.spec.name
         return sum(p.dataset_size(name) for p in sess.practitioners.values()) * sess.config.epoch
 
+    if args.workload == "fedavg_mlp_mnist":
+        # BASELINE.json config 1: the plumbing check (runs on the CPU executor as well)
+        cfg = {"distributed_algorithm": "fed_avg", "dataset_name": "MNIST", "model_name": "MLP", "worker_number": 4,
+               "epoch": 1, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.01,
+               "dataset_sampling": "iid"}
+        return {"config": {**cfg, **common}, "metric": "FL rounds/sec (FedAvg, 4 clients, MLP, MNIST-shaped)",
+                "data": "synthetic (MNIST-shaped, iid shards, random-init weights)", "samples_per_round": shard_samples}
     if args.workload == "fedavg_resnet18":
         algo_kwargs, endpoint_kwargs = {}, {}
         if args.algo == "fed_obd":

@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="time every conv_nt tile variant")
     ap.add_argument("--skip-misc", action="store_true", help="conv layers only (no BN/SGD)")
     ap.add_argument("--gl", action="store_true", help="A/B the LDS-DMA large-tile kernel (conv_gl) vs conv_nt")
+    ap.add_argument("--f32", action="store_true", help="fp32 tensors: the split-bf16 kernels (csrc/conv_f32.hip)")
     args = ap.parse_args()
     from distributed_learning_simulator_amd.ops import build
 
@@ -63,15 +64,19 @@ def main():
 
     K, B = args.K, args.B
     dev = "cuda"
+    dt = torch.float32 if args.f32 else torch.bfloat16
+    nt_attr, tn_attr = ("nt_f32_variant", "tn_f32_variant") if args.f32 else ("nt_variant", "tn_variant")
+    n_nt = hip._C.conv_nt_f32_num_variants() if args.f32 else hip._C.conv_nt_num_variants()
+    n_tn = hip._C.conv_tn_f32_num_variants() if args.f32 else hip._C.conv_tn_num_variants()
     rows = []
     for name, H, Ci, Co, k, s in RESNET18_CIFAR:
         if args.only and name not in args.only.split(","):
             continue
         pad = k // 2
         OH = (H + 2 * pad - k) // s + 1
-        x = torch.randn(K, B, H, H, Ci, device=dev).to(torch.bfloat16)
-        w = (torch.randn(K, Co, k, k, Ci, device=dev) * 0.05).to(torch.bfloat16)
-        dy = torch.randn(K, B, OH, OH, Co, device=dev).to(torch.bfloat16)
+        x = torch.randn(K, B, H, H, Ci, device=dev).to(dt)
+        w = (torch.randn(K, Co, k, k, Ci, device=dev) * 0.05).to(dt)
+        dy = torch.randn(K, B, OH, OH, Co, device=dev).to(dt)
         gw = torch.empty(K, Co, k, k, Ci, device=dev)
         flops = 2.0 * K * B * OH * OH * Co * Ci * k * k
         t_f = timeit(lambda: hip.conv_fwd(x, w, s, pad), args.iters)
@@ -97,19 +102,19 @@ def main():
         if args.sweep:
             # every NT tile configuration on this shape (fwd / dgrad TFLOP/s per variant id)
             sw = {}
-            for v in range(hip._C.conv_nt_num_variants()):
-                hip.nt_variant = v
+            for v in range(n_nt):
+                setattr(hip, nt_attr, v)
                 tf_v = timeit(lambda: hip.conv_fwd(x, w, s, pad), args.iters)
                 td_v = timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad), args.iters)
                 sw[v] = (round(flops / tf_v / 1e12, 1), round(flops / td_v / 1e12, 1))
-            hip.nt_variant = -1
+            setattr(hip, nt_attr, -1)
             row["sweep_fwd_dgrad"] = sw
             swt = {}
-            for v in range(hip._C.conv_tn_num_variants()):
-                hip.tn_variant = v
+            for v in range(n_tn):
+                setattr(hip, tn_attr, v)
                 tw_v = timeit(lambda: hip.conv_wgrad(dy, x, gw, s, pad), args.iters)
                 swt[v] = round(flops / tw_v / 1e12, 1)
-            hip.tn_variant = -1
+            setattr(hip, tn_attr, -1)
             row["sweep_wgrad"] = swt
         if args.torch:
             tf = timeit(lambda: ref.conv_fwd(x, w, s, pad), max(2, args.iters // 4))
@@ -123,17 +128,17 @@ def main():
         return
     # BN + SGD
     R, C = B * 32 * 32, 64
-    x = torch.randn(K, R, C, device=dev).to(torch.bfloat16)
-    g = torch.ones(K, C, device=dev).to(torch.bfloat16)
-    bb = torch.zeros(K, C, device=dev).to(torch.bfloat16)
+    x = torch.randn(K, R, C, device=dev).to(dt)
+    g = torch.ones(K, C, device=dev).to(dt)
+    bb = torch.zeros(K, C, device=dev).to(dt)
     valid = torch.full((K,), R, dtype=torch.int32, device=dev)
     t = timeit(lambda: hip.bn_fwd(x, g, bb, valid, True, x), args.iters)
-    nbytes = x.numel() * 2 * 4  # stats read + apply read x,res + write
+    nbytes = x.numel() * x.element_size() * 4  # stats read + apply read x,res + write
     print(json.dumps({"kernel": "bn_fwd_relu_res", "rows": R, "C": C, "ms": t * 1e3, "TB/s": nbytes / t / 1e12}))
     y, mean, rstd = hip.bn_fwd(x, g, bb, valid, True, None)
     gg = torch.zeros(K, C, device=dev)
     t = timeit(lambda: hip.bn_bwd(x, x, y, mean, rstd, g, valid, True, gg, gg, True), args.iters)
-    nbytes = x.numel() * 2 * 7
+    nbytes = x.numel() * x.element_size() * 7
     print(json.dumps({"kernel": "bn_bwd_relu", "ms": t * 1e3, "TB/s": nbytes / t / 1e12}))
     del x, y
     P = 11173968

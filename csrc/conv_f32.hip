@@ -574,17 +574,21 @@ bool launch_tn_f32_variant(int v, const ConvTNParams& p, int va, int vb, int gri
   }
 }
 
+// measured (kernel_bench --f32 --sweep, K = 100): Co = 64 layers want the 64x128 double-buffered
+// tile (l1 165 TFLOP/s), the rest the single-buffer 128x128 (l2 248, l3 277, l4a 260), the
+// 256x128 tile only at Co >= 512 with enough tiles (l4 286 vs 273)
 int tn_f32_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
   if (Co <= 32 || R <= 64) return 5;
   if (Co <= 64) return 1;
-  if (Co >= 256 && tiles(256, 128) >= 1024) return 3;
-  return 0;
+  if (Co >= 512 && tiles(256, 128) >= 1024) return 3;
+  return 2;
 }
 
 int resolve_tn_f32_variant(int variant, int K, int Co, int R, int va, int vb) {
   if (variant < 0 || variant >= kTnF32Variants) variant = tn_f32_default_variant(K, Co, R);
   if ((va != 8 || vb != 8) && !(variant == 0 || variant == 1 || variant == 5)) variant = Co <= 64 ? 1 : 0;
+  // (the all-widths tiles are the double-buffered 0 / 1 / 5)
   return variant;
 }
 
@@ -611,10 +615,11 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
   const int va = vw(p.C);
   int vb = bkm ? vw(p.N) : vw(p.R);
   if (variant < 0) {
-    if (p.N <= 64)
-      variant = bkm ? 6 : 4;
-    else
-      variant = 0;
+    // measured (bench/kernel_bench.py --f32 --sweep, ResNet-18 layers, K = 100): the single-buffer
+    // tiles win everywhere — 40-60 KB of LDS keeps 3 workgroups per CU, whose waves hide each
+    // other's split (VALU) and global-load phases: 128x128 fwd/dgrad 275-299 TFLOP/s on l2-l4
+    // (80 KB double-buffered v0: 262-276), 256x64 for N <= 64 (l1 fwd 211 vs 184, dgrad 209 vs 181)
+    variant = p.N <= 64 ? 6 : 1;
   }
   // variants without the requested vector widths fall back to the all-widths 64x64 tile
   const bool v88 = va == 8 && vb == 8;

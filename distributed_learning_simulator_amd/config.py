@@ -94,7 +94,9 @@ class DistributedTrainingConfig:
             else:
                 self.extra[k] = copy.deepcopy(v)
         self._normalise()
-        date_time = f"{datetime.datetime.now():%Y-%m-%d_%H_%M_%S}"
+        # ranks spawned by parallel/launch.py share the parent's run id (one save_dir per run)
+        run_id = os.environ.get("DLS_RUN_ID")
+        date_time = os.environ.get("DLS_RUN_TIME") or f"{datetime.datetime.now():%Y-%m-%d_%H_%M_%S}"
         dataset_name = self.dataset_kwargs.get("name", self.dataset_name)
         sampling = (
             self.dataset_sampling
@@ -106,7 +108,7 @@ class DistributedTrainingConfig:
             f"{dataset_name}_{sampling}",
             self.model_name,
             date_time,
-            str(uuid.uuid4()),
+            run_id or str(uuid.uuid4()),
         )
         if self.exp_name:
             dir_suffix = os.path.join(self.exp_name, dir_suffix)

@@ -111,6 +111,8 @@ def _bn_counters(K: int, device):
 # microbenchmark (bench/kernel_bench.py) sets explicit variant ids to sweep them.
 nt_variant = -1
 tn_variant = -1  # weight-gradient (TN) tile configuration, same convention
+nt_f32_variant = -1  # the same for the fp32 (split-bf16) kernels of csrc/conv_f32.hip
+tn_f32_variant = -1
 # large-tile LDS-DMA kernel (csrc/conv_gl.hip) for fwd / dgrad: -1 = shape heuristic (or env
 # DLS_CONV_GL), 0 = never, 1 = whenever the shape is supported (tests, A/B benchmarks)
 gl_mode = -1
@@ -143,7 +145,7 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
-               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, -1 if f32 else nt_variant, NULL, NULL, f32, _s())
+               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32, _s())
     return y
 
 
@@ -172,7 +174,7 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
     _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
-                  -1 if f32 else nt_variant, f32, _s())
+                  nt_f32_variant if f32 else nt_variant, f32, _s())
     return dx
 
 
@@ -188,7 +190,7 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int):
     assert Co2 == Co and Ci == C
     M = B * OH * OW
     R = KH * KW * C
-    tv = -1 if f32 else tn_variant
+    tv = tn_f32_variant if f32 else tn_variant
     if _C.conv_tn_splitk(K, Co, R, M, C, tv, f32) > 1:
         gw.zero_()
     _C.conv_tn(_p(dy), _p(x), _p(gw), M * Co, B * H * W * C, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M,
@@ -218,7 +220,7 @@ def linear_fwd(x, w, b=None, relu=False, acc=None):
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               int(relu), K, 0, -1 if f32 else nt_variant, _p(acc), NULL, f32, _s())
+               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s())
     return y
 
 
@@ -236,7 +238,7 @@ def linear_dgrad(dy, w, gate=None):
         assert gate.shape == dx.shape and gate.dtype == dy.dtype and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
-               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, -1 if f32 else nt_variant, NULL, _p(gate), f32, _s())
+               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s())
     return dx
 
 
@@ -248,7 +250,7 @@ def linear_wgrad(dy, x, gw, gb=None):
     f32 = _f32(dy)
     assert x.dtype == dy.dtype
     assert gw.shape == (K, Fo, Fi) and gw[0].is_contiguous()
-    tv = -1 if f32 else tn_variant
+    tv = tn_f32_variant if f32 else tn_variant
     if _C.conv_tn_splitk(K, Fo, Fi, N, Fi, tv, f32) > 1:
         gw.zero_()
     _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K,

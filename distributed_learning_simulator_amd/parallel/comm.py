@@ -154,7 +154,10 @@ def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> Comm:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # "nccl" is RCCL on ROCm (xGMI). DLS_DIST_BACKEND=gloo rehearses the multi-rank GPU
         # path with ranks sharing one GPU (RCCL needs one GPU per rank).
-        backend = os.environ.get("DLS_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        # More ranks than GPUs (e.g. parallel_number > visible GPUs) cannot use RCCL, which
+        # needs one GPU per rank: those jobs fall back to gloo.
+        n_dev = torch.cuda.device_count() if use_gpu else 0
+        backend = os.environ.get("DLS_DIST_BACKEND") or ("nccl" if use_gpu and world <= n_dev else "gloo")
         kwargs = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if use_gpu and backend == "nccl":

@@ -1,0 +1,56 @@
+#!/bin/bash
+# GPU-box driver for this repo (run through gpurun). Every GPU step has its own time limit and
+# the script stops at the first failing step (no retries).
+#
+#   scripts/gpu.sh tests              pytest -m gpu (every kernel vs its oracle, GPU sessions)
+#   scripts/gpu.sh bench [ARGS...]    bench.py ARGS  -> gpurun_out/bench.json
+#   scripts/gpu.sh prof  [ARGS...]    rocprofv3 --kernel-trace --stats of bench.py ARGS
+#   scripts/gpu.sh pmc   COUNTERS [ARGS...]   one rocprofv3 --pmc pass (counter limits: see guide)
+#   scripts/gpu.sh kbench [ARGS...]   bench/kernel_bench.py ARGS
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+mode=$1
+shift
+case "$mode" in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread "$@" \
+      > gpurun_out/gpu_tests.log 2>&1
+    rc=$?
+    tail -15 gpurun_out/gpu_tests.log
+    exit $rc
+    ;;
+  bench)
+    timeout -k 10 1000 python -u bench.py "$@" > gpurun_out/bench.log 2>&1
+    rc=$?
+    grep '^{' gpurun_out/bench.log | tail -1 | tee gpurun_out/bench.json
+    [ $rc -ne 0 ] && tail -20 gpurun_out/bench.log
+    exit $rc
+    ;;
+  prof)
+    timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+      python -u bench.py "$@" > gpurun_out/prof_bench.log 2>&1
+    rc=$?
+    grep '^{' gpurun_out/prof_bench.log | tail -1
+    find gpurun_out/prof -name '*kernel_stats.csv' | head -1 | xargs -r head -25
+    exit $rc
+    ;;
+  pmc)
+    counters=$1
+    shift
+    timeout -s KILL 300 rocprofv3 --pmc $counters --output-format csv -d gpurun_out/pmc -o run -- \
+      python -u bench.py "$@" > gpurun_out/pmc_bench.log 2>&1
+    exit $?
+    ;;
+  kbench)
+    timeout -k 10 900 python -u bench/kernel_bench.py "$@" > gpurun_out/kbench.log 2>&1
+    rc=$?
+    tail -40 gpurun_out/kbench.log
+    exit $rc
+    ;;
+  *)
+    echo "usage: $0 tests|bench|prof|pmc|kbench ..." >&2
+    exit 2
+    ;;
+esac
