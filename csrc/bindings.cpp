@@ -142,14 +142,14 @@ PYBIND11_MODULE(_dls_hip, m) {
     delta_rows(P<const float>(theta), P<const float>(base), P<float>(out), K, Pn, ld, S(s));
   });
   m.def("weighted_sum", [](ptr x, ptr w, ptr out, int K, long Pn, long ld, ptr s) {
-    weighted_sum(P<const float>(x), P<const float>(w), P<float>(out), K, Pn, ld, S(s));
+    weighted_sum(P<const float>(x), P<const double>(w), P<double>(out), K, Pn, ld, S(s));
   });
   m.def("mix_rows", [](ptr x, ptr w, ptr out, int K, int M, long Pn, long ld, long ld_out, int f32, ptr s) {
     mix_rows(P<const float>(x), P<const float>(w), P<void>(out), K, M, Pn, ld, ld_out, f32, S(s));
   });
   m.def("masked_weighted_sum", [](ptr x, ptr mask, ptr w, ptr num, ptr den, int K, long Pn, long ld, ptr s) {
-    masked_weighted_sum(P<const float>(x), P<const uint8_t>(mask), P<const float>(w), P<float>(num), P<float>(den), K, Pn,
-                        ld, S(s));
+    masked_weighted_sum(P<const float>(x), P<const uint8_t>(mask), P<const double>(w), P<double>(num), P<double>(den), K,
+                        Pn, ld, S(s));
   });
   m.def("dropout_mask", [](ptr mask, int K, long Pn, float p, ptr seeds, ptr s) {
     dropout_mask(P<uint8_t>(mask), K, Pn, p, P<const uint32_t>(seeds), S(s));

@@ -154,11 +154,12 @@ void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shad
                float wd, hipStream_t s);
 void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s);
 void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s);
-void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s);
+// out += Σ_k w_k x[k] / num += Σ w m x, den += Σ w m: fp64 accumulators (in place)
+void weighted_sum(const float* x, const double* w, double* out, int K, long P, long ld, hipStream_t s);
 void mix_rows(const float* x, const float* w, void* out, int K, int M, long P, long ld, long ld_out, int f32,
               hipStream_t s);
-void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
-                         long ld, hipStream_t s);
+void masked_weighted_sum(const float* x, const uint8_t* mask, const double* w, double* num, double* den, int K,
+                         long P, long ld, hipStream_t s);
 void dropout_mask(uint8_t* mask, int K, long P, float p, const uint32_t* seeds, hipStream_t s);
 void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
                     hipStream_t s);

@@ -312,20 +312,21 @@ __global__ void delta_kernel(const float* __restrict__ theta, const float* __res
   }
 }
 
-// Σ_k w_k x[k, :] with fp64 accumulation (reference FedAvg accumulates in float64)
-__global__ void __launch_bounds__(256) weighted_sum_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                           float* __restrict__ out, int K, long P4, long ld) {
+// out[:] += Σ_k w_k x[k, :] in fp64 (reference FedAvg accumulates float64(θ)·n, fed_avg_algorithm.py:
+// 39-52): the fp64 accumulator stays fp64 across cohorts and the RCCL all-reduce; fixed k order
+__global__ void __launch_bounds__(256) weighted_sum_kernel(const float* __restrict__ x, const double* __restrict__ w,
+                                                           double* __restrict__ out, int K, long P4, long ld) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
-    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    double4 a = reinterpret_cast<double4*>(out)[i];
     for (int k = 0; k < K; ++k) {
       const float4 v = reinterpret_cast<const float4*>(x + (long)k * ld)[i];
       const double wk = w[k];
-      a0 += wk * v.x;
-      a1 += wk * v.y;
-      a2 += wk * v.z;
-      a3 += wk * v.w;
+      a.x += wk * v.x;
+      a.y += wk * v.y;
+      a.z += wk * v.z;
+      a.w += wk * v.w;
     }
-    reinterpret_cast<float4*>(out)[i] = make_float4((float)a0, (float)a1, (float)a2, (float)a3);
+    reinterpret_cast<double4*>(out)[i] = a;
   }
 }
 
@@ -366,19 +367,20 @@ __global__ void __launch_bounds__(256) mix_rows_kernel(const float* __restrict__
   }
 }
 
+// FedDropoutAvg: num[:] += Σ_k w_k m_k x_k, den[:] += Σ_k w_k m_k (fp64, accumulated in place)
 __global__ void masked_weighted_sum_kernel(const float* __restrict__ x, const uint8_t* __restrict__ mask,
-                                           const float* __restrict__ w, float* __restrict__ num,
-                                           float* __restrict__ den, int K, long P, long ld) {
+                                           const double* __restrict__ w, double* __restrict__ num,
+                                           double* __restrict__ den, int K, long P, long ld) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
-    double a = 0, d = 0;
+    double a = num[i], d = den[i];
     for (int k = 0; k < K; ++k) {
       if (mask[(long)k * ld + i]) {
-        a += (double)w[k] * x[(long)k * ld + i];
+        a += w[k] * x[(long)k * ld + i];
         d += w[k];
       }
     }
-    num[i] = (float)a;
-    den[i] = (float)d;
+    num[i] = a;
+    den[i] = d;
   }
 }
 
@@ -636,7 +638,7 @@ void delta_rows(const float* theta, const float* base, float* out, int K, long P
   hipLaunchKernelGGL(delta_kernel, grid, dim3(256), 0, s, theta, base, out, P / 4, ld);
 }
 
-void weighted_sum(const float* x, const float* w, float* out, int K, long P, long ld, hipStream_t s) {
+void weighted_sum(const float* x, const double* w, double* out, int K, long P, long ld, hipStream_t s) {
   hipLaunchKernelGGL(weighted_sum_kernel, dim3(grid_for(P / 4, 256, 8192)), dim3(256), 0, s, x, w, out, K, P / 4, ld);
 }
 
@@ -651,7 +653,7 @@ void mix_rows(const float* x, const float* w, void* out, int K, int M, long P, l
                                      ld_out));
 }
 
-void masked_weighted_sum(const float* x, const uint8_t* mask, const float* w, float* num, float* den, int K, long P,
+void masked_weighted_sum(const float* x, const uint8_t* mask, const double* w, double* num, double* den, int K, long P,
                          long ld, hipStream_t s) {
   hipLaunchKernelGGL(masked_weighted_sum_kernel, dim3(grid_for(P, 256, 8192)), dim3(256), 0, s, x, mask, w, num, den,
                      K, P, ld);

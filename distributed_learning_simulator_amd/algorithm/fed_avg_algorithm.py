@@ -6,10 +6,12 @@ the first worker, merged `other_data`. Delta uploads are restored against θ_t f
 (`aggregation_algorithm.py:52-71`), i.e. θ_{t+1} = θ_t + Σ n_kΔ_k / Σ n_k.
 
 MI355X-native execution: per cohort ONE fused `weighted_sum` kernel
-over [K, P] (fp64 accumulation in registers, fp32 out) → after all local cohorts ONE
-`all_reduce(SUM)` of the accumulator and weights across ranks (RCCL over xGMI) → finalize
-on every rank. The result is already resident on every rank, so the broadcast M5 needs no
-second collective.
+over [K, P] adding into an fp64 accumulator (the reference's float64 invariant holds across
+cohorts AND ranks) → after all local cohorts ONE fp64 `all_reduce(SUM)` of the accumulator and
+weights across ranks (RCCL over xGMI; 2× the bytes of fp32, still ≈0.1 ms for ResNet-18) →
+finalize in fp64, cast to fp32 once. The result is already resident on every rank, so the
+broadcast M5 needs no second collective. A round in which no selected client reported (every
+one failed) leaves the global model unchanged.
 
 Generalisations used by the methods:
 * element masks (`msg.mask`, FedDropoutAvg) → per-element weights (`_get_weight` analogue);
@@ -23,6 +25,7 @@ import torch
 
 from ..message import CohortMessage, FlatParameterMessage
 from ..ops import fl
+from ..utils.logging import get_logger
 from .aggregation_algorithm import AggregationAlgorithm
 
 
@@ -40,7 +43,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
 
     # weights hook (reference `_get_weight`): dataset size
     def _weights(self, msg: CohortMessage) -> torch.Tensor:
-        return msg.dataset_sizes.to(self.device, torch.float32)
+        return msg.dataset_sizes.to(self.device, torch.float64)
 
     def _process(self, msg: CohortMessage, old_parameter) -> None:
         self.expected_kind = msg.kind if self._acc is None else self.expected_kind
@@ -49,13 +52,13 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             raise RuntimeError(f"mixed message kinds in one round: {self._kind} vs {msg.kind}")
         w = self._weights(msg)
         if msg.mask is not None:
-            num, den = fl.masked_weighted_sum(msg.data, msg.mask, w)
-            self._acc += num
-            self._w_elem = den if self._w_elem is None else self._w_elem + den
+            if self._w_elem is None:
+                self._w_elem = torch.zeros_like(self._acc)
+            fl.masked_weighted_sum(msg.data, msg.mask, w, self._acc, self._w_elem)
         else:
-            self._acc += fl.weighted_sum(msg.data, w)
+            fl.weighted_sum(msg.data, w, self._acc)
             if msg.block_mask is not None:
-                bw = (msg.block_mask.float() * w[:, None]).sum(0)
+                bw = (msg.block_mask.double() * w[:, None]).sum(0)
                 self._w_block = bw if self._w_block is None else self._w_block + bw
                 self._block_ids = msg.extra["block_ids"]
         self._w_total += w.sum()
@@ -71,13 +74,13 @@ class FedAVGAlgorithm(AggregationAlgorithm):
     def _ensure_acc(self) -> None:
         P = self.layout.padded_size
         if self._acc is None:
-            self._acc = torch.zeros(P, dtype=torch.float32, device=self.device)
-            self._w_total = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._acc = torch.zeros(P, dtype=torch.float64, device=self.device)
+            self._w_total = torch.zeros(1, dtype=torch.float64, device=self.device)
             self._kind = self.expected_kind
         if self.expects_element_mask and self._w_elem is None:
-            self._w_elem = torch.zeros(P, dtype=torch.float32, device=self.device)
+            self._w_elem = torch.zeros(P, dtype=torch.float64, device=self.device)
         if self.num_blocks and self._w_block is None:
-            self._w_block = torch.zeros(self.num_blocks, dtype=torch.float32, device=self.device)
+            self._w_block = torch.zeros(self.num_blocks, dtype=torch.float64, device=self.device)
             self._block_ids = self.block_ids
 
     def _reduce(self) -> None:
@@ -100,25 +103,35 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self._ensure_acc()
         self._reduce()
         acc = self._acc
-        old = old_parameter.to(self.device)
+        old_dtype = old_parameter.dtype
+        old = old_parameter.to(self.device, torch.float64)
+        zero = torch.zeros((), dtype=torch.float64, device=self.device)
         if self._w_elem is not None:
             den = self._w_elem
             if self._kind == "delta":
-                new = torch.where(den > 0, old + acc / den.clamp(min=1e-30), old)
+                new = torch.where(den > 0, old + acc / den.clamp(min=1e-300), old)
             else:
                 # reference `fed_dropout_avg/algorithm.py:9-18`: zero total weight -> 1
                 new = acc / torch.where(den == 0, torch.ones_like(den), den)
         elif self._w_block is not None:
             wb = self._w_block
             ids = self._block_ids.long()
-            we = torch.where(ids >= 0, wb[ids.clamp(min=0)], torch.zeros((), device=self.device))
+            we = torch.where(ids >= 0, wb[ids.clamp(min=0)], zero)
             if self._kind == "delta":
-                new = torch.where(we > 0, old + acc / we.clamp(min=1e-30), old)
+                new = torch.where(we > 0, old + acc / we.clamp(min=1e-300), old)
             else:
-                new = torch.where(we > 0, acc / we.clamp(min=1e-30), old)
+                new = torch.where(we > 0, acc / we.clamp(min=1e-300), old)
         else:
             wt = self._w_total
-            new = old + acc / wt if self._kind == "delta" else acc / wt
+            # every selected client failed / skipped: keep θ_t (no 0/0 NaN model)
+            if self._kind == "delta":
+                new = torch.where(wt > 0, old + acc / wt.clamp(min=1e-300), old)
+            else:
+                new = torch.where(wt > 0, acc / wt.clamp(min=1e-300), old)
+            if not bool(wt.item() > 0):
+                get_logger().warning("round without any reported client: global model unchanged")
+        self.last_fp64 = new  # pre-cast fp64 result (golden tests)
+        new = new.to(old_dtype)
         if self.config is not None and self.config.debug:
             assert not torch.isnan(new).any(), "NaN in aggregated parameters"
         msg = FlatParameterMessage(parameter=new, layout=self.layout, other_data=dict(self._other_data),

@@ -1,6 +1,11 @@
-"""Synthetic dataset zoo with the shapes of the datasets the reference configs name
-(SURVEY Appendix B). There is no network: every dataset is generated deterministically from
-(seed, name) — class-conditional and learnable, so FL accuracy curves are meaningful.
+"""Dataset zoo with the shapes of the datasets the reference configs name.
+
+There is no network: by default every dataset is generated deterministically from (seed, name)
+— class-conditional and learnable, so FL curves move, but accuracy is NOT comparable with the
+reference (runs are tagged `synthetic: true` in metrics.jsonl / round_record.json). Real data
+already on local disk is used instead when `dataset_kwargs.root` names a directory holding
+`<root>/<name>/{train,test}.npz` (images: `x` [N,H,W,C] uint8 or float, `y` [N]; text:
+`tokens` [N,L] int, `lengths` [N], `y` [N]); `numpy.load` with `allow_pickle=False`.
 
 Images are stored device-resident in the compute layout (NHWC, bf16 on GPU) when they fit
 (`materialize_limit` elements); larger ones (ImageNet-shaped) are generated procedurally per
@@ -81,6 +86,18 @@ def _hash_u32(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def _load_npz(root: str, name: str, split: str):
+    import os
+
+    import numpy as np
+
+    path = os.path.join(root, name, f"{split}.npz")
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"dataset_kwargs.root given but {path} is missing")
+    with np.load(path, allow_pickle=False) as f:
+        return {k: torch.from_numpy(np.ascontiguousarray(f[k])) for k in f.files}
+
+
 class ImageDataset:
     """Class-conditional images: x = prototype[y] (low-frequency pattern) + noise(index).
 
@@ -90,7 +107,7 @@ class ImageDataset:
 
     def __init__(self, spec: DatasetSpec, split: str, seed: int, device, dtype,
                  materialize_limit: int | None = None, noise: float = 1.0, signal: float = 0.35,
-                 channels: int | None = None):
+                 channels: int | None = None, arrays: dict | None = None, label_noise: float = 0.1):
         self.spec = spec
         self.split = split
         self.device = device
@@ -100,9 +117,21 @@ class ImageDataset:
         self.channels = max(int(channels or C0), C0)
         self.shape = (H0, W0, self.channels)
         n = spec.n_train if split == "train" else spec.n_test
+        if arrays is not None:
+            n = int(arrays["y"].shape[0])
         self.n = n
         g = torch.Generator().manual_seed(seed * 1000003 + (0 if split == "train" else 1))
         self.labels = (torch.randperm(n, generator=g) % spec.num_classes).to(torch.int32)
+        # the image is drawn from `source` class; a `label_noise` fraction carries a random label,
+        # so even a perfect model stays below 100 % (accuracy keeps discriminating numerics drift)
+        self.source = self.labels.clone()
+        if label_noise > 0:
+            flip = torch.rand(n, generator=g) < label_noise
+            self.labels = torch.where(flip, torch.randint(0, spec.num_classes, (n,), generator=g).to(torch.int32),
+                                      self.labels)
+        if arrays is not None:
+            self.labels = arrays["y"].to(torch.int32).reshape(-1)
+            self.source = self.labels
         H, W, C = spec.shape
         gp = torch.Generator().manual_seed(seed * 7919 + 17)  # prototypes shared by splits
         low = torch.randn(spec.num_classes, C, max(H // 4, 2), max(W // 4, 2), generator=gp)
@@ -112,10 +141,22 @@ class ImageDataset:
         self.salt = seed * 2654435761 + (0 if split == "train" else 97)
         if materialize_limit is None:  # elements: 32 GB of bf16 on a 288 GB MI355X, 4 GB on the host
             materialize_limit = 16_000_000_000 if torch.device(device).type == "cuda" else 2_000_000_000
-        self.materialized = n * H * W * self.channels <= materialize_limit
+        self.materialized = n * H * W * self.channels <= materialize_limit or arrays is not None
         self.labels_dev = self.labels.to(device)
+        self.source_dev = self.source.to(device)
         self.proto_dev = self.prototypes.to(device, dtype)
-        if self.materialized:
+        if arrays is not None:
+            x = arrays["x"].float()
+            if arrays["x"].dtype == torch.uint8:
+                x = x / 255.0
+            x = x.reshape(n, H, W, C)
+            mean = x.mean(dim=(0, 1, 2), keepdim=True)
+            std = x.std(dim=(0, 1, 2), keepdim=True).clamp(min=1e-6)
+            x = (x - mean) / std  # per-channel standardisation
+            if self.channels > C:
+                x = torch.nn.functional.pad(x, (0, self.channels - C))
+            self.data = x.to(device, dtype)
+        elif self.materialized:
             chunks = []
             dev = torch.device(device)
             for s in range(0, n, 8192):
@@ -135,7 +176,7 @@ class ImageDataset:
         # Box-Muller-free approx normal: sum of two uniforms, centred, var 1/6 -> scale
         u = (h.float() + h2.float()) * (1.0 / 4294967296.0) - 1.0
         noise = u * math.sqrt(6.0) * self.noise
-        lab = self.labels[idx.cpu()].long() if device.type == "cpu" else self.labels_dev[idx].long()
+        lab = self.source[idx.cpu()].long() if device.type == "cpu" else self.source_dev[idx].long()
         proto = (self.prototypes if device.type == "cpu" else self.proto_dev.float())[lab]
         img = (proto + noise.view(-1, H, W, C)).to(dtype)
         if self.channels > C:
@@ -165,8 +206,18 @@ class TextDataset:
     """Class-conditional token sequences: each class has its own Zipf-like preference over a
     slice of the vocabulary; lengths vary in [max_len/4, max_len]. Token 0 = padding."""
 
-    def __init__(self, spec: DatasetSpec, split: str, seed: int, device):
+    def __init__(self, spec: DatasetSpec, split: str, seed: int, device, arrays: dict | None = None):
         self.spec = spec
+        if arrays is not None:
+            tok = arrays["tokens"].to(torch.int32)[:, : spec.max_len]
+            if tok.shape[1] < spec.max_len:
+                tok = torch.nn.functional.pad(tok, (0, spec.max_len - tok.shape[1]))
+            self.n = int(tok.shape[0])
+            self.labels = arrays["y"].to(torch.int32).reshape(-1)
+            self.tokens = tok.to(device)
+            self.lengths = arrays["lengths"].to(torch.int32).clamp(max=spec.max_len).to(device)
+            self.labels_dev = self.labels.to(device)
+            return
         n = spec.n_train if split == "train" else spec.n_test
         self.n = n
         g = torch.Generator().manual_seed(seed * 1000033 + (0 if split == "train" else 1))
@@ -204,6 +255,7 @@ class DatasetCollection:
     # Validation phase carved out of the test split (`split_validation`); None = whole test set
     test_indices: torch.Tensor | None = None
     validation_indices: torch.Tensor | None = None
+    synthetic: bool = True
 
     @property
     def name(self):
@@ -229,15 +281,22 @@ def create_dataset_collection(name: str, dataset_kwargs: dict | None, seed: int,
     """`image_channels`: stored channel count for image sets (≥ the dataset's; zero-padded)."""
     spec = get_spec(name, dataset_kwargs)
     kw = dict(dataset_kwargs or {})
+    root = kw.get("root")
+    arrays = {sp: _load_npz(root, spec.name, sp) for sp in ("train", "test")} if root else {"train": None, "test": None}
+    if root and spec.kind == "image":
+        spec.n_train, spec.n_test = (int(arrays[sp]["y"].shape[0]) for sp in ("train", "test"))
     if spec.kind == "image":
         noise = float(kw.get("noise", 1.0))
         signal = float(kw.get("signal", 0.35))
+        ln = float(kw.get("label_noise", 0.1))
         return DatasetCollection(spec, ImageDataset(spec, "train", seed, device, dtype, noise=noise, signal=signal,
-                                                    channels=image_channels),
+                                                    channels=image_channels, arrays=arrays["train"], label_noise=ln),
                                  ImageDataset(spec, "test", seed, device, dtype, noise=noise, signal=signal,
-                                              channels=image_channels))
+                                              channels=image_channels, arrays=arrays["test"], label_noise=ln),
+                                 synthetic=not root)
     if spec.kind == "text":
-        return DatasetCollection(spec, TextDataset(spec, "train", seed, device), TextDataset(spec, "test", seed, device))
+        return DatasetCollection(spec, TextDataset(spec, "train", seed, device, arrays["train"]),
+                                 TextDataset(spec, "test", seed, device, arrays["test"]), synthetic=not root)
     if spec.kind == "graph":
         from .graph import GraphDataset
 

@@ -130,6 +130,7 @@ class CohortTrainer:
         # host time than the GPU needs to run them
         self.use_graphs = os.environ.get("DLS_GRAPHS", "1") != "0"
         self._graphs: dict = {}
+        self.max_graphs = int(os.environ.get("DLS_MAX_GRAPHS", "2"))
         self.hooks = HookRegistry()
         self.adam_step_count = torch.zeros(capacity, dtype=torch.float32, device=self.device)
         self.graph = dataset_collection.graph
@@ -412,6 +413,15 @@ class CohortTrainer:
         key = (K, B, tuple(parts))
         sg = self._graphs.get(key)
         if sg is None:
+            # each captured graph owns a private pool sized for a full K-client step; K varies
+            # with failures / last waves / uneven rank shares, so keep only the most recent
+            # `max_graphs` (the dropped graph's pool returns to the driver before the next capture)
+            while len(self._graphs) >= self.max_graphs:
+                old = self._graphs.pop(next(iter(self._graphs)))
+                old.graph = None
+                del old
+                torch.cuda.synchronize(self.device)
+                torch.cuda.empty_cache()
             sg = self._graphs[key] = _StepGraph(K, B, self.device)
         streams = self._streams(len(parts))
 

@@ -46,6 +46,19 @@ class ShapleyValueAlgorithm(FedAVGAlgorithm):
     def choose_best_subset(self) -> bool:
         return bool(self.config.algorithm_kwargs.get("choose_best_subset", False))
 
+    # checkpoint / resume: per-round values as plain floats, so the checkpoint
+    # still loads with torch.load(weights_only=True)
+    def state_dict(self) -> dict:
+        def plain(d):
+            return {int(r): {int(w): float(v) for w, v in vals.items()} for r, vals in d.items()}
+
+        # (the estimators are re-seeded per round: no other state to carry)
+        return {"shapley_values": plain(self.shapley_values), "shapley_values_S": plain(self.shapley_values_S)}
+
+    def load_state_dict(self, state: dict) -> None:
+        self.shapley_values = {int(r): dict(v) for r, v in state.get("shapley_values", {}).items()}
+        self.shapley_values_S = {int(r): dict(v) for r, v in state.get("shapley_values_S", {}).items()}
+
     def _process(self, msg, old_parameter) -> None:
         sizes = msg.dataset_sizes.tolist()
         for i, c in enumerate(msg.client_ids):
@@ -120,8 +133,8 @@ class ShapleyValueAlgorithm(FedAVGAlgorithm):
             chosen = sorted(self.shapley_values_S[rnd])
             get_logger().warning("use subset %s", chosen)
         sel = [ids.index(c) for c in chosen]
-        w = torch.tensor([sizes[i] for i in sel], dtype=torch.float32, device=rows.device)
-        new = fl.weighted_sum(rows[sel].contiguous(), w / w.sum())
+        w = torch.tensor([sizes[i] for i in sel], dtype=torch.float64, device=rows.device)
+        new = fl.weighted_sum(rows[sel].contiguous(), w / w.sum()).float()
         self._rows.clear()
         msg = FlatParameterMessage(parameter=new, layout=self.layout, other_data=dict(self._other_data),
                                    end_training=bool(self._end_training))

@@ -60,9 +60,9 @@ def delta_rows(theta_rows, base, out=None):
     return be.delta_rows(theta_rows, base, out)
 
 
-def weighted_sum(x, w):
-    """Σ_k w_k x[k,:] -> fp32 [P] (fp64 accumulation)."""
-    return backend.get(x).weighted_sum(x, w)
+def weighted_sum(x, w, out=None):
+    """out (fp64 [P]; zeros if None) += Σ_k w_k x[k,:], fp64 accumulation. Returns `out`."""
+    return backend.get(x).weighted_sum(x, w, out)
 
 
 def mix_rows(x, w, out_dtype):
@@ -71,8 +71,9 @@ def mix_rows(x, w, out_dtype):
     return backend.get(x).mix_rows(x, w, out_dtype)
 
 
-def masked_weighted_sum(x, mask, w):
-    return backend.get(x).masked_weighted_sum(x, mask, w)
+def masked_weighted_sum(x, mask, w, num=None, den=None):
+    """(num, den) fp64 [P] += (Σ_k w_k m_k x_k, Σ_k w_k m_k)."""
+    return backend.get(x).masked_weighted_sum(x, mask, w, num, den)
 
 
 # ------------------------------------------------------------------ compression ops

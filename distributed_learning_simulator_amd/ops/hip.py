@@ -511,10 +511,13 @@ def delta_rows(theta_rows, base, out=None):
     return out
 
 
-def weighted_sum(x, w):
+def weighted_sum(x, w, out=None):
+    """out (fp64 [P], zeros if None) += Σ_k w_k x[k, :] — fp64 accumulation, fp64 result."""
     K, P, ld = _row_args(x)
-    out = torch.empty(P, dtype=torch.float32, device=x.device)
-    _C.weighted_sum(_p(x), _p(w.float().contiguous()), _p(out), K, P, ld, _s())
+    if out is None:
+        out = torch.zeros(P, dtype=torch.float64, device=x.device)
+    assert out.dtype == torch.float64 and out.is_contiguous() and out.numel() == P
+    _C.weighted_sum(_p(x), _p(w.double().contiguous()), _p(out), K, P, ld, _s())
     return out
 
 
@@ -538,13 +541,15 @@ def mix_rows(x, w, out_dtype=BF16):
     return out
 
 
-def masked_weighted_sum(x, mask, w):
+def masked_weighted_sum(x, mask, w, num=None, den=None):
+    """(num, den) fp64 [P] += (Σ_k w_k m_k x_k, Σ_k w_k m_k)."""
     K, P, ld = _row_args(x)
     mask = mask.to(torch.uint8)
     assert mask.is_contiguous() and mask.shape == (K, P) and ld == P
-    num = torch.empty(P, dtype=torch.float32, device=x.device)
-    den = torch.empty(P, dtype=torch.float32, device=x.device)
-    _C.masked_weighted_sum(_p(x), _p(mask), _p(w.float().contiguous()), _p(num), _p(den), K, P, ld, _s())
+    num = torch.zeros(P, dtype=torch.float64, device=x.device) if num is None else num
+    den = torch.zeros(P, dtype=torch.float64, device=x.device) if den is None else den
+    assert num.dtype == den.dtype == torch.float64
+    _C.masked_weighted_sum(_p(x), _p(mask), _p(w.double().contiguous()), _p(num), _p(den), K, P, ld, _s())
     return num, den
 
 

@@ -351,13 +351,13 @@ def adam_step(theta, grad, m, v, lr, active, step, beta1, beta2, eps, weight_dec
         shadow.copy_(theta.to(shadow.dtype))
 
 
-def weighted_sum(x, w, base=None):
-    """Σ_k w_k x[k,:] (+ base·Σw if base given), accumulated in fp64 (reference FedAvg
-    accumulates in float64: `fed_avg_algorithm.py:39-52`). Returns fp32 [P]."""
+def weighted_sum(x, w, out=None):
+    """out (fp64) += Σ_k w_k x[k,:] accumulated in fp64 (reference FedAvg accumulates in
+    float64: `fed_avg_algorithm.py:39-52`). Returns the fp64 [P] accumulator."""
     acc = (x.double() * w.double().to(x.device)[:, None]).sum(dim=0)
-    if base is not None:
-        acc = acc + base.double() * w.double().sum()
-    return acc.float()
+    if out is None:
+        return acc
+    return out.add_(acc)
 
 
 def mix_rows(x, w, out_dtype=torch.float32):
@@ -365,10 +365,14 @@ def mix_rows(x, w, out_dtype=torch.float32):
     return (w.double().to(x.device) @ x.double()).to(out_dtype)
 
 
-def masked_weighted_sum(x, mask, w):
-    """FedDropoutAvg: numerator Σ w_k m_k x_k and per-element denominator Σ w_k m_k."""
+def masked_weighted_sum(x, mask, w, num=None, den=None):
+    """FedDropoutAvg: numerator Σ w_k m_k x_k and per-element denominator Σ w_k m_k (fp64)."""
     wm = mask.double() * w.double().to(x.device)[:, None]
-    return (x.double() * wm).sum(0).float(), wm.sum(0).float()
+    n, d = (x.double() * wm).sum(0), wm.sum(0)
+    if num is not None:
+        n = num.add_(n)
+        d = den.add_(d)
+    return n, d
 
 
 def broadcast_rows(dst, src, rows=None):

@@ -104,7 +104,8 @@ class AggregationServer(Server):
         elif result.end_training:
             self._record_compute_stat(result.parameter)
         self.global_parameter = result.parameter
-        if self.config.save_models and self.session.is_main and "init" not in result.other_data:
+        spill = self.config.save_models or self.config.limited_resource
+        if spill and self.session.is_main and "init" not in result.other_data:
             self._save_model(result.parameter, os.path.join(self.config.save_dir, "aggregated_model",
                                                             f"round_{self._round_number}.pk"))
 
@@ -147,6 +148,8 @@ class AggregationServer(Server):
     def _record_compute_stat(self, parameter: torch.Tensor, key=None) -> None:
         metric = self.get_metric(parameter)
         round_stat = {f"test_{k}": v for k, v in metric.items()}
+        # synthetic data (the default, no network): accuracy is not comparable with the reference
+        round_stat["synthetic"] = bool(getattr(self.session.dc, "synthetic", True))
         key = self._get_stat_key() if key is None else key
         self._stat[key] = round_stat
         self.last_recorded = (key, round_stat)

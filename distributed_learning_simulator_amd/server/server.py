@@ -35,8 +35,13 @@ class Server(Executor):
         n = self.config.algorithm_kwargs.get("random_client_number")
         if n is None or int(n) >= self.worker_number:
             return list(range(self.worker_number))
-        rng = random.Random((self.config.seed + 1) * 1_000_003 + self._get_stat_key() * 7919)
+        rng = random.Random((self.config.seed + 1) * 1_000_003 + self._selection_key() * 7919)
         return sorted(rng.sample(range(self.worker_number), int(n)))
+
+    def _selection_key(self) -> int:
+        """Seed of the round's client selection: the round number (not the stat key, which
+        stays constant between evaluations when `eval_every` > 1 or in FedOBD's stage 1)."""
+        return int(getattr(self, "_round_number", 0))
 
     def _get_stat_key(self):
         return 0

@@ -96,8 +96,12 @@ class Session:
         if self.dc.spec.kind == "graph":
             capacity = per_rank  # halo exchange needs every client of the rank resident at once
         else:
+            # `limited_resource` (reference aggregation_worker.py:124-130 spills the worker's model
+            # cache to disk): here the rank keeps a quarter of the HBM budget for clients (more,
+            # smaller waves) and the server spills each round's global model to disk
             capacity = plan_capacity(per_rank, self.layout, self.model, self.dc, self.hyper, self.device,
-                                     self.compute_dtype, explicit=cfg.cohort_size)
+                                     self.compute_dtype, explicit=cfg.cohort_size,
+                                     fraction=0.2 if cfg.limited_resource else 0.8)
         self.trainer = CohortTrainer(self.model, self.dc, self.hyper, self.device, self.compute_dtype, capacity)
         self.trainer.debug = bool(cfg.debug)
         algo = cfg.distributed_algorithm
@@ -151,6 +155,8 @@ class Session:
         else:
             init = server._before_start()
             theta_recv, down = server.send_result(init)
+            if not cfg.distribute_init_parameters:
+                down = 0  # no M1 message: clients start from their own init (AggregationWorker)
             self.bytes_down_total += down
             server.last_recorded = None  # the round-0 (init) stat is not a round row
         while not server._stopped():
@@ -261,7 +267,8 @@ class Session:
         active = [c for c in selected if c not in set(failed)]
         local = self.local_clients(active)
         if server.algorithm is not None:
-            server.algorithm.expected_kind = "delta" if getattr(worker, "_send_parameter_diff", True) else "parameter"
+            server.algorithm.expected_kind = (worker.upload_kind() if hasattr(worker, "upload_kind") else
+                                              "delta" if getattr(worker, "_send_parameter_diff", True) else "parameter")
         up0 = worker.endpoint.bytes_sent
         for msg in worker.run_round(r, theta_recv, local):
             server._process_worker_data(msg)
@@ -311,7 +318,7 @@ class Session:
             self.server.last_recorded = None
         row = {"round": r, "wall_s": wall, "rounds_per_s": 1.0 / max(wall, 1e-9), "selected_clients": len(selected),
                "comm_bytes_up": up, "comm_bytes_down": down, "comm_bytes_total": up + down,
-               "gpus": self.comm.world, **stat, **extra}
+               "gpus": self.comm.world, "synthetic": bool(self.dc.synthetic), **stat, **extra}
         self.metrics.append(row)
         get_logger().info("round %s done in %.3fs (up %.1f MiB, down %.1f MiB)", r, wall, up / 2**20, down / 2**20)
         return row

@@ -39,6 +39,11 @@ class AggregationWorker(Worker):
         self._best_acc: torch.Tensor | None = None
         if session is not None and config.dataset_sampling == "iid" and session.dc.validation_indices is not None:
             self.enable_choose_model_by_validation()
+        # `distribute_init_parameters: false` (reference aggregation_server.py:58,
+        # aggregation_worker.py:36): no θ0 broadcast — in the first round every client starts
+        # from its OWN random init (seeded by client id, so every rank agrees) and uploads full
+        # parameters (there is no common base to take a delta against)
+        self._own_init = not bool(getattr(config, "distribute_init_parameters", True))
 
     # ------------------------------------------------- keep best by validation
     def enable_choose_model_by_validation(self) -> None:
@@ -75,16 +80,23 @@ class AggregationWorker(Worker):
     def local_epochs(self) -> int:
         return self._epochs
 
+    def upload_kind(self) -> str:
+        return "delta" if (self._send_parameter_diff and not self._own_init) else "parameter"
+
     def run_round(self, round_num: int, theta_g: torch.Tensor, client_ids: list[int]) -> Iterator[CohortMessage]:
         self._round_num = round_num
         cap = self.trainer.capacity
         for w0 in range(0, len(client_ids), cap):
             wave = client_ids[w0 : w0 + cap]
             yield self.train_wave(round_num, theta_g, wave)
+        self._own_init = False  # from round 2 on every client starts from the broadcast model
 
     def train_wave(self, round_num: int, theta_g: torch.Tensor, wave: list[int]) -> CohortMessage:
         K = len(wave)
-        self._load_result_from_server(theta_g, K)
+        if self._own_init:
+            self._load_own_init(wave)
+        else:
+            self._load_result_from_server(theta_g, K)
         schedule = self.build_schedule(round_num, wave)
         if self._choose_model_by_validation:
             self.trainer.hooks.append_named_hook(ExecutorHookPoint.AFTER_EPOCH, "keep_model_hook",
@@ -114,12 +126,19 @@ class AggregationWorker(Worker):
             # gradient (first-step flags in the schedule); Adam moments zeroed
             self.trainer.reset_optimizer(K)
 
+    def _load_own_init(self, wave: list[int]) -> None:
+        layout = self.trainer.layout
+        rows = torch.stack([layout.init_flat(torch.Generator().manual_seed(
+            (self.config.seed * 1_000_003 + 7919 * (c + 1)) & 0x7FFFFFFF)) for c in wave])
+        self.trainer.load_rows(rows.to(self.trainer.device))
+        self.trainer.reset_optimizer(len(wave))
+
     def _get_sent_data(self, wave: list[int], theta_g: torch.Tensor, stats) -> CohortMessage:
         K = len(wave)
         rows = self.trainer.buffers.theta[:K]
         if self._choose_model_by_validation and self._best_acc is not None:
             rows.copy_(self._best_theta[:K])  # "use best model"
-        if self._send_parameter_diff:
+        if self.upload_kind() == "delta":
             data = fl.delta_rows(rows, theta_g, out=rows)
             kind = "delta"
         else:

@@ -37,29 +37,32 @@ class GradientWorker(AggregationWorker):
     def __init__(self, config, endpoint, session=None, **kwargs):
         super().__init__(config, endpoint, session, **kwargs)
         self.disable_choose_model_by_validation()
+        # gradient methods share ONE model (every client applies the same aggregated step), so
+        # without an initial broadcast all clients start from the same seeded init (0 bytes)
+        self._own_init = False
         self.epoch_stat: dict = {}
         opt = (session.trainer.hyper.optimizer_name if session is not None else config.optimizer_name) or "SGD"
         assert opt.lower() == "sgd", "GradientWorker applies SGD itself (reference gradient_worker.py:32)"
 
     # ------------------------------------------------------ aggregation hooks
     def _new_accumulator(self, P: int, device) -> dict:
-        return {"sum": torch.zeros(P, dtype=torch.float32, device=device),
-                "weight": torch.zeros(1, dtype=torch.float32, device=device)}
+        return {"sum": torch.zeros(P, dtype=torch.float64, device=device),
+                "weight": torch.zeros(1, dtype=torch.float64, device=device)}
 
     def _process_gradient(self, g: torch.Tensor) -> torch.Tensor:
         """Override point (reference `_process_gradient`): g [K,P] fp32 → wire payload."""
         return g
 
     def _accumulate(self, acc: dict, payload: torch.Tensor, active: torch.Tensor, weight: torch.Tensor) -> None:
-        w = weight * active.float()
-        acc["sum"] += fl.weighted_sum(payload, w)
+        w = weight.double() * active.double()
+        fl.weighted_sum(payload, w, acc["sum"])
         acc["weight"] += w.sum()
 
     def _reduce(self, acc: dict) -> None:
         self.session.comm.all_reduce_many_([acc["sum"], acc["weight"]])
 
     def _finalize(self, acc: dict) -> torch.Tensor:
-        return (acc["sum"] / acc["weight"].clamp(min=1e-12)).unsqueeze(0)
+        return (acc["sum"] / acc["weight"].clamp(min=1e-12)).float().unsqueeze(0)
 
     def _wire_bytes_per_client(self) -> int:
         return self.trainer.layout.num_params * 4

@@ -1,0 +1,117 @@
+"""FedAvg's fp64 invariant end to end (reference `algorithm/fed_avg_algorithm.py:39-52`:
+Σ float64(θ_k)·n_k over ALL workers, one division, one cast): 100 clients uploaded as 3 cohorts
+per rank over 2 ranks (gloo) give the CPU float64 FedAvg to 1e-12 before the final fp32 cast,
+and exactly its fp32 rounding after it. Also: a round in which every selected client failed
+keeps the global model (no 0/0 NaN) — ADVICE r1."""
+
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+P_LOGICAL = 1000
+
+
+def _layout():
+    from distributed_learning_simulator_amd.engine.params import ParamLayout
+
+    lay = ParamLayout()
+    lay.add("w", (P_LOGICAL,))
+    return lay
+
+
+def _data(seed=11, n_clients=100):
+    g = torch.Generator().manual_seed(seed)
+    lay = _layout()
+    P = lay.padded_size
+    old = torch.randn(P, generator=g) * 3
+    deltas = torch.randn(n_clients, P, generator=g) * torch.logspace(-6, 0, P)[None, :]
+    sizes = torch.randint(50, 600, (n_clients,), generator=g).double()
+    return lay, old, deltas, sizes
+
+
+def _aggregate(rank, world, clients, cohorts, comm):
+    from distributed_learning_simulator_amd.algorithm.fed_avg_algorithm import FedAVGAlgorithm
+    from distributed_learning_simulator_amd.message import CohortMessage
+
+    lay, old, deltas, sizes = _data()
+    algo = FedAVGAlgorithm()
+    algo.bind(None, lay, "cpu", comm)
+    mine = clients[rank::world]
+    for part in torch.tensor_split(torch.tensor(mine), cohorts):
+        ids = part.tolist()
+        if not ids:
+            continue
+        msg = CohortMessage(client_ids=ids, dataset_sizes=sizes[ids], kind="delta", data=deltas[ids].contiguous())
+        algo.process_worker_data(msg, old)
+    out = algo.aggregate_worker_data(old)
+    return out.parameter, algo.last_fp64
+
+
+def _golden(clients):
+    _, old, deltas, sizes = _data()
+    d = deltas[clients].double()
+    w = sizes[clients]
+    return old.double() + (w[:, None] * d).sum(0) / w.sum()
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DLS_FORCE_CPU="1")
+    from distributed_learning_simulator_amd.parallel import comm as commmod
+
+    commmod._COMM = None
+    c = commmod.init_distributed(prefer_gpu=False)
+    q.put((rank,) + _aggregate(rank, world, list(range(100)), 3, c))
+    commmod.shutdown()
+
+
+def test_fedavg_fp64_two_ranks_three_cohorts():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gold = _golden(list(range(100)))
+    for _, new32, new64 in outs:
+        assert new64.dtype == torch.float64
+        rel = ((new64 - gold).abs() / gold.abs().clamp(min=1e-30)).max().item()
+        assert rel <= 1e-12, rel
+        assert torch.equal(new32, gold.float())
+
+
+def test_fedavg_fp64_single_rank_matches():
+    from distributed_learning_simulator_amd.parallel.comm import Comm
+
+    new32, new64 = _aggregate(0, 1, list(range(100)), 7, Comm())
+    gold = _golden(list(range(100)))
+    assert ((new64 - gold).abs() / gold.abs().clamp(min=1e-30)).max().item() <= 1e-12
+    assert torch.equal(new32, gold.float())
+
+
+def test_all_clients_failed_keeps_model(tmp_path):
+    from distributed_learning_simulator_amd.config import config_from_dict
+    from distributed_learning_simulator_amd.parallel.comm import Comm
+    from distributed_learning_simulator_amd.session import Session
+
+    cfg = config_from_dict({"distributed_algorithm": "fed_avg", "dataset_name": "MNIST", "model_name": "LeNet5",
+                            "worker_number": 4, "round": 2, "epoch": 1, "batch_size": 32,
+                            "dataset_kwargs": {"scale": 0.02}, "save_dir": str(tmp_path), "log_level": "WARNING",
+                            "algorithm_kwargs": {"failure_rate": 1.0}})
+    sess = Session(cfg, comm=Comm())
+    init = sess.server._before_start()
+    theta, _ = sess.server.send_result(init)
+    theta0 = sess.server.global_parameter.clone()
+    sess.run_one_round(theta)
+    after = sess.server.global_parameter
+    assert torch.isfinite(after).all()
+    assert torch.equal(after, theta0)

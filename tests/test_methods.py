@@ -261,3 +261,45 @@ def test_failure_injection_and_phase_timers(tmp_path):
         assert r["selected_clients"] + r.get("failed_clients", 0) == 6
         assert r["comm_bytes_up"] == r["selected_clients"] * sess.layout.num_params * 4
         assert {"train_s", "aggregate_s", "eval_broadcast_s"} <= set(r)
+
+
+def test_checkpoint_resume_gtg_keeps_shapley_values(tmp_path):
+    """ShapleyValueAlgorithm state (per-round SV dicts) survives checkpoint/resume."""
+    base = {"round": 3, "epoch": 1, "worker_number": 3, "dataset_kwargs.scale": 0.04, "log_level": "WARNING",
+            "checkpoint_every": 1}
+    full, res_full = _run("gtg_sv/mnist.yaml", base, tmp_path / "full")
+    part, _ = _run("gtg_sv/mnist.yaml", {**base, "round": 2}, tmp_path / "part")
+    resumed, res = _run("gtg_sv/mnist.yaml", {**base, "resume_from": str(tmp_path / "part" / "checkpoint.pt")},
+                        tmp_path / "resumed")
+    assert sorted(res["sv"]) == sorted(res_full["sv"]) == [1, 2, 3]
+    for r in res_full["sv"]:
+        for w, v in res_full["sv"][r].items():
+            assert abs(res["sv"][r][w] - v) < 1e-9
+    import json
+
+    sv_json = json.load(open(tmp_path / "resumed" / "shapley_values.json"))
+    assert sorted(int(k) for k in sv_json) == [1, 2, 3]
+
+
+def test_no_initial_distribution_own_init(tmp_path):
+    """`distribute_init_parameters: false` (reference aggregation_server.py:58): no θ0 message,
+    round-1 clients start from their own init and upload full parameters."""
+    sess, res = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 3, "dataset_kwargs.scale": 0.04,
+                                            "log_level": "WARNING", "distribute_init_parameters": False}, tmp_path)
+    P = sess.layout.num_params * 4
+    # M1 costs nothing; rounds 1 and 2 broadcast to the 3 clients
+    assert res["bytes_down"] == 2 * 3 * P
+    assert torch.isfinite(sess.server.global_parameter).all()
+    ref_sess, _ = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 3,
+                                              "dataset_kwargs.scale": 0.04, "log_level": "WARNING"}, tmp_path / "b")
+    assert not torch.equal(ref_sess.server.global_parameter, sess.server.global_parameter)
+
+
+def test_limited_resource_spills_global_models(tmp_path):
+    sess, _ = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 2, "dataset_kwargs.scale": 0.04,
+                                          "log_level": "WARNING", "limited_resource": True, "save_models": False},
+                   tmp_path)
+    saved = sorted(os.listdir(tmp_path / "aggregated_model"))
+    assert saved == ["round_1.pk", "round_2.pk"]
+    t = torch.load(tmp_path / "aggregated_model" / "round_2.pk", weights_only=True)
+    assert set(t) == {e.name for e in sess.layout.entries}

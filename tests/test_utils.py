@@ -52,3 +52,38 @@ def test_memory_plan_cpu_and_state_bytes():
     # CPU: no device budget → every client resident; explicit cohort_size wins
     assert plan_capacity(37, model.layout, model, None, None, torch.device("cpu"), torch.float32) == 37
     assert plan_capacity(37, model.layout, model, None, None, torch.device("cpu"), torch.float32, explicit=8) == 8
+
+
+def test_local_npz_dataset_and_synthetic_tag(tmp_path):
+    """`dataset_kwargs.root`: real arrays from local disk replace the synthetic generator, and
+    runs say which one they used."""
+    import json
+
+    import numpy as np
+
+    from distributed_learning_simulator_amd.config import config_from_dict
+    from distributed_learning_simulator_amd.parallel.comm import Comm
+    from distributed_learning_simulator_amd.session import Session
+
+    rng = np.random.default_rng(0)
+    d = tmp_path / "data" / "MNIST"
+    d.mkdir(parents=True)
+    for split, n in (("train", 240), ("test", 80)):
+        y = rng.integers(0, 10, n)
+        x = (rng.random((n, 28, 28, 1)) * 60 + y[:, None, None, None] * 19).astype(np.uint8)
+        np.savez(d / f"{split}.npz", x=x, y=y)
+    base = {"distributed_algorithm": "fed_avg", "dataset_name": "MNIST", "model_name": "LeNet5", "worker_number": 2,
+            "round": 1, "epoch": 1, "batch_size": 32, "log_level": "WARNING"}
+    sess = Session(config_from_dict({**base, "dataset_kwargs": {"root": str(tmp_path / "data")},
+                                     "save_dir": str(tmp_path / "real")}), comm=Comm())
+    assert sess.dc.train.n == 240 and not sess.dc.synthetic
+    assert torch.equal(sess.dc.train.labels.long(), torch.from_numpy(np.load(d / "train.npz")["y"]).long())
+    sess.run()
+    row = json.loads(open(tmp_path / "real" / "metrics.jsonl").readline())
+    assert row["synthetic"] is False
+    rec = json.load(open(tmp_path / "real" / "server" / "round_record.json"))
+    assert rec["1"]["synthetic"] is False
+    syn = Session(config_from_dict({**base, "dataset_kwargs": {"scale": 0.01}, "save_dir": str(tmp_path / "syn")}),
+                  comm=Comm())
+    syn.run()
+    assert json.loads(open(tmp_path / "syn" / "metrics.jsonl").readline())["synthetic"] is True
