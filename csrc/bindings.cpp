@@ -19,9 +19,11 @@ PYBIND11_MODULE(_dls_hip, m) {
 
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
-                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s) {
+                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s, int ldx, int ldy) {
     ConvNTParams p{};
     p.f32 = f32;
+    p.ldx = ldx;
+    p.ldy = ldy;
     p.acc = P<const bf16_t>(acc);
     p.gate = P<const bf16_t>(gate);
     p.x = P<const bf16_t>(x);
@@ -35,9 +37,10 @@ PYBIND11_MODULE(_dls_hip, m) {
     conv_nt(p, K, variant, S(s));
   });
   m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, ptr acc, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
-                         int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, ptr s) {
+                         int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, ptr s, int ld_dy,
+                         long dy_cs) {
     conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), P<const bf16_t>(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
-               stride, pad, variant, f32, S(s));
+               stride, pad, variant, f32, S(s), ld_dy, dy_cs);
   });
   m.def("conv_gl_wanted", &conv_gl_wanted);
   m.def("conv_gl_fwd", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int K, int rep,
@@ -58,9 +61,11 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt_default_variant", &conv_nt_default_variant);
   m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,
                       int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, int variant, int f32,
-                      ptr s) {
+                      ptr s, int ldy, int ldx) {
     ConvTNParams p{};
     p.f32 = f32;
+    p.ldy = ldy;
+    p.ldx = ldx;
     p.dy = P<const bf16_t>(dy);
     p.x = P<const bf16_t>(x);
     p.dw = P<float>(dw);
@@ -69,24 +74,27 @@ PYBIND11_MODULE(_dls_hip, m) {
     p.M = M; p.Co = Co; p.R = R; p.splitk = 1; p.m_per_split = M;
     conv_tn(p, K, variant, S(s));
   });
-  m.def("conv_tn_splitk", &conv_tn_splitk);
+  m.def("conv_tn_splitk", &conv_tn_splitk, py::arg("K"), py::arg("Co"), py::arg("R"), py::arg("M"), py::arg("C"),
+        py::arg("variant"), py::arg("f32"), py::arg("ldy") = 0, py::arg("ldx") = 0);
   m.def("conv_tn_num_variants", &conv_tn_num_variants);
   m.def("conv_nt_f32_num_variants", &conv_nt_f32_num_variants);
   m.def("conv_tn_f32_num_variants", &conv_tn_f32_num_variants);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
-                     int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, int f32, ptr s) {
+                     int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, int f32, ptr s,
+                     int ldx) {
     bn_fwd(P<const void>(x), P<const void>(gamma), P<const void>(beta), P<const void>(res), P<void>(y), P<float>(mean),
            P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws), P<uint8_t>(mask),
-           P<unsigned>(counters), f32, S(s));
+           P<unsigned>(counters), f32, S(s), ldx);
   });
   m.def("bn_bwd", [](ptr dy, ptr x, ptr y, ptr mean, ptr rstd, ptr gamma, ptr valid, long g_cs, int K, int R, int C,
                      int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr mask, ptr counters,
-                     int f32, ptr s) {
+                     int f32, ptr s, int ldx, int acc_dx) {
     bn_bwd(P<const void>(dy), P<const void>(x), P<const void>(y), P<const float>(mean), P<const float>(rstd),
            P<const void>(gamma), P<const int>(valid), g_cs, K, R, C, relu, P<void>(dx), P<void>(dpre), P<float>(dgamma),
-           P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), P<unsigned>(counters), f32, S(s));
+           P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), P<unsigned>(counters), f32, S(s), ldx,
+           acc_dx);
   });
   m.def("ln_fwd", [](ptr x, ptr gamma, ptr beta, ptr y, ptr mean, ptr rstd, long g_cs, int K, long rpc, int C,
                      float eps, int rep, int f32, ptr s) {

@@ -19,6 +19,8 @@
 #include "dls.h"
 #include "gemm_common.h"
 
+#include <numeric>
+
 namespace {
 
 template <int V>
@@ -101,7 +103,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
     const uint32_t ow = rem - oh * p.OW;
     a_ih0[j] = (int)oh * p.stride - p.pad;
     a_iw0[j] = (int)ow * p.stride - p.pad_w;
-    a_ptr[j] = x + (long)b * p.H * p.W * p.C;
+    a_ptr[j] = x + (long)b * p.H * p.W * p.ldx;
   }
   int r_cur = kca * VA;
   int kh, kw, c;
@@ -133,7 +135,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
         qw /= p.dil;
       }
       if (qh < 0 || qh >= p.H || qw < 0 || qw >= p.W) continue;
-      fload(ra[j], a_ptr[j] + ((long)qh * p.W + qw) * p.C + c);
+      fload(ra[j], a_ptr[j] + ((long)qh * p.W + qw) * p.ldx + c);
     }
     if constexpr (!BKM) {
       const int rB = k0 + kcb * VB;
@@ -272,7 +274,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
     bvals[j] = (bias && n < p.N) ? bias[n] : 0.f;
   }
   float* slab = reinterpret_cast<float*>(smem) + wid * 32 * SW;
-  const bool vec_ok = (p.N % 4) == 0;
+  const bool vec_ok = (p.N % 4) == 0 && (p.ldy % 4) == 0 && ((uintptr_t)y & 15) == 0;
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -298,19 +300,19 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
         const uint32_t ow = rem - oh * p.OW;
         row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
       }
-      float* dst = y + row * p.N + n;
+      float* dst = y + row * p.ldy + n;
       const float* src = slab + r * SW + cc;
       if (vec_ok && n + 4 <= p.N) {
         float4 v = *reinterpret_cast<const float4*>(src);
         if (gatep) {
-          const float4 gv = *reinterpret_cast<const float4*>(gatep + row * p.N + n);
+          const float4 gv = *reinterpret_cast<const float4*>(gatep + row * p.ldy + n);
           v.x = gv.x > 0.f ? v.x : 0.f;
           v.y = gv.y > 0.f ? v.y : 0.f;
           v.z = gv.z > 0.f ? v.z : 0.f;
           v.w = gv.w > 0.f ? v.w : 0.f;
         }
         if (accp) {
-          const float4 av = *reinterpret_cast<const float4*>(accp + row * p.N + n);
+          const float4 av = *reinterpret_cast<const float4*>(accp + row * p.ldy + n);
           v.x += av.x;
           v.y += av.y;
           v.z += av.z;
@@ -320,8 +322,8 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
       } else {
         for (int t2 = 0; t2 < 4 && n + t2 < p.N; ++t2) {
           float o = src[t2];
-          if (gatep && !(gatep[row * p.N + n + t2] > 0.f)) o = 0.f;
-          if (accp) o += accp[row * p.N + n + t2];
+          if (gatep && !(gatep[row * p.ldy + n + t2] > 0.f)) o = 0.f;
+          if (accp) o += accp[row * p.ldy + n + t2];
           dst[t2] = o;
         }
       }
@@ -423,7 +425,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p
     for (int j = 0; j < PA; ++j) {
       const int m = k0 + tid / CCA + j * RPA;
       fzero(ra[j]);
-      if (cok && m < mend) fload(ra[j], dy + (long)m * p.Co + cocol);
+      if (cok && m < mend) fload(ra[j], dy + (long)m * p.ldy + cocol);
     }
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
@@ -436,7 +438,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p
       const uint32_t ow = rem - oh * p.OW;
       const int ih = (int)oh * p.stride - p.pad + kh, iw = (int)ow * p.stride - p.pad + kw;
       if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
-      fload(rb[j], x + (((long)b * p.H + ih) * p.W + iw) * p.C + c);
+      fload(rb[j], x + (((long)b * p.H + ih) * p.W + iw) * p.ldx + c);
     }
   };
   auto store = [&](int buf) {
@@ -612,7 +614,7 @@ int conv_nt_f32_num_variants() { return 8; }
 
 void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
   const bool bkm = p.b_kmajor != 0;
-  const int va = vw(p.C);
+  const int va = vw(std::gcd(p.C, p.ldx));
   int vb = bkm ? vw(p.N) : vw(p.R);
   if (variant < 0) {
     // measured (bench/kernel_bench.py --f32 --sweep, ResNet-18 layers, K = 100): the single-buffer
@@ -634,8 +636,8 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
 int conv_tn_f32_num_variants() { return kTnF32Variants; }
 
 void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s) {
-  const int va = vw(p.Co);
-  const int vb = vw(p.C);
+  const int va = vw(std::gcd(p.Co, p.ldy));
+  const int vb = vw(std::gcd(p.C, p.ldx));
   variant = resolve_tn_f32_variant(variant, K, p.Co, p.R, va, vb);
   tn_f32_split(K, p.Co, p.R, p.M, variant, p.splitk, p.m_per_split);
   const TnTile t = kTnF32Tiles[variant];
@@ -644,9 +646,10 @@ void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s) {
   if (!launch_tn_f32_variant(variant, p, va, vb, grid, s)) fprintf(stderr, "conv_tn_f32: bad variant %d\n", variant);
 }
 
-int conv_tn_f32_splitk(int K, int Co, int R, int M, int C, int variant) {
+// gco / gc: the channel counts' gcd with their row strides (they set the vector widths)
+int conv_tn_f32_splitk(int K, int Co, int R, int M, int gco, int gc, int variant) {
   int splitk, mps;
-  variant = resolve_tn_f32_variant(variant, K, Co, R, vw(Co), vw(C));
+  variant = resolve_tn_f32_variant(variant, K, Co, R, vw(gco), vw(gc));
   tn_f32_split(K, Co, R, M, variant, splitk, mps);
   return splitk;
 }

@@ -17,6 +17,8 @@
 #include "dls.h"
 #include "gemm_common.h"
 
+#include <numeric>
+
 namespace {
 
 template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int DEPTH>
@@ -68,7 +70,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
     const uint32_t ow = rem - oh * p.OW;
     a_ih0[j] = (int)oh * p.stride - p.pad;
     a_iw0[j] = (int)ow * p.stride - p.pad_w;
-    a_ptr[j] = x + (long)b * p.H * p.W * p.C;
+    a_ptr[j] = x + (long)b * p.H * p.W * p.ldx;
   }
   int r_cur = kca * VA;
   int kh, kw, c;
@@ -102,7 +104,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
         qw /= p.dil;
       }
       if (qh < 0 || qh >= p.H || qw < 0 || qw >= p.W) continue;
-      ra[j] = *reinterpret_cast<const TA*>(a_ptr[j] + ((long)qh * p.W + qw) * p.C + c);
+      ra[j] = *reinterpret_cast<const TA*>(a_ptr[j] + ((long)qh * p.W + qw) * p.ldx + c);
     }
     if constexpr (!BKM) {
       const int rB = k0 + kcb * VB;
@@ -244,7 +246,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
     bvals[j] = (bias && n < p.N) ? bf2f(bias[n]) : 0.f;
   }
   bf16_t* slab = reinterpret_cast<bf16_t*>(smem) + wid * 32 * SW;
-  const bool vec_ok = (p.N % 8) == 0;
+  const bool vec_ok = (p.N % 8) == 0 && (p.ldy % 8) == 0 && ((uintptr_t)y & 15) == 0;
   __syncthreads();  // every wave is done reading the K-loop tiles that the slabs overwrite
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -270,9 +272,9 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_kernel(ConvNTParams p) {
         const uint32_t ow = rem - oh * p.OW;
         row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
       }
-      bf16_t* dst = y + row * p.N + n;
-      const bf16_t* acc_row = accp ? accp + row * p.N + n : nullptr;
-      const bf16_t* gate_row = gatep ? gatep + row * p.N + n : nullptr;
+      bf16_t* dst = y + row * p.ldy + n;
+      const bf16_t* acc_row = accp ? accp + row * p.ldy + n : nullptr;
+      const bf16_t* gate_row = gatep ? gatep + row * p.ldy + n : nullptr;
       const bf16_t* src = slab + r * SW + cc;
       if (vec_ok && n + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
@@ -370,6 +372,8 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
     p.kh_step = p.kw_step = 1;
   }
   if (p.out_s == 0) p.out_s = 1;
+  if (p.ldx == 0) p.ldx = p.C;
+  if (p.ldy == 0) p.ldy = p.N;
   p.fd_ohw = make_fastdiv((uint32_t)(p.OH * p.OW));
   p.fd_ow = make_fastdiv((uint32_t)p.OW);
   p.fd_kwc = make_fastdiv((uint32_t)(p.KW * p.C));
@@ -379,7 +383,7 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
     return;
   }
   const bool bkm = p.b_kmajor != 0;
-  int va = vec_width(p.C);
+  int va = vec_width(std::gcd(p.C, p.ldx));  // vectors must not straddle a channel-sliced pixel
   int vb = bkm ? vec_width(p.N) : vec_width(p.R);
   if (va == 1 && vb == 4) vb = 1;
   if (variant < 0) {
@@ -400,15 +404,17 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
 }
 
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
-                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s) {
+                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
+                int ld_dy, long dy_cs) {
   ConvNTParams p{};
   p.f32 = f32;
+  p.ldx = ld_dy;  // dY may be a channel slice of a wider buffer (DenseNet block)
   p.x = dy;
   p.w = w;
   p.y = dx;
   p.bias = nullptr;
   p.acc = acc;
-  p.x_cs = (long)B * OH * OW * Co;
+  p.x_cs = dy_cs ? dy_cs : (long)B * OH * OW * (ld_dy ? ld_dy : Co);
   p.y_cs = (long)B * H * W * Ci;
   p.w_cs = w_cs;
   p.b_cs = 0;

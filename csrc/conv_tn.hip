@@ -11,6 +11,8 @@
 #include "dls.h"
 #include "gemm_common.h"
 
+#include <numeric>
+
 namespace {
 
 constexpr int BKT_MAX = 64;  // largest pixel (reduction) tile: split-K granularity
@@ -70,7 +72,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_kernel(ConvTNParams p) {
     for (int j = 0; j < PA; ++j) {
       const int m = k0 + tid / CCA + j * RPA;
       ra[j] = vzero<VA>();
-      if (cok && m < mend) ra[j] = *reinterpret_cast<const TA*>(dy + (long)m * p.Co + cocol);
+      if (cok && m < mend) ra[j] = *reinterpret_cast<const TA*>(dy + (long)m * p.ldy + cocol);
     }
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
@@ -83,7 +85,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_kernel(ConvTNParams p) {
       const uint32_t ow = rem - oh * p.OW;
       const int ih = (int)oh * p.stride - p.pad + kh, iw = (int)ow * p.stride - p.pad + kw;
       if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
-      rb[j] = *reinterpret_cast<const TB*>(x + (((long)b * p.H + ih) * p.W + iw) * p.C + c);
+      rb[j] = *reinterpret_cast<const TB*>(x + (((long)b * p.H + ih) * p.W + iw) * p.ldx + c);
     }
   };
   auto store_from = [&](const TA* ra, const TB* rb, int buf) {
@@ -273,12 +275,14 @@ int conv_tn_num_variants() { return kTnVariants; }
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s) {
   p.fd_ohw = make_fastdiv((uint32_t)(p.OH * p.OW));
   p.fd_ow = make_fastdiv((uint32_t)p.OW);
+  if (p.ldy == 0) p.ldy = p.Co;
+  if (p.ldx == 0) p.ldx = p.C;
   if (p.f32) {  // reference precision: split-bf16 MFMA kernel (conv_f32.hip)
     conv_tn_f32(p, K, variant, s);
     return;
   }
-  const int va = vec_width(p.Co);
-  const int vb = vec_width(p.C);
+  const int va = vec_width(std::gcd(p.Co, p.ldy));
+  const int vb = vec_width(std::gcd(p.C, p.ldx));
   variant = resolve_tn_variant(variant, K, p.Co, p.R, va, vb);
   tn_split(K, p.Co, p.R, p.M, variant, p.splitk, p.m_per_split);
   const TnTile t = kTnTiles[variant];
@@ -287,10 +291,12 @@ void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s) {
   if (!launch_tn_variant(variant, p, va, vb, grid, s)) fprintf(stderr, "conv_tn: bad variant %d\n", variant);
 }
 
-int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32) {
-  if (f32) return conv_tn_f32_splitk(K, Co, R, M, C, variant);
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32, int ldy, int ldx) {
+  if (ldy == 0) ldy = Co;
+  if (ldx == 0) ldx = C;
+  if (f32) return conv_tn_f32_splitk(K, Co, R, M, std::gcd(Co, ldy), std::gcd(C, ldx), variant);
   int splitk, mps;
-  variant = resolve_tn_variant(variant, K, Co, R, vec_width(Co), vec_width(C));
+  variant = resolve_tn_variant(variant, K, Co, R, vec_width(std::gcd(Co, ldy)), vec_width(std::gcd(C, ldx)));
   tn_split(K, Co, R, M, variant, splitk, mps);
   return splitk;
 }

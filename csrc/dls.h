@@ -49,6 +49,9 @@ struct ConvNTParams {
   // 1: every tensor pointer above is fp32 (reference precision); the GEMM runs as split-bf16
   // ("bf16x3") on the MFMA with fp32 accumulation (conv_f32.hip)
   int f32;
+  // channel strides of channel-sliced views (DenseNet's preallocated block buffer): A pixel
+  // stride ldx (0 = C), output / acc / gate row stride ldy (0 = N)
+  int ldx, ldy;
 };
 
 struct ConvTNParams {
@@ -61,6 +64,7 @@ struct ConvTNParams {
   int splitk, m_per_split;
   FastDiv fd_ohw, fd_ow;  // filled by conv_tn()
   int f32;                // 1: dy / x are fp32 (split-bf16 GEMM, conv_f32.hip)
+  int ldy, ldx;           // dy row stride (0 = Co), x pixel stride (0 = C): channel-sliced views
 };
 
 // Large-tile conv GEMM fed by the LDS-DMA (conv_gl.hip): K loop over a tap table × 64-channel
@@ -103,17 +107,18 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // dX of a conv (any stride): stride-1 → one flipped-weight NT GEMM; stride s > 1 → s² parity
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
-                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s);
+                int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
+                int ld_dy = 0, long dy_cs = 0);
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
-int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32);
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32, int ldy = 0, int ldx = 0);
 // fp32 (split-bf16 MFMA) GEMMs, conv_f32.hip; reached through conv_nt / conv_tn with p.f32 = 1
 void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s);
 int conv_nt_f32_num_variants();
 void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_f32_num_variants();
-int conv_tn_f32_splitk(int K, int Co, int R, int M, int C, int variant);
+int conv_tn_f32_splitk(int K, int Co, int R, int M, int gco, int gc, int variant);
 
 // ---------------------------------------------------------------- normalisation
 // Activation / γ / β pointers are the compute dtype: bf16 (f32 = 0) or fp32 (f32 = 1, the
@@ -121,12 +126,15 @@ int conv_tn_f32_splitk(int K, int Co, int R, int M, int C, int variant);
 long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
-            uint8_t* relu_mask, unsigned* counters, int f32,
-            hipStream_t s);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused coefs)
+            uint8_t* relu_mask, unsigned* counters, int f32, hipStream_t s,
+            int ldx = 0);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused coefs);
+                           // ldx: row stride of x / res (channel slice of a wider buffer), y contiguous
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
             float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, unsigned* counters, int f32,
-            hipStream_t s);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate
+            hipStream_t s, int ldx = 0,
+            int acc_dx = 0);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
+                              // stride ldx, acc_dx: dx += (DenseNet block-buffer gradient)
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
             long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s);
 void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,

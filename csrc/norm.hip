@@ -8,6 +8,7 @@
 // gradient buffer (row stride P).
 #include "common.h"
 #include <algorithm>
+#include <numeric>
 
 #include "dls.h"
 
@@ -83,7 +84,10 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
                                                           const float* __restrict__ rstd,
                                                           const int* __restrict__ valid_rows, int R, int C, int relu,
                                                           float* __restrict__ ws, long ws_cs, int rpb,
-                                                          const uint8_t* __restrict__ rmask, BNCoefArgs ca) {
+                                                          const uint8_t* __restrict__ rmask, BNCoefArgs ca, int lda,
+                                                          int ldb) {
+  // lda / ldb: row strides of a and of b (channel-sliced views of a wider buffer, DenseNet);
+  // yv is contiguous (row stride C)
   __shared__ float red[2][256 * V];
   __shared__ int is_last;
   const int k = blockIdx.y;
@@ -92,7 +96,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const int r0 = blockIdx.x * rpb;
   const int r1 = min(nvalid, r0 + rpb);
-  const long base = (long)k * R * C;
+  const long base = (long)k * R * C, base_a = (long)k * R * lda, base_b = (long)k * R * ldb;
   for (int cg = 0; cg < CT; cg += 256) {
     const int ctn = min(256, CT - cg);
     const int RT = 256 / ctn;
@@ -114,7 +118,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
       for (int r = r0 + rl; r < r1; r += RT) {
         const long off = base + (long)r * C + c0;
         float va[V];
-        load_vec<V>(a + off, va);
+        load_vec<V>(a + base_a + (long)r * lda + c0, va);
         if (MODE == 0) {
 #pragma unroll
           for (int i = 0; i < V; ++i) {
@@ -126,7 +130,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
           for (int i = 0; i < V; ++i) s0[i] += va[i];
         } else {
           float vx[V], vy[V];
-          load_vec<V>(b + off, vx);
+          load_vec<V>(b + base_b + (long)r * ldb + c0, vx);
           uint32_t mbits = 0xFFu;
           if (rmask) {  // 1-bit ReLU mask written by the forward (V == 8): 1/16 of reading y
             mbits = rmask[((long)k * R + r) * (C / 8) + c0 / 8];
@@ -272,12 +276,13 @@ template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                        T* __restrict__ y, const int* __restrict__ valid_rows,
                                                        const float* __restrict__ coef, int R, int C, int relu,
-                                                       int rpb, uint8_t* __restrict__ rmask) {
+                                                       int rpb, uint8_t* __restrict__ rmask, int ldx) {
+  // x / res rows at stride ldx (channel slice of a wider buffer), y contiguous
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const int r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
-  const long base = (long)k * R * C;
+  const long base = (long)k * R * C, base_x = (long)k * R * ldx;
   for (int cg = 0; cg < CT; cg += 256) {
     const int ctn = min(256, CT - cg);
     const int RT = 256 / ctn;
@@ -295,12 +300,13 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
       float out[V];
       if (r < nvalid) {
         float v[V];
-        load_vec<V>(x + off, v);
+        const long offx = base_x + (long)r * ldx + c0;
+        load_vec<V>(x + offx, v);
 #pragma unroll
         for (int j = 0; j < V; ++j) out[j] = fmaf(v[j], sc[j], sh[j]);
         if (res) {
           float rv[V];
-          load_vec<V>(res + off, rv);
+          load_vec<V>(res + offx, rv);
 #pragma unroll
           for (int j = 0; j < V; ++j) out[j] += rv[j];
         }
@@ -329,12 +335,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
                                                            const int* __restrict__ valid_rows,
                                                            const float* __restrict__ coef, int R, int C, int relu,
                                                            T* __restrict__ dx, T* __restrict__ dpre,
-                                                           int rpb, const uint8_t* __restrict__ rmask) {
+                                                           int rpb, const uint8_t* __restrict__ rmask, int ldx,
+                                                           int acc_dx) {
+  // x and dx rows at stride ldx (channel slice of a wider buffer); acc_dx: dx += (DenseNet: the
+  // block buffer's gradient collects every later layer's contribution); dy / y / dpre contiguous
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const int r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
-  const long base = (long)k * R * C;
+  const long base = (long)k * R * C, base_x = (long)k * R * ldx;
   for (int cg = 0; cg < CT; cg += 256) {
     const int ctn = min(256, CT - cg);
     const int RT = 256 / ctn;
@@ -351,11 +360,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
     }
     for (int r = r0 + rl; r < r1; r += RT) {
       const long off = base + (long)r * C + c0;
+      const long offx = base_x + (long)r * ldx + c0;
       float o[V], gp[V];
       if (r < nvalid) {
         float vdy[V], vx[V];
         load_vec<V>(dy + off, vdy);
-        load_vec<V>(x + off, vx);
+        load_vec<V>(x + offx, vx);
         if (rmask) {
           const uint32_t mbits = rmask[((long)k * R + r) * (C / 8) + c0 / 8];
 #pragma unroll
@@ -375,7 +385,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
         for (int j = 0; j < V; ++j) o[j] = gp[j] = 0.f;
       }
-      store_vec<V>(dx + off, o);
+      if (acc_dx) {
+        float prev[V];
+        load_vec<V>(dx + offx, prev);
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] += prev[j];
+      }
+      store_vec<V>(dx + offx, o);
       if (dpre) store_vec<V>(dpre + off, gp);
     }
   }
@@ -503,46 +519,50 @@ long bn_workspace_floats(int K, long R, int C) {
 
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
-            uint8_t* rmask, unsigned* counters, int f32, hipStream_t s) {
+            uint8_t* rmask, unsigned* counters, int f32, hipStream_t s, int ldx) {
+  if (ldx == 0) ldx = C;
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
-  const int V = vw(C);
+  const int V = vw(std::gcd(C, ldx));
   BNCoefArgs ca{gamma, beta, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, eps, rep, 0, counters};
   if (V != 8) rmask = nullptr;  // bit masks need 8-channel vectors
   DISPATCH_T(f32, {
     DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 0>), grid, dim3(256), 0, s, CP(x), nullptr, nullptr,
-                                     nullptr, nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr, ca));
+                                     nullptr, nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr, ca, ldx,
+                                     ldx));
     if (!counters)
       hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, CP(gamma),
                          CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C,
                          eps, rep, 0);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
-                                     valid_rows, coef, R, C, relu, rpb, rmask));
+                                     valid_rows, coef, R, C, relu, rpb, rmask, ldx));
   });
 }
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
-            float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s) {
+            float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s,
+            int ldx, int acc_dx) {
+  if (ldx == 0) ldx = C;
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
-  const int V = vw(C);
+  const int V = vw(std::gcd(C, ldx));
   if (V != 8) rmask = nullptr;
   BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1, counters};
   DISPATCH_T(f32, {
     DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
-                                     mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca));
+                                     mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
     if (!counters)
       hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, CP(gamma),
                          (const TT*)nullptr, valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs,
                          g_cs, K, R, C, 0.f, 1, 1);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
-                                     valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask));
+                                     valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx));
   });
 }
 
@@ -553,7 +573,7 @@ void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, in
   const int V = vw(C);
   DISPATCH_T(f32, DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 2>), grid, dim3(256), 0, s, CP(x),
                                                    nullptr, nullptr, nullptr, nullptr, nullptr, (int)rows, C, 0, out,
-                                                   out_cs, rpb, nullptr, BNCoefArgs{})));
+                                                   out_cs, rpb, nullptr, BNCoefArgs{}, C, C)));
 }
 
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,

@@ -208,6 +208,25 @@ class Transition(Module):
         return self.pool.forward(self.conv.forward(self.norm.forward(x, ctx), ctx), ctx)
 
 
+class DenseBlock(Seq):
+    """The layers of one dense block run as ONE fused autograd op over a preallocated feature
+    buffer (Fn.dense_block: no per-layer concat). Module/param names are the Sequential's
+    (`dense1.0.norm.weight`, ...), so OBD block discovery and messages see the same structure."""
+
+    kind = "Sequential"
+
+    def __init__(self, layers, growth):
+        super().__init__(*layers)
+        self.growth = growth
+
+    def forward(self, x, ctx):
+        P = ctx.P
+        lps = [Fn.DenseLayerParams(P.w(l.norm.gamma), P.w(l.norm.beta), P.g(l.norm.gamma), P.g(l.norm.beta),
+                                   P.w(l.conv.w), P.g(l.conv.w)) for l in self.children]
+        rps = x.shape[2] * x.shape[3]
+        return Fn.dense_block(x, ctx.token, lps, self.growth, ctx.valid_rows(rps))
+
+
 class DenseNetNet(Module):
     kind = "DenseNet"
 
@@ -222,7 +241,7 @@ class DenseNetNet(Module):
             for _ in range(n):
                 layers.append(DenseLayer(c, growth))
                 c += growth
-            self.blocks.append(self.child(f"dense{b + 1}", Seq(*layers)))
+            self.blocks.append(self.child(f"dense{b + 1}", DenseBlock(layers, growth)))
             if b < 2:
                 self.blocks.append(self.child(f"trans{b + 1}", Transition(c, c)))
         self.child("norm", BatchNorm(c, relu=True))

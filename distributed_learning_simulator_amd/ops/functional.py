@@ -384,3 +384,90 @@ class _SpMM(torch.autograd.Function):
 def spmm(x, graph):
     """A @ x for a shared normalised adjacency `graph` (CSR + its transpose)."""
     return _SpMM.apply(x, graph.rowptr, graph.col, graph.val, graph.rowptr_t, graph.col_t, graph.val_t)
+
+
+# ---------------------------------------------------------------------- dense block
+class DenseLayerParams:
+    """One DenseNet layer's parameter views: BN (γ, β and their grads) + 3x3 conv (w, grad)."""
+
+    __slots__ = ("gamma", "beta", "ggamma", "gbeta", "w", "gw")
+
+    def __init__(self, gamma, beta, ggamma, gbeta, w, gw):
+        self.gamma, self.beta, self.ggamma, self.gbeta, self.w, self.gw = gamma, beta, ggamma, gbeta, w, gw
+
+
+class _DenseBlock(torch.autograd.Function):
+    """A whole DenseNet block (L × [BN-ReLU-Conv3x3, concat]) over ONE preallocated feature
+    buffer F [K, B, H, W, c0 + L·g]: layer i's BN reads the channel prefix F[..., :c_i] in place
+    (channel-strided kernels) and its conv writes the g new channels straight into
+    F[..., c_i : c_i + g] through the epilogue's row stride — no per-layer `torch.cat` (which
+    re-copies the growing prefix every layer: Σ c_i channel-copies per block). The backward walks
+    the layers in reverse over one gradient buffer dF: layer i's conv dgrad reads its slice of dF
+    in place and the BN backward ADDS its input gradient into dF[..., :c_i].
+    Reference: torchvision-style `_DenseLayer` + `torch.cat` (the cyy_torch_vision densenet40,
+    SURVEY §2.7), BN with batch statistics (`util/model.py:23`)."""
+
+    @staticmethod
+    def forward(ctx, x, token, layers, growth, valid_rows):
+        be = _be(x)
+        K, B, H, W, c0 = x.shape
+        L = len(layers)
+        Ct = c0 + L * growth
+        F = torch.empty((K, B, H, W, Ct), dtype=x.dtype, device=x.device)
+        F[..., :c0].copy_(x)
+        native = be is not ref
+        saved = []
+        for i, lp in enumerate(layers):
+            ci = c0 + i * growth
+            xi = F[..., :ci].reshape(K, -1, ci)
+            if native:
+                y, mean, rstd, mask = be.bn_fwd(xi, lp.gamma, lp.beta, valid_rows, True, None, with_mask=True)
+                be.conv_fwd(y.view(K, B, H, W, ci), lp.w, 1, 1, out=F[..., ci : ci + growth])
+            else:
+                y, mean, rstd = ref.bn_fwd(xi, lp.gamma, lp.beta, valid_rows, True, None)
+                mask = None
+                F[..., ci : ci + growth].copy_(ref.conv_fwd(y.view(K, B, H, W, ci), lp.w, 1, 1))
+            saved.append((y, mean, rstd, mask))
+        ctx.save_for_backward(F)
+        ctx.saved = saved
+        ctx.layers, ctx.growth, ctx.valid_rows, ctx.c0 = layers, growth, valid_rows, c0
+        return F
+
+    @staticmethod
+    def backward(ctx, dF_out):
+        (F,) = ctx.saved_tensors
+        be = _be(dF_out)
+        native = be is not ref
+        K, B, H, W, Ct = F.shape
+        g, c0 = ctx.growth, ctx.c0
+        dF = dF_out.contiguous().clone() if native else dF_out.float().clone()
+        for i in range(len(ctx.layers) - 1, -1, -1):
+            lp = ctx.layers[i]
+            y, mean, rstd, mask = ctx.saved[i]
+            ci = c0 + i * g
+            d_out = dF[..., ci : ci + g]
+            yv = y.view(K, B, H, W, ci)
+            xi = F[..., :ci].reshape(K, -1, ci)
+            if native:
+                if lp.gw is not None:
+                    be.conv_wgrad(d_out, yv, lp.gw, 1, 1)
+                dy = be.conv_dgrad(d_out, lp.w, (H, W), 1, 1)
+                be.bn_bwd(dy.view(K, -1, ci), xi, y, mean, rstd, lp.gamma, ctx.valid_rows, True, lp.ggamma, lp.gbeta,
+                          False, relu_mask=mask, dx_out=dF[..., :ci].reshape(K, -1, ci))
+            else:
+                d_out = d_out.contiguous()
+                if lp.gw is not None:
+                    lp.gw.copy_(ref.conv_wgrad(d_out.float(), yv.float(), (K,) + tuple(lp.w.shape[1:]), 1, 1))
+                dy = ref.conv_dgrad(d_out, lp.w.to(d_out.dtype), (H, W), 1, 1)
+                dx, dgamma, dbeta, _ = ref.bn_bwd(dy.view(K, -1, ci), xi, y, mean, rstd, lp.gamma, ctx.valid_rows, True)
+                if lp.ggamma is not None:
+                    lp.ggamma.copy_(dgamma)
+                    lp.gbeta.copy_(dbeta)
+                dF[..., :ci] += dx.view(K, B, H, W, ci).to(dF.dtype)
+        ctx.saved = None
+        return dF[..., :c0].contiguous().to(dF_out.dtype), None, None, None, None
+
+
+def dense_block(x, token, layers: list[DenseLayerParams], growth: int, valid_rows=None):
+    """All layers of a DenseNet block in one buffer (see _DenseBlock)."""
+    return _DenseBlock.apply(x, token, layers, growth, valid_rows)

@@ -72,6 +72,25 @@ def _check(t: torch.Tensor, dtype=None, contiguous=True, name="tensor"):
         assert t.is_contiguous(), f"{name} must be contiguous"
 
 
+def _pix_stride(t: torch.Tensor):
+    """(t, pixel/row stride) of a [K, ..., C] tensor. A channel slice of a wider contiguous
+    buffer (DenseNet's block buffer F[..., a:b]) keeps one uniform stride between consecutive
+    pixels: it is passed to the kernels as is (stride ld ≥ C, client stride t.stride(0));
+    anything else is made contiguous (ld = C)."""
+    C = t.shape[-1]
+    if t.is_contiguous():
+        return t, C
+    if t.stride(-1) != 1 or t.dim() < 3:
+        return t.contiguous(), C
+    ld = t.stride(-2)
+    expect = ld
+    for d in range(t.dim() - 2, 0, -1):
+        if t.shape[d] != 1 and t.stride(d) != expect:
+            return t.contiguous(), C
+        expect *= t.shape[d]
+    return t, ld
+
+
 _ws_cache: dict = {}
 
 
@@ -123,37 +142,46 @@ def _gl(K: int, M: int, N: int, C: int, taps: int) -> bool:
     return bool(_C.conv_gl_wanted(K, M, N, C, taps, mode))
 
 
-def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False):
+def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None):
+    """`x` may be a channel slice of a wider buffer, `out` (optional) a channel slice to write
+    into (DenseNet block buffer): both are read / written in place through channel strides."""
     K, B, H, W, C = x.shape
-    x = x.contiguous()
+    x, ldx = _pix_stride(x)
     f32 = _f32(x)
-    _check(x, x.dtype, name="x")
+    _check(x, x.dtype, contiguous=False, name="x")
     _check(w, x.dtype, contiguous=False, name="w")
     Kw, Co, KH, KW, Ci = w.shape
     assert Ci == C, (Ci, C)
     w_cs, rep = _client_view(w, K)
     OH = (H + 2 * pad - KH) // stride + 1
     OW = (W + 2 * pad - KW) // stride + 1
-    y = torch.empty((K, B, OH, OW, Co), dtype=x.dtype, device=x.device)
+    if out is None:
+        y, ldy = torch.empty((K, B, OH, OW, Co), dtype=x.dtype, device=x.device), Co
+    else:
+        assert out.shape == (K, B, OH, OW, Co) and out.dtype == x.dtype
+        y, ldy = _pix_stride(out)
+        assert y.data_ptr() == out.data_ptr(), "out must be a row-strided view"
     b_cs = 0
     if bias is not None:
         assert bias.dtype == x.dtype
         b_cs, _ = _client_view(bias, K)
     M = B * OH * OW
-    if not f32 and _gl(K, M, Co, C, KH * KW):
+    if not f32 and ldx == C and ldy == Co and _gl(K, M, Co, C, KH * KW):
         _C.conv_gl_fwd(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, K, rep, B, H, W, C, OH, OW,
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
-    _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
-               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32, _s())
+    _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), x.stride(0), y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
+               pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32,
+               _s(), ldx, ldy)
     return y
 
 
 def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
     """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
-    residual branch of a ResNet block, so autograd never materialises the sum separately)."""
+    residual branch of a ResNet block, so autograd never materialises the sum separately).
+    `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient)."""
     K, B, OH, OW, Co = dy.shape
-    dy = dy.contiguous()
+    dy, ld_dy = _pix_stride(dy)
     f32 = _f32(dy)
     _check(w, dy.dtype, contiguous=False, name="w")
     Kw, Co2, KH, KW, Ci = w.shape
@@ -163,7 +191,7 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
     dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
     if acc is not None:
         assert stride == 1 and acc.shape == dx.shape and acc.dtype == dy.dtype and acc.is_contiguous(), acc.shape
-    if not f32 and (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
+    if not f32 and ld_dy == Co and (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
         # (strided dgrad splits into stride² short-K parity classes: conv_nt's smaller tiles win
         # there, l3a dgrad 447 vs 396 TFLOP/s). Large tiles want a k-contiguous B: one flip+transpose pass over the weight rows
         # (weights are small next to the activations), then stride² parity-class launches
@@ -174,27 +202,27 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
     _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
-                  nt_f32_variant if f32 else nt_variant, f32, _s())
+                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy.stride(0))
     return dx
 
 
 def conv_wgrad(dy, x, gw, stride: int, pad: int):
     K, B, OH, OW, Co = dy.shape
     _, _, H, W, C = x.shape
-    dy = dy.contiguous()
-    x = x.contiguous()
+    dy, ldy = _pix_stride(dy)
+    x, ldx = _pix_stride(x)
     f32 = _f32(dy)
-    _check(x, dy.dtype, name="x")
+    _check(x, dy.dtype, contiguous=False, name="x")
     assert gw.dtype == torch.float32 and gw.shape[0] == K and gw[0].is_contiguous()
     _, Co2, KH, KW, Ci = gw.shape
     assert Co2 == Co and Ci == C
     M = B * OH * OW
     R = KH * KW * C
     tv = tn_f32_variant if f32 else tn_variant
-    if _C.conv_tn_splitk(K, Co, R, M, C, tv, f32) > 1:
+    if _C.conv_tn_splitk(K, Co, R, M, C, tv, f32, ldy, ldx) > 1:
         gw.zero_()
-    _C.conv_tn(_p(dy), _p(x), _p(gw), M * Co, B * H * W * C, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M,
-               Co, R, K, tv, f32, _s())
+    _C.conv_tn(_p(dy), _p(x), _p(gw), dy.stride(0), x.stride(0), gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad,
+               M, Co, R, K, tv, f32, _s(), ldy, ldx)
 
 
 def bias_grad(dy, gb):
@@ -220,7 +248,7 @@ def linear_fwd(x, w, b=None, relu=False, acc=None):
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s())
+               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0)
     return y
 
 
@@ -238,7 +266,7 @@ def linear_dgrad(dy, w, gate=None):
         assert gate.shape == dx.shape and gate.dtype == dy.dtype and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
-               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s())
+               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0)
     return dx
 
 
@@ -254,7 +282,7 @@ def linear_wgrad(dy, x, gw, gb=None):
     if _C.conv_tn_splitk(K, Fo, Fi, N, Fi, tv, f32) > 1:
         gw.zero_()
     _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K,
-               tv, f32, _s())
+               tv, f32, _s(), 0, 0)
     if gb is not None:
         gb.zero_()
         _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, f32, _s())
@@ -263,41 +291,55 @@ def linear_wgrad(dy, x, gw, gb=None):
 # ------------------------------------------------------------------------ batchnorm
 def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False):
     """Returns (y, mean, rstd); with_mask=True (ReLU, C % 8 == 0) also returns the 1-bit ReLU
-    mask [K, R, C/8] uint8 that bn_bwd can read instead of y."""
+    mask [K, R, C/8] uint8 that bn_bwd can read instead of y. `x` (and `residual`) may be
+    channel slices of a wider buffer ([K, R, C] at row stride ld); y is contiguous."""
     K, R, C = x.shape
-    x = x.contiguous()
+    x, ldx = _pix_stride(x)
+    assert x.stride(0) == R * ldx, "client stride of a strided BN input must be R*ld"
     g_cs, rep = _client_view(gamma, K)
-    y = torch.empty_like(x)
+    y = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
     mean = torch.empty((K, C), dtype=torch.float32, device=x.device)
     rstd = torch.empty((K, C), dtype=torch.float32, device=x.device)
     ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     if residual is not None:
-        residual = residual.contiguous()
+        residual = residual.contiguous() if ldx == C else residual
+        assert _pix_stride(residual)[1] == ldx and residual.stride() == x.stride()
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     mask = None
-    if with_mask and relu and C % 8 == 0:
+    if with_mask and relu and C % 8 == 0 and ldx % 8 == 0:
         mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
     assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
-              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s())
+              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx)
     if with_mask:
         return y, mean, rstd, mask
     return y, mean, rstd
 
 
-def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None):
+def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None):
+    """`dx_out`: a channel slice of a wider gradient buffer (same strides as `x`) that dX is ADDED
+    into (DenseNet block-buffer gradient); otherwise dX is returned contiguous."""
     K, R, C = x.shape
+    x, ldx = _pix_stride(x)
+    assert x.stride(0) == R * ldx
+    dy = dy.contiguous()
     g_cs, rep = _client_view(gamma, K)
     # the kernels index γ by client k with stride g_cs: shared (Kw=1 → stride 0) or per client
     assert rep == 1 or gamma.shape[0] == 1, "bn_bwd supports per-client or fully shared γ"
-    dx = torch.empty_like(x)
-    dpre = torch.empty_like(x) if need_dpre else None
+    if dx_out is not None:
+        assert dx_out.shape == (K, R, C) and dx_out.stride() == x.stride() and dx_out.dtype == x.dtype
+        dx = dx_out
+    else:
+        assert ldx == C, "strided x needs a strided dx_out"
+        dx = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
+    dpre = torch.empty((K, R, C), dtype=x.dtype, device=x.device) if need_dpre else None
     ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     dg_cs = ggamma.stride(0) if ggamma is not None else 0
     assert dy.dtype == x.dtype == gamma.dtype
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
-              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s())
+              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx,
+              int(dx_out is not None))
     return dx, dpre
 
 

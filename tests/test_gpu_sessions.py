@@ -1,0 +1,124 @@
+"""GPU sessions at the reference's precision (fp32: `use_amp: false`) against the CPU oracle.
+
+The same config and seed run twice: on the MI355X through the native kernels (split-bf16 MFMA
+GEMMs with fp32 storage/accumulation, HIP-graph replayed steps, multi-stream cohorts) and on the
+CPU through the plain-PyTorch fp32 oracle (`ops.ref`). Global parameters after each round and
+the loss trajectory must agree — not just be finite (SURVEY §7.3 exit
+criterion: "accuracy trajectory matches the CPU oracle").
+"""
+
+import pytest
+import torch
+
+from distributed_learning_simulator_amd.config import load_config
+from distributed_learning_simulator_amd.ops import backend
+from distributed_learning_simulator_amd.parallel.comm import Comm
+from distributed_learning_simulator_amd.session import Session
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cfg_name, overrides, tmp_path, device):
+    group = cfg_name.split("/")[0]
+    args = ["--config-name", cfg_name] + [f"++{group}.{k}={v}" for k, v in overrides.items()]
+    args += [f"++{group}.save_dir={tmp_path}", f"++{group}.log_level=WARNING", f"++{group}.save_models=False"]
+    cfg = load_config(args)
+    sess = Session(cfg, comm=Comm(device=torch.device(device)))
+    if device == "cuda":
+        assert backend.using_hip(sess.trainer.buffers.theta) and sess.compute_dtype == torch.float32
+    res = sess.run()
+    return sess, res
+
+
+def _pair(cfg_name, overrides, tmp_path):
+    gpu = _run(cfg_name, overrides, tmp_path / "gpu", "cuda")
+    cpu = _run(cfg_name, overrides, tmp_path / "cpu", "cpu")
+    return gpu, cpu
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp(min=1e-30)).item()
+
+
+def _losses(res):
+    perf = res["performance"]
+    return [perf[k]["test_loss"] for k in sorted(perf)]
+
+
+def test_fedavg_lenet5_three_rounds_match_cpu(hip, tmp_path):
+    (gs, gr), (cs, cr) = _pair("fed_avg/mnist.yaml", {"round": 3, "epoch": 1, "worker_number": 4,
+                                                       "dataset_kwargs.scale": 0.03}, tmp_path)
+    gl, cl = _losses(gr), _losses(cr)
+    assert len(gl) == 3
+    assert max(abs(a - b) for a, b in zip(gl, cl)) < 1e-3, (gl, cl)
+    assert _rel(gs.server.global_parameter, cs.server.global_parameter) < 1e-3
+    assert gr["bytes_up"] == cr["bytes_up"]
+
+
+def test_fedavg_resnet18_matches_cpu(hip, tmp_path):
+    (gs, gr), (cs, cr) = _pair("fed_avg/cifar10.yaml", {"round": 2, "epoch": 1, "worker_number": 4,
+                                                         "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
+                                                         "learning_rate": 0.01}, tmp_path)
+    gl, cl = _losses(gr), _losses(cr)
+    assert max(abs(a - b) for a, b in zip(gl, cl)) < 1e-3, (gl, cl)
+    assert _rel(gs.server.global_parameter, cs.server.global_parameter) < 2e-3
+
+
+@pytest.mark.parametrize("cfg_name,overrides,tol", [
+    ("fed_dropout_avg/cifar10.yaml", {"model_name": "LeNet5", "worker_number": 4, "algorithm_kwargs.dropout_rate": 0.3}, 1e-3),
+    ("fed_paq/cifar10.yaml", {"model_name": "LeNet5", "worker_number": 4,
+                              "algorithm_kwargs.random_client_number": 4}, 2e-2),
+    ("fed_obd/cifar10.yaml", {"model_name": "LeNet5", "worker_number": 4, "algorithm_kwargs.random_client_number": 4,
+                              "algorithm_kwargs.second_phase_epoch": 1}, 2e-2),
+    ("fed_obd_sq/cifar100.yaml", {"model_name": "LeNet5", "worker_number": 4,
+                                  "algorithm_kwargs.random_client_number": 4,
+                                  "algorithm_kwargs.second_phase_epoch": 1}, 2e-2),
+])
+def test_methods_match_cpu(hip, tmp_path, cfg_name, overrides, tol):
+    """Round-1 global model of the compression / dropout methods: GPU == CPU oracle. Lossy
+    quantisers (FedPAQ stochastic, FedOBD NNADQ) may flip single steps where fp32 client models
+    differ in the last bits, hence the looser bound; the block selection must agree exactly."""
+    ov = {"round": 1, "epoch": 1, "dataset_kwargs.scale": 0.02, **overrides}
+    (gs, gr), (cs, cr) = _pair(cfg_name, ov, tmp_path)
+    g, c = gs.server.global_parameter, cs.server.global_parameter
+    assert torch.isfinite(g).all()
+    assert _rel(g, c) < tol, _rel(g, c)
+    if "fed_obd" not in cfg_name:
+        # most elements agree to fp32 noise (stochastic-rounding flips are rare); FedOBD's
+        # broadcast is NNADQ-quantised to a few bits, where a last-bit difference of a segment's
+        # min / max moves every level of that tensor: compared through rel error and loss instead
+        close = ((g.cpu() - c.cpu()).abs() <= 1e-4 * c.abs().max().cpu() + 1e-6).float().mean().item()
+        assert close > 0.97, close
+    assert abs(_losses(gr)[-1] - _losses(cr)[-1]) < 1e-2
+    assert gr["bytes_up"] == cr["bytes_up"]
+
+
+def test_sign_sgd_matches_cpu(hip, tmp_path):
+    (gs, _), (cs, _) = _pair("sign_sgd/cifar10.yaml", {"round": 1, "epoch": 1, "worker_number": 3,
+                                                        "model_name": "LeNet5", "dataset_kwargs.scale": 0.01,
+                                                        "learning_rate": 0.001}, tmp_path)
+    # votes are integers; a vote can only flip where a client's gradient sign is within fp32
+    # noise of 0 — essentially never
+    g, c = gs.server.global_parameter.cpu(), cs.server.global_parameter.cpu()
+    assert (g - c).abs().max().item() < 1e-4
+
+
+def test_gtg_shapley_matches_cpu(hip, tmp_path):
+    (gs, gr), (cs, cr) = _pair("gtg_sv/mnist.yaml", {"round": 1, "epoch": 1, "worker_number": 3,
+                                                      "dataset_kwargs.scale": 0.03}, tmp_path)
+    assert gr["sv"].keys() == cr["sv"].keys()
+    for r in cr["sv"]:
+        for w, v in cr["sv"][r].items():
+            assert abs(gr["sv"][r][w] - v) < 2e-2, (gr["sv"], cr["sv"])
+    assert _rel(gs.server.global_parameter, cs.server.global_parameter) < 1e-3
+
+
+def test_densenet40_session_matches_cpu(hip, tmp_path):
+    """DenseNet-40 (the model of 29 of the reference's 54 configs) end to end on the GPU at fp32."""
+    (gs, gr), (cs, cr) = _pair("fed_avg/cifar10.yaml", {"round": 1, "epoch": 1, "worker_number": 2,
+                                                        "model_name": "densenet40", "dataset_kwargs.scale": 0.004,
+                                                        "learning_rate": 0.01}, tmp_path)
+    gl, cl = _losses(gr), _losses(cr)
+    assert abs(gl[0] - cl[0]) < 1e-3, (gl, cl)
+    assert _rel(gs.server.global_parameter, cs.server.global_parameter) < 2e-3

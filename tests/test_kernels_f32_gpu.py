@@ -87,16 +87,16 @@ def test_conv_f32_every_variant(hip, case):
     for v in range(hip._C.conv_nt_f32_num_variants()):
         y = torch.empty_like(dy)
         hip._C.conv_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, B * H * W * Ci, M * Co, w.stride(0), 0, B, H, W,
-                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream)
+                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0)
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
-                          W, Ci, k, k, s, p, v, 1, stream)
+                          W, Ci, k, k, s, p, v, 1, stream, 0, 0)
         _close(dx, dx_ref)
     for v in range(hip._C.conv_tn_f32_num_variants()):
         gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
         hip._C.conv_tn(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M * Co, B * H * W * Ci, gw.stride(0), B, H, W, Ci,
-                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream)
+                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream, 0, 0)
         _close(gw, dw_ref)
 
 
@@ -230,3 +230,36 @@ def test_mix_rows_f32_and_gather(hip):
     src = _f(100, 4, 4, 4)
     idx = torch.randint(0, 100, (3, 5), device=DEV)
     assert torch.equal(hip.gather_rows(src, idx), src[idx.reshape(-1)])
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 6e-2)])
+def test_dense_block_strided_kernels_match_cpu(hip, dtype, tol):
+    """DenseNet block on the GPU: BN reads channel prefixes of the block buffer in place, convs
+    write their 12 new channels through the epilogue row stride, the backward accumulates into
+    channel slices of dF — against the CPU autograd-verified path (tests/test_models.py)."""
+    from distributed_learning_simulator_amd.data.datasets import get_spec
+    from distributed_learning_simulator_amd.engine.params import BoundParams
+    from distributed_learning_simulator_amd.models.layers import RunCtx
+    from distributed_learning_simulator_amd.models.zoo import build_model
+    from distributed_learning_simulator_amd.ops import functional as Fn
+
+    model = build_model("densenet10", get_spec("CIFAR10"))
+    layout = model.layout
+    K = 3
+    theta = torch.stack([layout.init_flat(torch.Generator().manual_seed(s)) for s in range(K)])
+    x = torch.randn(K, 6, 32, 32, 8)
+    x[..., 3:] = 0
+    y = torch.randint(0, 10, (K, 6))
+    valid = torch.tensor([6, 4, 1], dtype=torch.int32)
+    out = {}
+    for dev in ("cpu", "cuda"):
+        th = theta.to(dev)
+        comp = th if (dev == "cpu" or dtype == torch.float32) else th.to(dtype)
+        grad = torch.zeros_like(th)
+        ctx = RunCtx(BoundParams(layout, comp, grad), valid.to(dev))
+        xi = x.to(dev, torch.float32 if dev == "cpu" else dtype)
+        loss, _ = Fn.cross_entropy(model.forward(xi, ctx), y.to(dev), ctx.valid)
+        loss.sum().backward()
+        out[dev] = (loss.detach().cpu(), grad.cpu())
+    _close(out["cuda"][0], out["cpu"][0], tol)
+    _close(out["cuda"][1], out["cpu"][1], tol * 5)

@@ -30,11 +30,11 @@ def test_transformer_layer_count():
     assert m.num_params == 20000 * 100 + 2 * 452548 + 202
 
 
-def _run(model, x, labels, K, theta):
+def _run(model, x, labels, K, theta, valid=None):
     layout = model.layout
     grad = torch.zeros_like(theta)
     params = BoundParams(layout, theta, grad)
-    ctx = RunCtx(params, torch.full((K,), labels.shape[1], dtype=torch.int32))
+    ctx = RunCtx(params, valid if valid is not None else torch.full((K,), labels.shape[1], dtype=torch.int32))
     logits = model.forward(x, ctx)
     loss, correct = Fn.cross_entropy(logits, labels, ctx.valid)
     loss.sum().backward()
@@ -165,3 +165,51 @@ def test_transformer_epilogue_fusions_match_unfused(monkeypatch):
     ref_ = _run(model, (tokens, lengths), y, 1, theta.clone())
     torch.testing.assert_close(fused[0], ref_[0])
     torch.testing.assert_close(fused[1], ref_[1], rtol=1e-4, atol=1e-6)
+
+
+def test_densenet_fused_block_matches_autograd_concat():
+    """The fused dense block (one preallocated buffer, in-place channel slices, reverse-order
+    gradient accumulation) == plain torch autograd of BN-ReLU-Conv + torch.cat (the reference's
+    DenseNet). Depth 10 = 2 layers per block, 2 clients, ragged batch."""
+    import torch.nn.functional as F
+
+    spec = get_spec("CIFAR10")
+    model = build_model("densenet10", spec)
+    layout = model.layout
+    K = 2
+    theta = torch.stack([layout.init_flat(torch.Generator().manual_seed(s)) for s in (5, 6)])
+    # non-trivial γ/β
+    for e in layout.entries:
+        if e.name.endswith("norm.weight") or e.name.endswith("norm.bias"):
+            theta[:, e.offset : e.offset + e.numel] += 0.3 * torch.randn(K, e.numel)
+    x = torch.randn(K, 5, 32, 32, 3)
+    y = torch.randint(0, 10, (K, 5))
+    valid = torch.tensor([5, 3], dtype=torch.int32)
+    loss, grad = _run(model, x, y, K, theta.clone(), valid=valid)
+    for k in range(K):
+        n = int(valid[k])
+        t = {kk: v.clone().requires_grad_() for kk, v in layout.unflatten(theta[k]).items()}
+
+        def bn(h, name, relu=True):
+            m = h.mean(dim=(0, 2, 3), keepdim=True)
+            v = ((h - m) ** 2).mean(dim=(0, 2, 3), keepdim=True)
+            o = (h - m) / torch.sqrt(v + 1e-5) * t[name + ".weight"][None, :, None, None] + t[name + ".bias"][None, :, None, None]
+            return F.relu(o) if relu else o
+
+        def conv(h, name, pad):
+            return F.conv2d(h, t[name + ".weight"].permute(0, 3, 1, 2), padding=pad)
+
+        h = conv(x[k, :n].permute(0, 3, 1, 2), "conv1", 1)
+        for b in (1, 2, 3):
+            for i in range(2):
+                h = torch.cat([h, conv(bn(h, f"dense{b}.{i}.norm"), f"dense{b}.{i}.conv", 1)], 1)
+            if b < 3:
+                h = F.avg_pool2d(conv(bn(h, f"trans{b}.norm"), f"trans{b}.conv", 0), 2)
+        h = bn(h, "norm").mean(dim=(2, 3))
+        out = F.linear(h, t["fc.weight"], t["fc.bias"])
+        ref_loss = F.cross_entropy(out, y[k, :n])
+        ref_loss.backward()
+        assert abs(ref_loss.item() - loss[k].item()) < 1e-4
+        got = layout.unflatten(grad[k])
+        for kk, v in t.items():
+            torch.testing.assert_close(got[kk], v.grad, rtol=1e-3, atol=1e-5, msg=kk)
