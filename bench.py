@@ -5,11 +5,15 @@ with cosine schedule).
 
 The other BASELINE.json configs are selectable with `--workload` (same JSON contract):
   fedavg_resnet18     (default) config 2 above
-  fedobd_transformer  FedOBD, 100 clients, TransformerClassificationModel on imdb-shaped tokens
-                      (`conf/large_scale/fed_obd/imdb.yaml`: block dropout 0.3 + NNADQ 1e-4)
-  signsgd_resnet50    sign-SGD, 128 clients, ResNet-50, ImageNet-shaped (batch 128; one round =
-                      one local epoch of 1-bit majority-vote steps over a scaled ImageNet shard)
-  gtg_resnet18        GTG-Shapley, 32 clients, ResNet-18, CIFAR-10-shaped
+  fedavg_densenet40   the reference's own `conf/large_scale/fed_avg/cifar10.yaml` (DenseNet-40)
+  fedobd_transformer  config 3: FedOBD, 100 clients (50 per round), Transformer-base (d 512, 8 heads,
+                      6 layers, FFN 2048), AG-News-shaped; stage 1 timed, stage 2 reported apart
+  fedobd_imdb         `conf/large_scale/fed_obd/imdb.yaml` verbatim (d 100, 2 layers, L 300,
+                      second_phase_epoch 10): block dropout 0.3 + NNADQ 1e-4
+  signsgd_resnet50    config 4: sign-SGD, 128 clients, ResNet-50, ImageNet-shaped (batch 128; one
+                      round = one local epoch of 1-bit majority-vote steps over a scaled ImageNet shard)
+  gtg_resnet18        config 5: GTG-Shapley, 32 clients, ResNet-18, 5 local epochs, full test split
+  fedavg_mlp_mnist    config 1: FedAvg, 4 clients, MLP, MNIST-shaped (the CPU plumbing check)
 
 One step = one full FL round: every selected client trains its local epochs (lock-step cohort
 on the rank's GPU), uploads are aggregated (fused weighted reduction + RCCL all-reduce across
@@ -38,8 +42,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="fedavg_resnet18",
-                    choices=["fedavg_resnet18", "fedobd_transformer", "signsgd_resnet50", "gtg_resnet18",
-                             "fedavg_mlp_mnist"])
+                    choices=["fedavg_resnet18", "fedavg_densenet40", "fedobd_transformer", "fedobd_imdb",
+                             "signsgd_resnet50", "gtg_resnet18", "fedavg_mlp_mnist"])
     ap.add_argument("--algo", default="fed_avg", choices=["fed_avg", "fed_obd"])
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--clients", type=int, default=100)
@@ -47,6 +51,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--cohort", type=int, default=0)
+    ap.add_argument("--no-stage2", action="store_true", help="FedOBD workloads: skip timing the second phase")
     ap.add_argument("--amp", action="store_true",
                     help="bf16 fast mode (use_amp: true). Default: fp32, the reference's precision "
                          "(conf/global.yaml use_amp: false) — split-bf16 MFMA GEMMs, fp32 storage/accumulate")
@@ -98,6 +103,12 @@ def main() -> None:
     init = server._before_start()
     theta, _ = server.send_result(init)
 
+    def progress(tag):
+        # one stderr line per round keeps long runs visibly alive (gpurun's silence watchdog)
+        if comm.rank == 0:
+            row = sess.metrics[-1] if sess.metrics else {}
+            print(f"[bench] {tag} round {row.get('round')} {row.get('wall_s', 0):.2f}s", file=sys.stderr, flush=True)
+
     def barrier_sync():
         if comm.world > 1:
             comm.barrier()
@@ -106,17 +117,37 @@ def main() -> None:
 
     for _ in range(args.warmup):
         theta = sess.run_one_round(theta)
+        progress("warmup")
     barrier_sync()
     t0 = time.perf_counter()
     m0 = len(sess.metrics)
     for _ in range(args.steps):
         theta = sess.run_one_round(theta)
+        progress("timed")
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    stage2 = None
+    if wl.get("stage2") and not args.no_stage2:
+        # FedOBD: the timed rounds above are stage 1; the whole second phase (all clients,
+        # `second_phase_epoch` epochs, aggregation after every epoch) is timed on its own
+        m1 = len(sess.metrics)
+        t1 = time.perf_counter()
+        while not server._stopped():
+            theta = sess.run_one_round(theta)
+            progress("stage2")
+        barrier_sync()
+        stage2 = {"seconds": time.perf_counter() - t1, "epochs": len(sess.metrics) - m1,
+                  "clients": cfg.worker_number,
+                  "comm_bytes": sum(r["comm_bytes_total"] for r in sess.metrics[m1:]),
+                  "test_accuracy": sess.metrics[-1].get("test_accuracy") if len(sess.metrics) > m1 else None}
     if comm.world > 1 and not emulated:
         t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        if stage2 is not None:
+            t[0] = stage2["seconds"]
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            stage2["seconds"] = float(t.item())
     rows = sess.metrics[m0:]
     bytes_per_round = sum(r["comm_bytes_total"] for r in rows) / max(len(rows), 1)
     acc = rows[-1].get("test_accuracy") if rows else None
@@ -150,9 +181,11 @@ def main() -> None:
                 "local_epochs": cfg.epoch, "global_batch": cfg.batch_size * cfg.worker_number,
                 "per_client_batch": cfg.batch_size, "seq_len": wl.get("seq_len"),
                 "parallelism": f"emulated-rank0-of-{comm.world}" if emulated else f"client-dp{comm.world}",
-                "backend": args.backend, "workload": args.workload,
+                "backend": args.backend, "workload": args.workload, **wl.get("config_extra", {}),
             },
         }
+        if stage2 is not None:
+            out["stage2"] = stage2
         print(json.dumps(out), flush=True)
 
 
@@ -187,18 +220,42 @@ def workload_config(args, rounds: int) -> dict:
         metric = f"FL rounds/sec ({algo}, {args.clients} clients, {model}, CIFAR-10-shaped)"
         data = "synthetic (CIFAR-10-shaped, random_label_iid non-IID shards, random-init weights)"
         return {"config": {**cfg, **common}, "metric": metric, "data": data, "samples_per_round": shard_samples}
-    if args.workload == "fedobd_transformer":
-        cfg = {"distributed_algorithm": "fed_obd", "dataset_name": "imdb", "model_name": "TransformerClassificationModel",
-               "dataset_kwargs": {"max_len": 300}, "model_kwargs": {"d_model": 100, "nhead": 5, "num_encoder_layer": 2,
-                                                                     "max_len": 300},
-               "worker_number": 100, "epoch": 5, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.01,
-               "learning_rate_scheduler_name": "CosineAnnealingLR", "dataset_sampling": "random_label_iid",
-               "dataset_sampling_kwargs": {"sampled_class_number": 1},
-               "algorithm_kwargs": {"second_phase_epoch": 1, "dropout_rate": 0.3, "random_client_number": 100},
-               "endpoint_kwargs": {"server": {"weight": 0.0001}, "worker": {"weight": 0.0001}}}
-        return {"config": {**cfg, **common}, "metric": "FL rounds/sec (FedOBD, 100 clients, Transformer, imdb-shaped)",
-                "data": "synthetic (imdb-shaped token sequences, max_len 300, non-IID shards, random-init weights)",
-                "samples_per_round": shard_samples, "seq_len": 300}
+    if args.workload == "fedavg_densenet40":
+        # the reference's own large-scale FedAvg config, verbatim (conf/large_scale/fed_avg/cifar10.yaml):
+        # DenseNet-40, 100 clients, 5 local epochs, batch 64, SGD lr 0.1 cosine, iid sampling
+        # (⇒ keep-best-by-validation uploads, reference aggregation_worker.py:28-29)
+        cfg = {"distributed_algorithm": "fed_avg", "dataset_name": "CIFAR10", "model_name": "densenet40",
+               "worker_number": args.clients, "epoch": args.epoch, "batch_size": args.batch, "optimizer_name": "SGD",
+               "learning_rate": 0.1, "learning_rate_scheduler_name": "CosineAnnealingLR"}
+        return {"config": {**cfg, **common}, "samples_per_round": shard_samples,
+                "metric": f"FL rounds/sec (FedAvg, {args.clients} clients, DenseNet-40, CIFAR-10-shaped)",
+                "data": "synthetic (CIFAR-10-shaped, iid shards, random-init weights)"}
+    if args.workload in ("fedobd_transformer", "fedobd_imdb"):
+        # stage-1 rounds are the timed steps; stage 2 (second_phase_epoch epochs over all clients)
+        # is run to the end afterwards and reported under "stage2"
+        obd = {"distributed_algorithm": "fed_obd", "worker_number": 100, "epoch": 5, "batch_size": 64,
+               "optimizer_name": "SGD", "learning_rate": 0.01, "learning_rate_scheduler_name": "CosineAnnealingLR",
+               "algorithm_kwargs": {"second_phase_epoch": 10, "dropout_rate": 0.3, "random_client_number": 50},
+               "endpoint_kwargs": {"server": {"weight": 0.0001}, "worker": {"weight": 0.0001}},
+               **common, "round": rounds}
+        if args.workload == "fedobd_imdb":
+            # the reference's conf/large_scale/fed_obd/imdb.yaml verbatim (d_model 100, 5 heads, 2 layers)
+            cfg = {**obd, "dataset_name": "imdb", "model_name": "TransformerClassificationModel",
+                   "dataset_kwargs": {"max_len": 300},
+                   "model_kwargs": {"d_model": 100, "nhead": 5, "num_encoder_layer": 2, "max_len": 300}}
+            return {"config": cfg, "stage2": True, "samples_per_round": shard_samples, "seq_len": 300,
+                    "metric": "FL rounds/sec (FedOBD stage 1, 100 clients / 50 per round, Transformer, imdb-shaped)",
+                    "data": "synthetic (imdb-shaped token sequences, max_len 300, iid shards, random-init weights)"}
+        # BASELINE.json config 3: Transformer-base (d_model 512, 8 heads, 6 layers, FFN 2048) on
+        # AG-News-shaped data (4 classes, max_len 128), the reference's FedOBD hyper-parameters
+        cfg = {**obd, "dataset_name": "AG_NEWS", "model_name": "TransformerClassificationModel",
+               "dataset_kwargs": {"max_len": 128},
+               "model_kwargs": {"d_model": 512, "nhead": 8, "num_encoder_layer": 6, "dim_feedforward": 2048,
+                                "max_len": 128}}
+        return {"config": cfg, "stage2": True, "samples_per_round": shard_samples, "seq_len": 128,
+                "config_extra": {"d_model": 512, "nhead": 8, "layers": 6, "ffn": 2048},
+                "metric": "FL rounds/sec (FedOBD stage 1, 100 clients / 50 per round, Transformer-base, AG-News-shaped)",
+                "data": "synthetic (AG-News-shaped token sequences, max_len 128, iid shards, random-init weights)"}
     if args.workload == "signsgd_resnet50":
         cfg = {"distributed_algorithm": "sign_SGD", "dataset_name": "ImageNet", "model_name": "Resnet50",
                "dataset_kwargs": {"scale": 0.01}, "worker_number": 128, "epoch": 1, "batch_size": 128,
@@ -206,14 +263,15 @@ def workload_config(args, rounds: int) -> dict:
         return {"config": {**cfg, **common}, "metric": "FL rounds/sec (sign-SGD, 128 clients, ResNet-50, ImageNet-shaped)",
                 "data": "synthetic (ImageNet-shaped 224x224, 1% scale shards, random-init weights)",
                 "samples_per_round": shard_samples}
-    # utility v(S) = test accuracy of the subset model; GTG evaluates thousands of subsets per
-    # round, so the utility set is a 1,000-image CIFAR-shaped test split (all batched on device)
+    # utility v(S) = test accuracy of the subset model on the FULL test split (reference
+    # shapley_value_algorithm.py:67-76); 5 local epochs as conf/gtg_sv/cifar10.yaml
     cfg = {"distributed_algorithm": "GTG_shapley_value", "dataset_name": "CIFAR10", "model_name": "ResNet18",
-           "dataset_kwargs": {"n_test": 1000}, "worker_number": 32, "epoch": 1, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.1,
+           "worker_number": 32, "epoch": args.epoch, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.1,
+           "learning_rate_scheduler_name": "CosineAnnealingLR",
            "dataset_sampling": "random_label_iid", "dataset_sampling_kwargs": {"sampled_class_number": 5}}
     return {"config": {**cfg, **common}, "metric": "FL rounds/sec (GTG-Shapley, 32 clients, ResNet-18, CIFAR-10-shaped)",
-            "data": "synthetic (CIFAR-10-shaped, 1k-image utility/test split, random_label_iid non-IID shards, "
-                    "random-init weights)",
+            "data": "synthetic (CIFAR-10-shaped, full 10k test split as the utility set, random_label_iid non-IID "
+                    "shards, random-init weights)",
             "samples_per_round": shard_samples}
 
 
