@@ -15,6 +15,8 @@
 //   dq  : δ_i = do_i·o_i;  dq_i = Σ_j p_ij (do_i·v_j − δ_i) k_j / √DH       (writes δ)
 //   dkv : dv_j = Σ_i p_ij do_i;  dk_j = Σ_i p_ij (do_i·v_j − δ_i) q_i / √DH
 #include "common.h"
+
+#include <stdlib.h>
 #include "dls.h"
 
 namespace {
@@ -259,7 +261,19 @@ static int attn_rows(int L) {
   return ((cdiv(L, nblk) + 63) / 64) * 64;
 }
 
+// head dims 32 / 64 run on the MFMA kernels (attention_mfma.hip) unless DLS_ATTN_MFMA=0; the
+// VALU kernels below keep the small heads (the imdb model's dh = 20, 8, 16), where a 32-wide
+// MFMA operand would be mostly padding
+static bool use_mfma(int L, int DH) {
+  static const int mode = [] {
+    const char* e = getenv("DLS_ATTN_MFMA");
+    return e ? atoi(e) : 1;
+  }();
+  return mode != 0 && attn_mfma_supported(L, DH);
+}
+
 bool attn_supported(int L, int DH) {
+  if (attn_mfma_supported(L, DH)) return true;
   if (!(DH == 8 || DH == 16 || DH == 20 || DH == 32 || DH == 64)) return false;
   return (2L * L * DH + 2L * L) * 4 <= 160L * 1024;
 }
@@ -277,7 +291,8 @@ bool attn_supported(int L, int DH) {
 
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
               int L, int DH, int f32, hipStream_t s) {
-  if (!attn_supported(L, DH)) return false;
+  if (use_mfma(L, DH)) return attn_fwd_mfma(q, k, v, key_valid, o, lse, KBH, H, L, DH, f32, s);
+  if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));
   const size_t sh = (size_t)2 * L * DH * sizeof(float);
@@ -291,7 +306,8 @@ bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid,
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
               hipStream_t s) {
-  if (!attn_supported(L, DH)) return false;
+  if (use_mfma(L, DH)) return attn_bwd_mfma(dout, q, k, v, o, lse, key_valid, dq, dk, dv, delta, KBH, H, L, DH, f32, s);
+  if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));
   const float scale = 1.0f / sqrtf((float)DH);

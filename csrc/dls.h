@@ -185,6 +185,13 @@ void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long
                    hipStream_t s);
 // --------------------------------------------------------------- attention / graph
 bool attn_supported(int L, int DH);
+// MFMA flash attention (attention_mfma.hip), head dim 32 / 64; attn_fwd / attn_bwd route to it
+bool attn_mfma_supported(int L, int DH);
+bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
+                   int H, int L, int DH, int f32, hipStream_t s);
+bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
+                   const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
+                   int f32, hipStream_t s);
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
               int L, int DH, int f32, hipStream_t s);
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
