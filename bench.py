@@ -75,8 +75,13 @@ def main() -> None:
     import torch.distributed as dist
 
     from distributed_learning_simulator_amd.config import config_from_dict
-    from distributed_learning_simulator_amd.parallel.comm import init_distributed
+    from distributed_learning_simulator_amd.parallel.comm import init_distributed, shutdown
     from distributed_learning_simulator_amd.session import Session
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1 and not torch.cuda.is_available():
+        # CPU ranks share the host: split the intra-op threads instead of oversubscribing
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // world_env))
 
     if torch.cuda.is_available() and args.backend == "hip":
         from distributed_learning_simulator_amd.ops import build
@@ -187,6 +192,9 @@ def main() -> None:
         if stage2 is not None:
             out["stage2"] = stage2
         print(json.dumps(out), flush=True)
+    # tear the process group down on every rank (an exiting rank with a live gloo/RCCL group
+    # aborts in the communicator's destructor)
+    shutdown()
 
 
 def workload_config(args, rounds: int) -> dict:

@@ -272,6 +272,8 @@ static bool use_mfma(int L, int DH) {
   return mode != 0 && attn_mfma_supported(L, DH);
 }
 
+bool attn_packed_supported(int L, int DH) { return use_mfma(L, DH); }
+
 bool attn_supported(int L, int DH) {
   if (attn_mfma_supported(L, DH)) return true;
   if (!(DH == 8 || DH == 16 || DH == 20 || DH == 32 || DH == 64)) return false;
@@ -290,8 +292,9 @@ bool attn_supported(int L, int DH) {
 #define MP(p) static_cast<TT*>(p)
 
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
-              int L, int DH, int f32, hipStream_t s) {
-  if (use_mfma(L, DH)) return attn_fwd_mfma(q, k, v, key_valid, o, lse, KBH, H, L, DH, f32, s);
+              int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo) {
+  if (use_mfma(L, DH)) return attn_fwd_mfma(q, k, v, key_valid, o, lse, KBH, H, L, DH, f32, s, ldqkv, ldo);
+  if (ldqkv || ldo) return false;  // packed layouts: MFMA kernels only
   if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));
@@ -305,8 +308,10 @@ bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid,
 
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
-              hipStream_t s) {
-  if (use_mfma(L, DH)) return attn_bwd_mfma(dout, q, k, v, o, lse, key_valid, dq, dk, dv, delta, KBH, H, L, DH, f32, s);
+              hipStream_t s, int ldqkv, int ldo) {
+  if (use_mfma(L, DH))
+    return attn_bwd_mfma(dout, q, k, v, o, lse, key_valid, dq, dk, dv, delta, KBH, H, L, DH, f32, s, ldqkv, ldo);
+  if (ldqkv || ldo) return false;
   if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));

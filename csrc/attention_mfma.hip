@@ -98,15 +98,27 @@ __device__ __forceinline__ Frag<T> frag_km(const Img<T>& m, int k0, int r0) {
   return f;
 }
 
-// stage rows [r0, r0+RB) of a [L][DH] matrix into an image (zero rows past L), all threads
+// Where one head's [L][DH] matrix lives: rows at stride ld, head base = (head / H)·s_kb +
+// (head % H)·s_h. Contiguous [KBH][L][DH]: (H·L·DH, L·DH, DH). Packed projection output
+// [KB][L][n·D] read in place (q/k/v are column blocks of the QKV GEMM's rows, o is the out
+// projection's input rows): (L·ld, DH, ld) — no permute / contiguous copies around attention.
+struct HeadLayout {
+  long s_kb, s_h;
+  int ld;
+};
+__device__ __forceinline__ long hbase(const HeadLayout& hl, long head, int H) {
+  return (head / H) * hl.s_kb + (head % H) * hl.s_h;
+}
+
+// stage rows [r0, r0+RB) of a head matrix (row stride ld) into an image (zero rows past L)
 template <typename T, int DH>
-__device__ __forceinline__ void stage(const T* __restrict__ src, int r0, int L, const Img<T>& m) {
+__device__ __forceinline__ void stage(const T* __restrict__ src, int ld, int r0, int L, const Img<T>& m) {
   for (int c = threadIdx.x; c < RB * DH / 8; c += WG) {
     const int r = c / (DH / 8), d = (c % (DH / 8)) * 8;
     const bool ok = r0 + r < L;
     float x[8];
     if (ok) {
-      load_vec<8>(src + (long)(r0 + r) * DH + d, x);
+      load_vec<8>(src + (long)(r0 + r) * ld + d, x);
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = 0.f;
@@ -172,14 +184,14 @@ template <typename T, int DH>
 __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__ q, const T* __restrict__ k,
                                                            const T* __restrict__ v, const int* __restrict__ key_valid,
                                                            T* __restrict__ o, float* __restrict__ lse, int L, int H,
-                                                           float scale) {
+                                                           float scale, HeadLayout lq, HeadLayout lo) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
   constexpr int LDK = pad_ld(DH), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NP * RB * LDK], Vs[NP * RB * LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Ps[4][NP * RB * LDP];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 31;
   const long head = blockIdx.x;
-  const long base = head * L * DH;
+  const long base = hbase(lq, head, H), obase = hbase(lo, head, H);
   const int nk = key_valid ? min(key_valid[head / H], L) : L;
   const int qrow = blockIdx.y * (4 * RB) + wid * RB + c;
   const bool qok = qrow < L;
@@ -187,14 +199,14 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
 
   Frag<T> qf[DH / 16];
 #pragma unroll
-  for (int ks = 0; ks < DH / 16; ++ks) qf[ks] = frag_global<T>(q + base + (long)qrow * DH + ks * 16 + 8 * (lane >> 5), qok);
+  for (int ks = 0; ks < DH / 16; ++ks) qf[ks] = frag_global<T>(q + base + (long)qrow * lq.ld + ks * 16 + 8 * (lane >> 5), qok);
   f32x16 ot[DH / 32];
 #pragma unroll
   for (int t = 0; t < DH / 32; ++t) ot[t] = f32x16{};
   float m = -INFINITY, l = 0.f;
   for (int k0 = 0; k0 < nk; k0 += RB) {
-    stage<T, DH>(k + base, k0, nk, KI);
-    stage<T, DH>(v + base, k0, nk, VI);
+    stage<T, DH>(k + base, lq.ld, k0, nk, KI);
+    stage<T, DH>(v + base, lq.ld, k0, nk, VI);
     __syncthreads();
     f32x16 st = f32x16{};  // Sᵀ[key][query]
 #pragma unroll
@@ -232,7 +244,7 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
   if (qok) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t) store_rowcols<T>(o + base + (long)qrow * DH, t * 32, ot[t], inv);
+    for (int t = 0; t < DH / 32; ++t) store_rowcols<T>(o + obase + (long)qrow * lo.ld, t * 32, ot[t], inv);
     if ((lane >> 5) == 0) lse[head * L + qrow] = l > 0.f ? m + __logf(l) : 0.f;
   }
 }
@@ -243,14 +255,15 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
                                                               const T* __restrict__ k, const T* __restrict__ v,
                                                               const T* __restrict__ o, const float* __restrict__ lse,
                                                               const int* __restrict__ key_valid, T* __restrict__ dq,
-                                                              float* __restrict__ delta, int L, int H, float scale) {
+                                                              float* __restrict__ delta, int L, int H, float scale,
+                                                              HeadLayout lq, HeadLayout lo) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
   constexpr int LDK = pad_ld(DH), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NP * RB * LDK], Vs[NP * RB * LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Ps[4][NP * RB * LDP];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   const long head = blockIdx.x;
-  const long base = head * L * DH;
+  const long base = hbase(lq, head, H), obase = hbase(lo, head, H);
   const int nk = key_valid ? min(key_valid[head / H], L) : L;
   const int qrow = blockIdx.y * (4 * RB) + wid * RB + c;
   const bool qok = qrow < L;
@@ -259,14 +272,14 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
   Frag<T> qf[DH / 16], df[DH / 16];
 #pragma unroll
   for (int ks = 0; ks < DH / 16; ++ks) {
-    qf[ks] = frag_global<T>(q + base + (long)qrow * DH + ks * 16 + 8 * h, qok);
-    df[ks] = frag_global<T>(dout + base + (long)qrow * DH + ks * 16 + 8 * h, qok);
+    qf[ks] = frag_global<T>(q + base + (long)qrow * lq.ld + ks * 16 + 8 * h, qok);
+    df[ks] = frag_global<T>(dout + obase + (long)qrow * lo.ld + ks * 16 + 8 * h, qok);
   }
   // δ = dO·O of this lane's query (each half-wave sums half of the head dim)
   float dl = 0.f;
   if (qok) {
-    const T* dr = dout + base + (long)qrow * DH + h * (DH / 2);
-    const T* orow = o + base + (long)qrow * DH + h * (DH / 2);
+    const T* dr = dout + obase + (long)qrow * lo.ld + h * (DH / 2);
+    const T* orow = o + obase + (long)qrow * lo.ld + h * (DH / 2);
 #pragma unroll
     for (int d = 0; d < DH / 2; d += 8) {
       float a[8], b[8];
@@ -278,13 +291,13 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
   }
   dl += __shfl_xor(dl, 32, 64);
   if (qok && h == 0) delta[head * L + qrow] = dl;
-  const float lq = qok ? lse[head * L + qrow] : 0.f;
+  const float lse_q = qok ? lse[head * L + qrow] : 0.f;
   f32x16 dqt[DH / 32];
 #pragma unroll
   for (int t = 0; t < DH / 32; ++t) dqt[t] = f32x16{};
   for (int k0 = 0; k0 < nk; k0 += RB) {
-    stage<T, DH>(k + base, k0, nk, KI);
-    stage<T, DH>(v + base, k0, nk, VI);
+    stage<T, DH>(k + base, lq.ld, k0, nk, KI);
+    stage<T, DH>(v + base, lq.ld, k0, nk, VI);
     __syncthreads();
     f32x16 st = f32x16{}, dpt = f32x16{};
 #pragma unroll
@@ -295,7 +308,7 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const bool ok = qok && (k0 + crow(e) < nk);
-      const float p = ok ? __expf(st[e] * scale - lq) : 0.f;
+      const float p = ok ? __expf(st[e] * scale - lse_q) : 0.f;
       st[e] = p * (dpt[e] - dl) * scale;  // dSᵀ
     }
     put_colrows<T>(PI, st);  // dS[query][key]
@@ -308,7 +321,7 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
   }
   if (qok) {
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t) store_rowcols<T>(dq + base + (long)qrow * DH, t * 32, dqt[t], 1.f);
+    for (int t = 0; t < DH / 32; ++t) store_rowcols<T>(dq + base + (long)qrow * lq.ld, t * 32, dqt[t], 1.f);
   }
 }
 
@@ -319,7 +332,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
                                                                const int* __restrict__ key_valid, T* __restrict__ dk,
-                                                               T* __restrict__ dv, int L, int H, float scale) {
+                                                               T* __restrict__ dv, int L, int H, float scale,
+                                                               HeadLayout lq, HeadLayout lo) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
   constexpr int LDK = pad_ld(DH), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NP * RB * LDK], Os[NP * RB * LDK];
@@ -327,7 +341,7 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   __shared__ __attribute__((aligned(16))) float Lq[RB], Dq[RB];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
   const long head = blockIdx.x;
-  const long base = head * L * DH;
+  const long base = hbase(lq, head, H), obase = hbase(lo, head, H);
   const int nk = key_valid ? min(key_valid[head / H], L) : L;
   const int key = blockIdx.y * (4 * RB) + wid * RB + c;
   const bool kok = key < nk;
@@ -337,8 +351,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   Frag<T> kf[DH / 16], vf[DH / 16];
 #pragma unroll
   for (int ks = 0; ks < DH / 16; ++ks) {
-    kf[ks] = frag_global<T>(k + base + (long)key * DH + ks * 16 + 8 * h, kok);
-    vf[ks] = frag_global<T>(v + base + (long)key * DH + ks * 16 + 8 * h, kok);
+    kf[ks] = frag_global<T>(k + base + (long)key * lq.ld + ks * 16 + 8 * h, kok);
+    vf[ks] = frag_global<T>(v + base + (long)key * lq.ld + ks * 16 + 8 * h, kok);
   }
   f32x16 dkt[DH / 32], dvt[DH / 32];
 #pragma unroll
@@ -347,8 +361,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   // every wave must reach every barrier)
   const bool any = blockIdx.y * (4 * RB) < nk;
   for (int q0 = 0; any && q0 < L; q0 += RB) {
-    stage<T, DH>(q + base, q0, L, QI);
-    stage<T, DH>(dout + base, q0, L, OI);
+    stage<T, DH>(q + base, lq.ld, q0, L, QI);
+    stage<T, DH>(dout + obase, lo.ld, q0, L, OI);
     if (threadIdx.x < RB) {
       const bool ok = q0 + threadIdx.x < L;
       Lq[threadIdx.x] = ok ? lse[head * L + q0 + threadIdx.x] : 0.f;
@@ -385,8 +399,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   if (key < L) {
 #pragma unroll
     for (int t = 0; t < DH / 32; ++t) {
-      store_rowcols<T>(dk + base + (long)key * DH, t * 32, dkt[t], 1.f);
-      store_rowcols<T>(dv + base + (long)key * DH, t * 32, dvt[t], 1.f);
+      store_rowcols<T>(dk + base + (long)key * lq.ld, t * 32, dkt[t], 1.f);
+      store_rowcols<T>(dv + base + (long)key * lq.ld, t * 32, dvt[t], 1.f);
     }
   }
 }
@@ -419,27 +433,35 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
 
 bool attn_mfma_supported(int L, int DH) { return (DH == 32 || DH == 64) && L >= 1; }
 
+// ldqkv / ldo = 0: contiguous [KBH][L][DH]; otherwise packed [KB][L][ld] rows (module docs)
+static HeadLayout head_layout(int ld, int H, int L, int DH) {
+  if (ld == 0) return HeadLayout{(long)H * L * DH, (long)L * DH, DH};
+  return HeadLayout{(long)L * ld, (long)DH, ld};
+}
+
 bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
-                   int H, int L, int DH, int f32, hipStream_t s) {
+                   int H, int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo) {
   if (!attn_mfma_supported(L, DH)) return false;
   const dim3 grid((unsigned)KBH, cdiv(L, 4 * RB));
   const float scale = 1.0f / sqrtf((float)DH);
+  const HeadLayout lq = head_layout(ldqkv, H, L, DH), lo = head_layout(ldo, H, L, DH);
   DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_fwd_mfma_kernel<TT, D>), grid, dim3(WG), 0, s, CP(q), CP(k),
-                                                 CP(v), key_valid, MP(o), lse, L, H, scale)));
+                                                 CP(v), key_valid, MP(o), lse, L, H, scale, lq, lo)));
   return true;
 }
 
 bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                    const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
-                   int f32, hipStream_t s) {
+                   int f32, hipStream_t s, int ldqkv, int ldo) {
   if (!attn_mfma_supported(L, DH)) return false;
   const dim3 grid((unsigned)KBH, cdiv(L, 4 * RB));
   const float scale = 1.0f / sqrtf((float)DH);
+  const HeadLayout lq = head_layout(ldqkv, H, L, DH), lo = head_layout(ldo, H, L, DH);
   DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dq_mfma_kernel<TT, D>), grid, dim3(WG), 0, s, CP(dout),
                                                  CP(q), CP(k), CP(v), CP(o), lse, key_valid, MP(dq), delta, L, H,
-                                                 scale)));
+                                                 scale, lq, lo)));
   DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dkv_mfma_kernel<TT, D>), grid, dim3(WG), 0, s, CP(dout),
                                                  CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk), MP(dv), L, H,
-                                                 scale)));
+                                                 scale, lq, lo)));
   return true;
 }

@@ -178,22 +178,33 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("sign_vote", [](ptr packed, ptr active, ptr votes, int K, long Pn, ptr s) {
     sign_vote(P<const uint8_t>(packed), P<const uint8_t>(active), P<int>(votes), K, Pn, S(s));
   });
-  m.def("embedding_fwd", [](ptr tok, ptr table, ptr out, int K, long n_tok, int D, long t_cs, int rep, int f32, ptr s) {
-    embedding_fwd(P<const int>(tok), P<const void>(table), P<void>(out), K, n_tok, D, t_cs, rep, f32, S(s));
+  m.def("embedding_fwd", [](ptr tok, ptr table, ptr out, int K, long n_tok, int D, long t_cs, int rep, int f32, ptr s,
+                            float scale, ptr pe, int L) {
+    embedding_fwd(P<const int>(tok), P<const void>(table), P<void>(out), K, n_tok, D, t_cs, rep, f32, S(s), scale,
+                  P<const float>(pe), L);
   });
-  m.def("embedding_bwd", [](ptr tok, ptr dy, ptr dtable, int K, long n_tok, int D, long t_cs, int f32, ptr s) {
-    embedding_bwd(P<const int>(tok), P<const void>(dy), P<float>(dtable), K, n_tok, D, t_cs, f32, S(s));
+  m.def("embedding_bwd", [](ptr tok, ptr dy, ptr dtable, int K, long n_tok, int D, long t_cs, int f32, ptr s,
+                            float scale) {
+    embedding_bwd(P<const int>(tok), P<const void>(dy), P<float>(dtable), K, n_tok, D, t_cs, f32, S(s), scale);
+  });
+  m.def("seq_mean_fwd", [](ptr x, ptr len, ptr y, long S_, int L, int D, int f32, ptr s) {
+    seq_mean_fwd(P<const void>(x), P<const int>(len), P<void>(y), S_, L, D, f32, S(s));
+  });
+  m.def("seq_mean_bwd", [](ptr dy, ptr len, ptr dx, long S_, int L, int D, int f32, ptr s) {
+    seq_mean_bwd(P<const void>(dy), P<const int>(len), P<void>(dx), S_, L, D, f32, S(s));
   });
   m.def("attn_supported", &attn_supported);
-  m.def("attn_fwd", [](ptr q, ptr k, ptr v, ptr kv, ptr o, ptr lse, long KBH, int H, int L, int DH, int f32, ptr s) {
+  m.def("attn_packed_supported", &attn_packed_supported);
+  m.def("attn_fwd", [](ptr q, ptr k, ptr v, ptr kv, ptr o, ptr lse, long KBH, int H, int L, int DH, int f32, ptr s,
+                       int ldqkv, int ldo) {
     return attn_fwd(P<const void>(q), P<const void>(k), P<const void>(v), P<const int>(kv), P<void>(o), P<float>(lse),
-                    KBH, H, L, DH, f32, S(s));
+                    KBH, H, L, DH, f32, S(s), ldqkv, ldo);
   });
   m.def("attn_bwd", [](ptr dout, ptr q, ptr k, ptr v, ptr o, ptr lse, ptr kv, ptr dq, ptr dk, ptr dv, ptr delta,
-                       long KBH, int H, int L, int DH, int f32, ptr s) {
+                       long KBH, int H, int L, int DH, int f32, ptr s, int ldqkv, int ldo) {
     return attn_bwd(P<const void>(dout), P<const void>(q), P<const void>(k), P<const void>(v), P<const void>(o),
                     P<const float>(lse), P<const int>(kv), P<void>(dq), P<void>(dk), P<void>(dv), P<float>(delta), KBH,
-                    H, L, DH, f32, S(s));
+                    H, L, DH, f32, S(s), ldqkv, ldo);
   });
   m.def("spmm", [](ptr rowptr, ptr col, ptr val, ptr x, ptr y, int K, int N, int Nx, int F, long x_cs, long y_cs,
                    int f32, ptr s) {

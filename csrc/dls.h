@@ -179,24 +179,31 @@ void nnadq_qdq(float* x, const int* seg, const float* lo, const float* scale, co
                long ld, int nseg, hipStream_t s);
 void sign_pack(const float* g, uint8_t* out, int K, long P, long ld, hipStream_t s);
 void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, long P, hipStream_t s);
+// embedding lookup · scale (+ positional encoding pe [L][D] fp32, position = token index mod L)
 void embedding_fwd(const int* tokens, const void* table, void* out, int K, long n_tok, int D, long t_cs, int rep,
-                   int f32, hipStream_t s);
+                   int f32, hipStream_t s, float scale = 1.f, const float* pe = nullptr, int L = 0);
 void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long n_tok, int D, long t_cs, int f32,
-                   hipStream_t s);
+                   hipStream_t s, float scale = 1.f);
+// masked mean over the sequence axis of x [S][L][D] (valid length per sequence)
+void seq_mean_fwd(const void* x, const int* len, void* y, long S, int L, int D, int f32, hipStream_t s);
+void seq_mean_bwd(const void* dy, const int* len, void* dx, long S, int L, int D, int f32, hipStream_t s);
 // --------------------------------------------------------------- attention / graph
 bool attn_supported(int L, int DH);
 // MFMA flash attention (attention_mfma.hip), head dim 32 / 64; attn_fwd / attn_bwd route to it
 bool attn_mfma_supported(int L, int DH);
+// ldqkv / ldo > 0: q/k/v (and dq/dk/dv) are column blocks of packed [KB][L][ldqkv] rows, o / do
+// of [KB][L][ldo] rows (the QKV / out projections' own layouts; attention_mfma.hip)
 bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
-                   int H, int L, int DH, int f32, hipStream_t s);
+                   int H, int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0);
 bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                    const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
-                   int f32, hipStream_t s);
+                   int f32, hipStream_t s, int ldqkv = 0, int ldo = 0);
+bool attn_packed_supported(int L, int DH);
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
-              int L, int DH, int f32, hipStream_t s);
+              int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0);
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
-              hipStream_t s);
+              hipStream_t s, int ldqkv = 0, int ldo = 0);
 void spmm(const int* rowptr, const int* col, const float* val, const void* x, void* y, int K, int N, int Nx, int F,
           long x_cs, long y_cs, int f32, hipStream_t s);
 void gather_rows(const void* src, const int* idx, void* dst, long n, long row_bytes, hipStream_t s);

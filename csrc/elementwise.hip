@@ -522,26 +522,58 @@ __global__ void sign_vote_kernel(const uint8_t* __restrict__ packed, const uint8
   }
 }
 
+// out[k, t, :] = table[k / rep][tok[k, t], :] · scale (+ pe[t mod L, :]): the Transformer's
+// embedding lookup, √d scaling and positional-encoding add in one pass
 template <typename T>
 __global__ void embedding_fwd_kernel(const int* __restrict__ tok, const T* __restrict__ table,
-                                     T* __restrict__ out, long n_tok, int D, long t_cs, int rep, long total) {
+                                     T* __restrict__ out, long n_tok, int D, long t_cs, int rep, long total, float scale,
+                                     const float* __restrict__ pe, int L) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const long row = i / D;
   const int d = i % D;
   const int k = (int)(row / n_tok);
-  out[i] = table[(long)(k / rep) * t_cs + (long)tok[row] * D + d];
+  float v = ldf(table + (long)(k / rep) * t_cs + (long)tok[row] * D + d) * scale;
+  if (pe) v += pe[(long)((row % n_tok) % L) * D + d];
+  stf(out + i, v);
 }
 
 template <typename T>
 __global__ void embedding_bwd_kernel(const int* __restrict__ tok, const T* __restrict__ dy,
-                                     float* __restrict__ dtable, long n_tok, int D, long t_cs, long total) {
+                                     float* __restrict__ dtable, long n_tok, int D, long t_cs, long total, float scale) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const long row = i / D;
   const int d = i % D;
   const int k = (int)(row / n_tok);
-  atomicAdd(&dtable[(long)k * t_cs + (long)tok[row] * D + d], ldf(dy + i));
+  atomicAdd(&dtable[(long)k * t_cs + (long)tok[row] * D + d], ldf(dy + i) * scale);
+}
+
+// masked mean over the sequence: y[s, :] = Σ_{t < len[s]} x[s, t, :] / max(len[s], 1)
+template <typename T>
+__global__ void seq_mean_fwd_kernel(const T* __restrict__ x, const int* __restrict__ len, T* __restrict__ y, int L,
+                                    int D, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long s = i / D;
+  const int d = i % D;
+  const int n = min(len[s], L);
+  float acc = 0.f;
+  for (int t = 0; t < n; ++t) acc += ldf(x + (s * L + t) * D + d);
+  stf(y + i, acc / (float)max(n, 1));
+}
+
+template <typename T>
+__global__ void seq_mean_bwd_kernel(const T* __restrict__ dy, const int* __restrict__ len, T* __restrict__ dx, int L,
+                                    int D, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int d = i % D;
+  const long st = i / D;
+  const int t = st % L;
+  const long s = st / L;
+  const int n = min(len[s], L);
+  stf(dx + i, t < n ? ldf(dy + s * D + d) / (float)max(n, 1) : 0.f);
 }
 
 __global__ void gather_rows_kernel(const uint4* __restrict__ src, const int* __restrict__ idx,
@@ -701,17 +733,29 @@ void sign_vote(const uint8_t* packed, const uint8_t* active, int* votes, int K, 
 }
 
 void embedding_fwd(const int* tokens, const void* table, void* out, int K, long n_tok, int D, long t_cs, int rep,
-                   int f32, hipStream_t s) {
+                   int f32, hipStream_t s, float scale, const float* pe, int L) {
   const long total = (long)K * n_tok * D;
   DISPATCH_T(f32, hipLaunchKernelGGL(embedding_fwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens,
-                                     CP(table), MP(out), n_tok, D, t_cs, rep, total));
+                                     CP(table), MP(out), n_tok, D, t_cs, rep, total, scale, pe, L > 0 ? L : 1));
 }
 
 void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long n_tok, int D, long t_cs, int f32,
-                   hipStream_t s) {
+                   hipStream_t s, float scale) {
   const long total = (long)K * n_tok * D;
   DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, CP(dy),
-                                     dtable, n_tok, D, t_cs, total));
+                                     dtable, n_tok, D, t_cs, total, scale));
+}
+
+void seq_mean_fwd(const void* x, const int* len, void* y, long S, int L, int D, int f32, hipStream_t s) {
+  const long total = S * D;
+  DISPATCH_T(f32, hipLaunchKernelGGL(seq_mean_fwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, CP(x), len,
+                                     MP(y), L, D, total));
+}
+
+void seq_mean_bwd(const void* dy, const int* len, void* dx, long S, int L, int D, int f32, hipStream_t s) {
+  const long total = S * L * D;
+  DISPATCH_T(f32, hipLaunchKernelGGL(seq_mean_bwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, CP(dy), len,
+                                     MP(dx), L, D, total));
 }
 
 void gather_rows(const void* src, const int* idx, void* dst, long n, long row_bytes, hipStream_t s) {

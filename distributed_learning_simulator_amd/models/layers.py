@@ -201,9 +201,9 @@ class Embedding(Module):
     def own_params(self):
         return [self.w]
 
-    def forward(self, tokens, ctx):
+    def forward(self, tokens, ctx, scale: float = 1.0, pe=None):
         P = ctx.P
-        return Fn.embedding(tokens, ctx.token, P.w(self.w), P.g(self.w))
+        return Fn.embedding(tokens, ctx.token, P.w(self.w), P.g(self.w), scale, pe)
 
 
 class MaxPool(Module):

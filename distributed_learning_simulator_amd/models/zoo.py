@@ -270,7 +270,12 @@ class MultiheadAttention(Module):
     def forward(self, x, ctx, key_valid, residual=None):
         """Returns out_proj(attention) (+ residual, added in the projection's epilogue)."""
         K, B, L, D = x.shape
-        qkv = self.in_proj.forward(x, ctx).reshape(K, B, L, 3, self.h, D // self.h)
+        qkv = self.in_proj.forward(x, ctx)
+        if Fn.packed_attention_ok(qkv, L, D // self.h):
+            # heads read / written in place in the projections' row layouts (no permute copies)
+            o = Fn.attention_packed(qkv, key_valid, self.h)
+            return self.out_proj.forward(o, ctx, residual=residual)
+        qkv = qkv.reshape(K, B, L, 3, self.h, D // self.h)
         qkv = qkv.permute(3, 0, 1, 4, 2, 5)  # 3,K,B,H,L,dh
         o = Fn.attention(qkv[0].contiguous(), qkv[1].contiguous(), qkv[2].contiguous(), key_valid)
         o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
@@ -317,16 +322,15 @@ class TransformerClassifier(Module):
 
     def forward(self, batch, ctx):
         tokens, lengths = batch  # [K,B,L] int, [K,B] int
-        x = self.embedding.forward(tokens, ctx)
-        key = (x.device, x.dtype)
-        if key not in self._pe_dev:
-            self._pe_dev[key] = self._pe.to(x.device, x.dtype)
         L = tokens.shape[-1]
-        x = x * math.sqrt(self.d) + self._pe_dev[key][:L]
+        key = tokens.device
+        if key not in self._pe_dev:
+            self._pe_dev[key] = self._pe.to(tokens.device, torch.float32)
+        # embedding · √d + positional encoding: one fused kernel
+        x = self.embedding.forward(tokens, ctx, scale=math.sqrt(self.d), pe=self._pe_dev[key][:L].contiguous())
         for l in self.layers:
             x = l.forward(x, ctx, lengths)
-        m = (torch.arange(L, device=x.device)[None, None, :] < lengths[..., None]).to(x.dtype)
-        pooled = (x * m[..., None]).sum(2) / lengths.clamp(min=1)[..., None].to(x.dtype)
+        pooled = Fn.seq_mean(x, lengths)  # masked mean over the valid tokens
         return self.classifier.forward(pooled, ctx)
 
 

@@ -326,11 +326,14 @@ def cross_entropy(logits, labels, valid=None):
 
 # ------------------------------------------------------------------------ embedding
 class _Emb(torch.autograd.Function):
+    """Embedding lookup × scale (+ positional encoding) in one kernel (Transformer input:
+    emb·√d + PE, reference TransformerClassificationModel)."""
+
     @staticmethod
-    def forward(ctx, tokens, token, table, gtable):
+    def forward(ctx, tokens, token, table, gtable, scale=1.0, pe=None):
         ctx.save_for_backward(tokens)
-        ctx.gtable, ctx.vocab = gtable, table.shape[1]
-        return _be(table).embedding_fwd(tokens, table)
+        ctx.gtable, ctx.vocab, ctx.scale = gtable, table.shape[1], scale
+        return _be(table).embedding_fwd(tokens, table, scale, pe)
 
     @staticmethod
     def backward(ctx, dy):
@@ -338,14 +341,33 @@ class _Emb(torch.autograd.Function):
         if ctx.gtable is not None:
             be = _be(dy)
             if be is ref:
-                ctx.gtable.copy_(ref.embedding_bwd(dy, tokens, ctx.vocab))
+                ctx.gtable.copy_(ref.embedding_bwd(dy, tokens, ctx.vocab, ctx.scale))
             else:
-                be.embedding_bwd(dy.contiguous(), tokens, ctx.gtable)
-        return None, None, None, None
+                be.embedding_bwd(dy.contiguous(), tokens, ctx.gtable, ctx.scale)
+        return None, None, None, None, None, None
 
 
-def embedding(tokens, token, table, gtable):
-    return _Emb.apply(tokens, token, table, gtable)
+def embedding(tokens, token, table, gtable, scale: float = 1.0, pe=None):
+    return _Emb.apply(tokens, token, table, gtable, scale, pe)
+
+
+class _SeqMean(torch.autograd.Function):
+    """Masked mean over the sequence axis (the classifier's pooling of valid tokens)."""
+
+    @staticmethod
+    def forward(ctx, x, lengths):
+        ctx.save_for_backward(lengths)
+        ctx.L = x.shape[-2]
+        return _be(x).seq_mean_fwd(x, lengths)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (lengths,) = ctx.saved_tensors
+        return _be(dy).seq_mean_bwd(dy.contiguous(), lengths, ctx.L), None
+
+
+def seq_mean(x, lengths):
+    return _SeqMean.apply(x, lengths)
 
 
 # ------------------------------------------------------------------------ attention
@@ -366,6 +388,57 @@ class _Attn(torch.autograd.Function):
 
 def attention(q, k, v, key_valid=None):
     return _Attn.apply(q, k, v, key_valid)
+
+
+class _AttnPacked(torch.autograd.Function):
+    """Attention on the QKV projection's own output rows qkv [K, B, L, 3·D] → o [K, B, L, D]
+    (the out projection's input layout); backward returns dqkv in the QKV layout. On the GPU the
+    MFMA kernels read / write the heads in place (no permute copies either way)."""
+
+    @staticmethod
+    def forward(ctx, qkv, key_valid, H):
+        be = _be(qkv)
+        K, B, L, D3 = qkv.shape
+        D = D3 // 3
+        if be is ref:
+            t = qkv.reshape(K, B, L, 3, H, D // H).permute(3, 0, 1, 4, 2, 5)
+            o, lse = ref.attn_fwd(t[0], t[1], t[2], key_valid)
+            o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
+        else:
+            o, lse = be.attn_fwd_packed(qkv, H, key_valid)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.key_valid, ctx.H = key_valid, H
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        be = _be(do)
+        H = ctx.H
+        K, B, L, D3 = qkv.shape
+        D = D3 // 3
+        if be is ref:
+            t = qkv.reshape(K, B, L, 3, H, D // H).permute(3, 0, 1, 4, 2, 5)
+            op = o.reshape(K, B, L, H, D // H).permute(0, 1, 3, 2, 4)
+            dop = do.reshape(K, B, L, H, D // H).permute(0, 1, 3, 2, 4)
+            dq, dk, dv = ref.attn_bwd(dop, t[0], t[1], t[2], op, lse, ctx.key_valid)
+            dqkv = torch.stack([dq, dk, dv]).permute(1, 2, 4, 0, 3, 5).reshape(K, B, L, D3)
+        else:
+            dqkv = be.attn_bwd_packed(do.contiguous(), qkv, o, lse, H, ctx.key_valid)
+        return dqkv, None, None
+
+
+def attention_packed(qkv, key_valid, H: int):
+    return _AttnPacked.apply(qkv, key_valid, H)
+
+
+def packed_attention_ok(t: torch.Tensor, L: int, DH: int) -> bool:
+    """Whether the packed (copy-free) attention path runs for this device / shape."""
+    if not backend.using_hip(t):
+        return True
+    from . import hip
+
+    return hip.attn_packed_supported(L, DH)
 
 
 # ---------------------------------------------------------------------------- spmm

@@ -437,23 +437,49 @@ def ce_fwd_bwd(logits, labels, valid=None):
 
 
 # ------------------------------------------------------------------------ embedding
-def embedding_fwd(tokens, table):
+def embedding_fwd(tokens, table, scale: float = 1.0, pe=None):
+    """table[tokens] · scale (+ pe[position]) in one pass; pe [L, D] fp32 (L = tokens.shape[-1])."""
     K = tokens.shape[0]
     tok = tokens.to(torch.int32).contiguous()
     t_cs, rep = _client_view(table, K)
     D = table.shape[-1]
     n_tok = tok.numel() // K
     out = torch.empty((*tokens.shape, D), dtype=table.dtype, device=table.device)
-    _C.embedding_fwd(_p(tok), _p(table), _p(out), K, n_tok, D, t_cs, rep, _f32(table), _s())
+    L = tokens.shape[-1]
+    if pe is not None:
+        pe = pe.to(device=table.device, dtype=torch.float32).contiguous()
+        assert pe.shape == (L, D)
+    _C.embedding_fwd(_p(tok), _p(table), _p(out), K, n_tok, D, t_cs, rep, _f32(table), _s(), float(scale), _p(pe), L)
     return out
 
 
-def embedding_bwd(dy, tokens, gtable):
+def embedding_bwd(dy, tokens, gtable, scale: float = 1.0):
     K = tokens.shape[0]
     tok = tokens.to(torch.int32).contiguous()
     D = dy.shape[-1]
     gtable.zero_()
-    _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _f32(dy), _s())
+    _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _f32(dy), _s(),
+                     float(scale))
+
+
+def seq_mean_fwd(x, lengths):
+    """x [..., L, D] → masked mean over L with per-sequence lengths [...]."""
+    *lead, L, D = x.shape
+    x = x.contiguous()
+    S = x.numel() // (L * D)
+    ln = lengths.to(torch.int32).reshape(-1).contiguous()
+    y = torch.empty((*lead, D), dtype=x.dtype, device=x.device)
+    _C.seq_mean_fwd(_p(x), _p(ln), _p(y), S, L, D, _f32(x), _s())
+    return y
+
+
+def seq_mean_bwd(dy, lengths, L: int):
+    *lead, D = dy.shape
+    S = dy.numel() // D
+    ln = lengths.to(torch.int32).reshape(-1).contiguous()
+    dx = torch.empty((*lead, L, D), dtype=dy.dtype, device=dy.device)
+    _C.seq_mean_bwd(_p(dy.contiguous()), _p(ln), _p(dx), S, L, D, _f32(dy), _s())
+    return dx
 
 
 # ------------------------------------------------------------------------ attention
@@ -482,7 +508,7 @@ def attn_fwd(q, k, v, key_valid=None):
     kv = _key_valid(key_valid, q)
     o = torch.empty_like(q)
     lse = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
-    _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _f32(q), _s())
+    _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _f32(q), _s(), 0, 0)
     return o, lse
 
 
@@ -493,8 +519,51 @@ def attn_bwd(do, q, k, v, o, lse, key_valid=None):
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     delta = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
     _C.attn_bwd(_p(do), _p(q), _p(k), _p(v), _p(o), _p(lse.contiguous()), _p(kv), _p(dq), _p(dk), _p(dv), _p(delta),
-                KBH, H, L, DH, _f32(q), _s())
+                KBH, H, L, DH, _f32(q), _s(), 0, 0)
     return dq, dk, dv
+
+
+def attn_packed_supported(L: int, DH: int) -> bool:
+    return bool(_C.attn_packed_supported(L, DH))
+
+
+def attn_fwd_packed(qkv, H: int, key_valid=None):
+    """Attention straight from the QKV projection's output rows qkv [K, B, L, 3·D] (q | k | v
+    column blocks, heads of dh = D/H inside each): returns o [K, B, L, D] — the out projection's
+    input layout — and lse [K, B, H, L]. No permute / contiguous copies."""
+    K, B, L, D3 = qkv.shape
+    D = D3 // 3
+    DH = D // H
+    qkv = qkv.contiguous()
+    assert qkv.dtype in _DTYPES and attn_packed_supported(L, DH)
+    kv = _key_valid(key_valid, qkv)
+    o = torch.empty((K, B, L, D), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((K, B, H, L), dtype=torch.float32, device=qkv.device)
+    base = qkv.data_ptr()
+    es = qkv.element_size()
+    _keepalive.append(qkv)
+    ok = _C.attn_fwd(base, base + D * es, base + 2 * D * es, _p(kv), _p(o), _p(lse), K * B * H, H, L, DH,
+                     _f32(qkv), _s(), D3, D)
+    assert ok
+    return o, lse
+
+
+def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None):
+    """dqkv [K, B, L, 3·D] (the QKV projection's gradient layout) from do / o [K, B, L, D]."""
+    K, B, L, D3 = qkv.shape
+    D = D3 // 3
+    DH = D // H
+    do, o, qkv = do.contiguous(), o.contiguous(), qkv.contiguous()
+    kv = _key_valid(key_valid, qkv)
+    dqkv = torch.empty_like(qkv)
+    delta = torch.empty((K, B, H, L), dtype=torch.float32, device=qkv.device)
+    b, g, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+    _keepalive.append(qkv)
+    _keepalive.append(dqkv)
+    ok = _C.attn_bwd(_p(do), b, b + D * es, b + 2 * D * es, _p(o), _p(lse.contiguous()), _p(kv), g, g + D * es,
+                     g + 2 * D * es, _p(delta), K * B * H, H, L, DH, _f32(qkv), _s(), D3, D)
+    assert ok
+    return dqkv
 
 
 # ----------------------------------------------------------------------------- SpMM

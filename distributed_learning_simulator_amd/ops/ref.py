@@ -255,21 +255,39 @@ def ce_fwd_bwd(logits, labels, valid=None):
 
 
 # ----------------------------------------------------------------------- embedding
-def embedding_fwd(tokens, table):
+def embedding_fwd(tokens, table, scale: float = 1.0, pe=None):
     K = tokens.shape[0]
     table = _match(table, K)
     flat = tokens.reshape(K, -1).long()
     out = torch.gather(table, 1, flat.unsqueeze(-1).expand(-1, -1, table.shape[-1]))
-    return out.reshape(*tokens.shape, table.shape[-1])
+    out = out.reshape(*tokens.shape, table.shape[-1])
+    if scale != 1.0 or pe is not None:
+        out = out.float() * scale
+        if pe is not None:
+            out = out + pe.to(out.device, torch.float32)
+        out = out.to(table.dtype)
+    return out
 
 
-def embedding_bwd(dy, tokens, vocab: int):
+def embedding_bwd(dy, tokens, vocab: int, scale: float = 1.0):
     K = tokens.shape[0]
     D = dy.shape[-1]
     flat = tokens.reshape(K, -1).long()
     out = torch.zeros((K, vocab, D), dtype=torch.float32, device=dy.device)
-    out.scatter_add_(1, flat.unsqueeze(-1).expand(-1, -1, D), dy.reshape(K, -1, D).float())
+    out.scatter_add_(1, flat.unsqueeze(-1).expand(-1, -1, D), dy.reshape(K, -1, D).float() * scale)
     return out
+
+
+def seq_mean_fwd(x, lengths):
+    L = x.shape[-2]
+    m = (torch.arange(L, device=x.device) < lengths.to(x.device)[..., None]).to(torch.float32)
+    return ((x.float() * m[..., None]).sum(-2) / lengths.to(x.device).clamp(min=1)[..., None].float()).to(x.dtype)
+
+
+def seq_mean_bwd(dy, lengths, L: int):
+    m = (torch.arange(L, device=dy.device) < lengths.to(dy.device)[..., None]).to(torch.float32)
+    g = dy.float()[..., None, :] * m[..., None] / lengths.to(dy.device).clamp(min=1)[..., None, None].float()
+    return g.to(dy.dtype)
 
 
 # ----------------------------------------------------------------------- attention

@@ -32,8 +32,12 @@ case "$mode" in
     timeout -k 10 1000 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
       python -u bench.py "$@" > gpurun_out/prof_bench.log 2>&1
     rc=$?
-    grep '^{' gpurun_out/prof_bench.log | tail -1
-    find gpurun_out/prof -name '*kernel_stats.csv' | head -1 | xargs -r head -25
+    grep '^{' gpurun_out/prof_bench.log | tail -1 | tee gpurun_out/prof_bench.json
+    # keep the summaries only: the per-dispatch trace of a long run exceeds the copy-back cap
+    stats=$(find gpurun_out/prof -name '*kernel_stats.csv' | head -1)
+    [ -n "$stats" ] && cp "$stats" gpurun_out/prof_kernel_stats.csv
+    rm -rf gpurun_out/prof
+    [ -f gpurun_out/prof_kernel_stats.csv ] && cut -c1-200 gpurun_out/prof_kernel_stats.csv | head -25
     exit $rc
     ;;
   pmc)

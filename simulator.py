@@ -21,5 +21,10 @@ if __name__ == "__main__":
         sys.exit(launch.spawn_ranks(n))
     from distributed_learning_simulator_amd.training import train
 
+    from distributed_learning_simulator_amd.parallel.comm import shutdown
+
     global_config.apply_global_config()
-    train(config=global_config)
+    try:
+        train(config=global_config)
+    finally:
+        shutdown()  # every rank leaves the process group before exit

@@ -290,3 +290,55 @@ def test_attention_mfma(hip, L, dh, dtype, tol):
         for bb in range(B):
             n = int(kv[kk, bb])
             assert torch.all(dk[kk, bb, :, n:] == 0) and torch.all(dv[kk, bb, :, n:] == 0)
+
+
+@pytest.mark.parametrize("L,H,D", [(200, 8, 512), (37, 4, 128), (130, 2, 64)])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 3e-5), (torch.bfloat16, 2.5e-2)])
+def test_attention_packed_qkv(hip, L, H, D, dtype, tol):
+    """Attention read straight from the QKV projection rows [K, B, L, 3D] (strided heads, no
+    permute copies) and the gradient written back in that layout: against the float64 oracle
+    applied to the explicitly split / permuted q, k, v."""
+    K, B = 2, 2
+    dh = D // H
+    if not hip.attn_packed_supported(L, dh):
+        pytest.skip("no packed kernel for this head dim")
+    torch.manual_seed(L + D)
+    qkv = _f(K, B, L, 3 * D).to(dtype)
+    kv = torch.randint(1, L + 1, (K, B), device=DEV, dtype=torch.int32)
+    o, lse = hip.attn_fwd_packed(qkv, H, kv)
+    assert o.shape == (K, B, L, D)
+
+    def heads(t):  # [K,B,L,D] → [K,B,H,L,dh]
+        return t.reshape(K, B, L, H, dh).permute(0, 1, 3, 2, 4)
+
+    q, k, v = (heads(_d(t)) for t in qkv.split(D, dim=-1))
+    o2, lse2 = ref.attn_fwd(q, k, v, kv.cpu())
+    _close(o, o2.permute(0, 1, 3, 2, 4).reshape(K, B, L, D), tol)
+    _close(lse, lse2, max(tol, 1e-5))
+    do = _f(K, B, L, D).to(dtype)
+    dqkv = hip.attn_bwd_packed(do, qkv, o, lse, H, kv)
+    rq, rk, rv = ref.attn_bwd(heads(_d(do)), q, k, v, o2, lse2, kv.cpu())
+    flat = lambda t: t.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)  # noqa: E731
+    _close(dqkv, torch.cat([flat(rq), flat(rk), flat(rv)], -1), tol * 2)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 1e-2)])
+def test_embedding_scale_pe_and_seq_mean(hip, dtype, tol):
+    """Fused Transformer input (table[tok]·√d + PE) and masked mean pooling, fwd + bwd."""
+    K, B, L, V, D = 3, 4, 37, 100, 64
+    table = _f(K, V, D).to(dtype)
+    tok = torch.randint(0, V, (K, B, L), device=DEV)
+    pe = torch.randn(L, D, device=DEV)
+    s = D ** 0.5
+    out = hip.embedding_fwd(tok, table, s, pe)
+    exp = ref.embedding_fwd(tok.cpu(), _d(table), s, pe.cpu().double())
+    _close(out, exp, tol)
+    dy = _f(K, B, L, D).to(dtype)
+    g = torch.empty(K, V, D, device=DEV, dtype=torch.float32)
+    hip.embedding_bwd(dy, tok, g, s)
+    _close(g, ref.embedding_bwd(_d(dy), tok.cpu(), V, s), max(tol, 1e-5))
+    x = _f(K, B, L, D).to(dtype)
+    lengths = torch.randint(1, L + 1, (K, B), device=DEV, dtype=torch.int32)
+    _close(hip.seq_mean_fwd(x, lengths), ref.seq_mean_fwd(_d(x), lengths.cpu()), tol)
+    dp = _f(K, B, D).to(dtype)
+    _close(hip.seq_mean_bwd(dp, lengths, L), ref.seq_mean_bwd(_d(dp), lengths.cpu(), L), tol)
