@@ -53,13 +53,25 @@ __device__ __forceinline__ void st_split(bf16_t* hi, bf16_t* lo, const FV<V>& f)
   *reinterpret_cast<TV*>(lo) = l.v;
 }
 
+// element offset of k-column e inside row r of a BK-wide bf16 row-major image (16-B slot XOR)
+template <int BK>
+__device__ __forceinline__ int swz(int r, int e) {
+  constexpr int S = BK / 8, RPR = 256 / (BK * 2);  // slots per row, rows per 256-B bank row
+  static_assert(S >= 2 && RPR >= 1, "swizzle needs 16..128-element rows");
+  return (((e >> 3) ^ ((r / RPR) % S)) << 3) | (e & 7);
+}
+
 // ------------------------------------------------------------------------- NT (fwd / dgrad)
 template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int NBUF>
 __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p) {
   constexpr int T = WM * WN * 64;
   constexpr int TM = BM / (WM * 32);
   constexpr int TN = BN / (WN * 32);
-  constexpr int LDA = BK + 8;
+  // row-major [row][k] images (A, and B when !BKM) are unpadded BK-element rows whose 16-B slots
+  // are XOR-swizzled by the row's position in the 256-B bank row: ds_read_b128 fragment reads and
+  // the 8-lane ds_write_b128 / 16-lane ds_write_b64 split stores are all conflict-free (a +8 pad
+  // made the stores straddle bank rows: 2-way, 20-35 % of LDS cycles in SQ_LDS_BANK_CONFLICT)
+  constexpr int LDA = BK;
   constexpr int KCA = BK / VA, RPA = T / KCA, PA = BM / RPA;
   constexpr int KCB = BK / VB, RPB = T / KCB, PB = BN / RPB;  // B row-major [n][k]
   constexpr int CCB = BN / VB, RPK = T / CCB, PK = BK / RPK;  // B k-major [k][n]
@@ -173,13 +185,15 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
   auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
-      const int off = (buf * BM + tid / KCA + j * RPA) * LDA + kca * VA;
+      const int r = tid / KCA + j * RPA;
+      const int off = (buf * BM + r) * LDA + swz<BK>(r, kca * VA);
       st_split(As + off, As + A_PLANE + off, ra[j]);
     }
     if constexpr (!BKM) {
 #pragma unroll
       for (int j = 0; j < PB; ++j) {
-        const int off = (buf * B_ROWS + tid / KCB + j * RPB) * B_COLS + kcb * VB;
+        const int r = tid / KCB + j * RPB;
+        const int off = (buf * B_ROWS + r) * B_COLS + swz<BK>(r, kcb * VB);
         st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
       }
     } else {
@@ -205,14 +219,16 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
       bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int off = (buf * BM + wm0 + i * 32 + (lane & 31)) * LDA + ks * 16 + 8 * h;
+        const int r = wm0 + i * 32 + (lane & 31);
+        const int off = (buf * BM + r) * LDA + swz<BK>(r, ks * 16 + 8 * h);
         ah[i] = *reinterpret_cast<const bf16x8*>(As + off);
         al[i] = *reinterpret_cast<const bf16x8*>(As + A_PLANE + off);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if constexpr (!BKM) {
-          const int off = (buf * B_ROWS + wn0 + j * 32 + (lane & 31)) * B_COLS + ks * 16 + 8 * h;
+          const int r = wn0 + j * 32 + (lane & 31);
+          const int off = (buf * B_ROWS + r) * B_COLS + swz<BK>(r, ks * 16 + 8 * h);
           bh[j] = *reinterpret_cast<const bf16x8*>(Bs + off);
           bl[j] = *reinterpret_cast<const bf16x8*>(Bs + B_PLANE + off);
         } else {

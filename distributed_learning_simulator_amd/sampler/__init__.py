@@ -10,6 +10,7 @@ from __future__ import annotations
 
 from typing import Callable
 
+import numpy as np
 import torch
 
 from ..utils.logging import get_logger
@@ -102,12 +103,12 @@ def dirichlet_split(labels: torch.Tensor, part_number: int, seed: int = 0, alpha
     num_classes = int(labels.max().item()) + 1
     g = torch.Generator().manual_seed(seed + 37)
     parts: list[list[torch.Tensor]] = [[] for _ in range(part_number)]
-    dist = torch.distributions.Dirichlet(torch.full((part_number,), float(alpha)))
-    torch.manual_seed(seed + 41)
+    # a private generator: partitioning must not reseed the process-wide torch RNG
+    rng = np.random.default_rng(seed + 41)
     for c in range(num_classes):
         idx = (labels == c).nonzero().flatten()
         idx = idx[torch.randperm(idx.numel(), generator=g)]
-        prop = dist.sample()
+        prop = torch.from_numpy(rng.dirichlet(np.full(part_number, float(alpha))))
         cuts = (prop.cumsum(0) * idx.numel()).round().long().tolist()[:-1]
         for p, chunk in enumerate(torch.tensor_split(idx, cuts)):
             parts[p].append(chunk)

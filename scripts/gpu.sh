@@ -6,6 +6,7 @@
 #   scripts/gpu.sh bench [ARGS...]    bench.py ARGS  -> gpurun_out/bench.json
 #   scripts/gpu.sh prof  [ARGS...]    rocprofv3 --kernel-trace --stats of bench.py ARGS
 #   scripts/gpu.sh pmc   COUNTERS [ARGS...]   one rocprofv3 --pmc pass (counter limits: see guide)
+#   scripts/gpu.sh pmcset [ARGS...]  MFMA/LDS/HBM counter passes -> gpurun_out/pmc_summary.csv
 #   scripts/gpu.sh kbench [ARGS...]   bench/kernel_bench.py ARGS
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
@@ -46,6 +47,23 @@ case "$mode" in
     timeout -s KILL 300 rocprofv3 --pmc $counters --output-format csv -d gpurun_out/pmc -o run -- \
       python -u bench.py "$@" > gpurun_out/pmc_bench.log 2>&1
     exit $?
+    ;;
+  pmcset)
+    # two counter passes over the same bench run (each within the per-block slot limits), folded
+    # into gpurun_out/pmc_summary.csv by scripts/pmc_summary.py; the raw per-dispatch CSVs are removed
+    rm -rf gpurun_out/pmcA gpurun_out/pmcB
+    timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1 || true
+    timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+      SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmcA -o run -- \
+      python -u bench.py "$@" > gpurun_out/pmcA.log 2>&1 || { tail -5 gpurun_out/pmcA.log; exit 1; }
+    timeout -s KILL 400 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE --kernel-trace \
+      --output-format csv -d gpurun_out/pmcB -o run -- \
+      python -u bench.py "$@" > gpurun_out/pmcB.log 2>&1 || { tail -5 gpurun_out/pmcB.log; exit 1; }
+    python scripts/pmc_summary.py gpurun_out/pmc_summary.csv gpurun_out/pmcA gpurun_out/pmcB
+    rc=$?
+    rm -rf gpurun_out/pmcA gpurun_out/pmcB
+    cut -d, -f1-8 gpurun_out/pmc_summary.csv | cut -c1-220 | head -20
+    exit $rc
     ;;
   kbench)
     timeout -k 10 900 python -u bench/kernel_bench.py "$@" > gpurun_out/kbench.log 2>&1
