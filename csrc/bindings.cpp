@@ -19,8 +19,11 @@ PYBIND11_MODULE(_dls_hip, m) {
 
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
-                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s, int ldx, int ldy) {
+                      int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s, int ldx, int ldy,
+                      ptr stats, ptr stats_valid) {
     ConvNTParams p{};
+    p.stats = P<float>(stats);
+    p.stats_valid = P<const int>(stats_valid);
     p.f32 = f32;
     p.ldx = ldx;
     p.ldy = ldy;
@@ -83,10 +86,10 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
                      int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, int f32, ptr s,
-                     int ldx) {
+                     int ldx, ptr pre_part, int pre_nparts) {
     bn_fwd(P<const void>(x), P<const void>(gamma), P<const void>(beta), P<const void>(res), P<void>(y), P<float>(mean),
            P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws), P<uint8_t>(mask),
-           P<unsigned>(counters), f32, S(s), ldx);
+           P<unsigned>(counters), f32, S(s), ldx, P<const float>(pre_part), pre_nparts);
   });
   m.def("bn_bwd", [](ptr dy, ptr x, ptr y, ptr mean, ptr rstd, ptr gamma, ptr valid, long g_cs, int K, int R, int C,
                      int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr mask, ptr counters,

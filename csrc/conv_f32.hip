@@ -291,9 +291,38 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
   }
   float* slab = reinterpret_cast<float*>(smem) + wid * 32 * SW;
   const bool vec_ok = (p.N % 4) == 0 && (p.ldy % 4) == 0 && ((uintptr_t)y & 15) == 0;
+  // BN statistics rows: GEMM rows of this client's valid samples
+  const int stat_rows = p.stats ? (p.stats_valid ? min(p.M, p.stats_valid[client] * p.OH * p.OW) : p.M) : 0;
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    const int g0 = m0 + wm0 + i * 32;  // this wave's 32-row group (a multiple of 32)
+    if (p.stats && g0 < p.M) {
+      // per-column Σy, Σy² of the group straight from the accumulators: lane (c, h) holds rows
+      // (e&3) + 8(e>>2) + 4h of column c; the two half-waves combine with one xor-shuffle
+      float* part = p.stats + ((long)client * ((p.M + 31) / 32) + g0 / 32) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = g0 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          float v = acc[i][j][e] + bvals[j];
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (m < stat_rows) {
+            s0 += v;
+            s1 = fmaf(v, v, s1);
+          }
+        }
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        const int n = n0 + wn0 + j * 32 + (lane & 31);
+        if (lane < 32 && n < p.N) {
+          part[n] = s0;
+          part[p.N + n] = s1;
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
 #pragma unroll

@@ -382,6 +382,10 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
     conv_nt_f32(p, K, variant, s);
     return;
   }
+  if (p.stats) {  // epilogue BN statistics exist in the fp32 kernels only (callers check)
+    fprintf(stderr, "conv_nt: epilogue statistics need the fp32 kernels\n");
+    abort();
+  }
   const bool bkm = p.b_kmajor != 0;
   int va = vec_width(std::gcd(p.C, p.ldx));  // vectors must not straddle a channel-sliced pixel
   int vb = bkm ? vec_width(p.N) : vec_width(p.R);

@@ -52,6 +52,12 @@ struct ConvNTParams {
   // channel strides of channel-sliced views (DenseNet's preallocated block buffer): A pixel
   // stride ldx (0 = C), output / acc / gate row stride ldy (0 = N)
   int ldx, ldy;
+  // optional BN statistics of the output (fp32 kernels): per 32-row group g and column n,
+  // stats[client][g][0][n] = Σ y, stats[client][g][1][n] = Σ y² over the rows of valid samples
+  // (row < stats_valid[client]·OH·OW) — the [K][parts][2N] partial layout bn_fwd consumes
+  // (parts = cdiv(M, 32)), so BN skips its own statistics pass over y
+  float* stats;
+  const int* stats_valid;  // [K] valid samples per client (nullptr: all rows)
 };
 
 struct ConvTNParams {
@@ -127,8 +133,11 @@ long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
             uint8_t* relu_mask, unsigned* counters, int f32, hipStream_t s,
-            int ldx = 0);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused coefs);
-                           // ldx: row stride of x / res (channel slice of a wider buffer), y contiguous
+            int ldx = 0, const float* pre_part = nullptr,
+            int pre_nparts = 0);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused
+                                  // coefs); ldx: row stride of x / res (channel slice of a wider buffer), y
+                                  // contiguous; pre_part: [K][pre_nparts][2C] Σx / Σx² partials from the
+                                  // producing conv's epilogue (ConvNTParams::stats) — no statistics pass
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
             float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, unsigned* counters, int f32,

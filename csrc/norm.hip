@@ -222,34 +222,38 @@ __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ 
                                                       float* __restrict__ coef, float* __restrict__ dgamma,
                                                       float* __restrict__ dbeta, long dg_cs, long g_cs, int K, int R, int C,
                                                       float eps, int rep, int bwd) {
-  __shared__ float red[2][8][33];
+  // partials are summed in fp64 (the conv-epilogue statistics arrive as thousands of 32-row
+  // partials per channel; Σx² − n·μ² then keeps its precision), in a fixed order
+  __shared__ double red[2][8][33];
   const int k = blockIdx.y;
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
-  float s0 = 0.f, s1 = 0.f;
+  double d0 = 0.0, d1 = 0.0;
   if (c < C) {
     const float* part = ws + (long)k * nparts * 2 * C;
     for (int b = grp; b < nparts; b += 8) {
-      s0 += part[(long)b * 2 * C + c];
-      s1 += part[(long)b * 2 * C + C + c];
+      d0 += part[(long)b * 2 * C + c];
+      d1 += part[(long)b * 2 * C + C + c];
     }
   }
-  red[0][grp][cl] = s0;
-  red[1][grp][cl] = s1;
+  red[0][grp][cl] = d0;
+  red[1][grp][cl] = d1;
   __syncthreads();
   if (grp != 0 || c >= C) return;
 #pragma unroll
   for (int g2 = 1; g2 < 8; ++g2) {
-    s0 += red[0][g2][cl];
-    s1 += red[1][g2][cl];
+    d0 += red[0][g2][cl];
+    d1 += red[1][g2][cl];
   }
+  const float s0 = (float)d0, s1 = (float)d1;
   const long i = (long)k * C + c;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
   const float n = (float)max(nvalid, 1);
   const float g = ldf(gamma + (long)(k / rep) * g_cs + c);
   if (!bwd) {
-    const float mu = s0 / n;
-    const float var = fmaxf(s1 / n - mu * mu, 0.f);
+    const double mud = d0 / n;
+    const float mu = (float)mud;
+    const float var = (float)fmax(d1 / n - mud * mud, 0.0);
     const float rs = rsqrtf(var + eps);
     const float sc = g * rs;
     mean_out[i] = mu;
@@ -519,22 +523,26 @@ long bn_workspace_floats(int K, long R, int C) {
 
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
-            uint8_t* rmask, unsigned* counters, int f32, hipStream_t s, int ldx) {
+            uint8_t* rmask, unsigned* counters, int f32, hipStream_t s, int ldx, const float* pre_part,
+            int pre_nparts) {
   if (ldx == 0) ldx = C;
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
   float* coef = ws;
-  float* part = ws + (long)3 * C * K;
+  const float* part = pre_part ? pre_part : ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
+  const int nparts = pre_part ? pre_nparts : (int)grid.x;
   const int V = vw(std::gcd(C, ldx));
   BNCoefArgs ca{gamma, beta, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, eps, rep, 0, counters};
   if (V != 8) rmask = nullptr;  // bit masks need 8-channel vectors
   DISPATCH_T(f32, {
-    DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 0>), grid, dim3(256), 0, s, CP(x), nullptr, nullptr,
-                                     nullptr, nullptr, valid_rows, R, C, 0, part, (long)2 * C, rpb, nullptr, ca, ldx,
-                                     ldx));
-    if (!counters)
-      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, CP(gamma),
+    if (!pre_part) {  // (else the producing conv's epilogue already wrote the partial sums)
+      DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 0>), grid, dim3(256), 0, s, CP(x), nullptr, nullptr,
+                                       nullptr, nullptr, valid_rows, R, C, 0, ws + (long)3 * C * K, (long)2 * C, rpb,
+                                       nullptr, ca, ldx, ldx));
+    }
+    if (!counters || pre_part)
+      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, nparts, CP(gamma),
                          CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C,
                          eps, rep, 0);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),

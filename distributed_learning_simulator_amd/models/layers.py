@@ -115,11 +115,11 @@ class Conv2d(Module):
     def own_params(self):
         return [self.w] + ([self.b] if self.b else [])
 
-    def forward(self, x, ctx, link=None):
+    def forward(self, x, ctx, link=None, stats=None):
         P = ctx.P
         b = P.w(self.b) if self.b else None
         gb = P.g(self.b) if self.b else None
-        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb, link=link)
+        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb, link=link, stats=stats)
 
 
 class BatchNorm(Module):
@@ -139,13 +139,20 @@ class BatchNorm(Module):
     def own_params(self):
         return [self.gamma, self.beta]
 
-    def forward(self, x, ctx, residual=None, relu=None, link=None):
+    def forward(self, x, ctx, residual=None, relu=None, link=None, stats=None):
         P = ctx.P
         rps = 1
         for d in x.shape[2:-1]:
             rps *= d
         return Fn.batch_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta),
-                             ctx.valid_rows(rps), self.relu if relu is None else relu, residual, link=link)
+                             ctx.valid_rows(rps), self.relu if relu is None else relu, residual, link=link,
+                             stats=stats)
+
+
+def conv_bn(conv: Conv2d, bn: BatchNorm, x, ctx, conv_link=None, **bn_kw):
+    """conv → BatchNorm with the BN statistics taken from the conv's epilogue (Fn.BNStats)."""
+    st = Fn.BNStats(ctx.valid)
+    return bn.forward(conv.forward(x, ctx, link=conv_link, stats=st), ctx, stats=st, **bn_kw)
 
 
 class Linear(Module):

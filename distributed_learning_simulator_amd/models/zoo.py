@@ -14,7 +14,7 @@ import torch
 
 from ..engine.params import ParamLayout
 from ..ops import functional as Fn
-from .layers import (AvgPool, BatchNorm, Conv2d, Embedding, Flatten, LayerNorm, Linear,
+from .layers import (AvgPool, BatchNorm, Conv2d, Embedding, conv_bn, Flatten, LayerNorm, Linear,
                      MaxPool, Module, ReLU, RunCtx, Seq)
 
 
@@ -94,6 +94,12 @@ def _residual_link(block, x, ctx):
     return None
 
 
+def _down(seq: Seq, x, ctx):
+    """Downsample shortcut Seq(Conv2d 1x1, BatchNorm) with epilogue statistics."""
+    conv, bn = seq.children
+    return conv_bn(conv, bn, x, ctx)
+
+
 class BasicBlock(Module):
     kind = "BasicBlock"
     expansion = 1
@@ -110,10 +116,9 @@ class BasicBlock(Module):
 
     def forward(self, x, ctx):
         link = _residual_link(self, x, ctx)
-        out = self.bn1.forward(self.conv1.forward(x, ctx, link=link), ctx)
-        out = self.conv2.forward(out, ctx)
-        sc = x if self.down is None else self.down.forward(x, ctx)
-        return self.bn2.forward(out, ctx, residual=sc, relu=True, link=link)
+        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link)
+        sc = x if self.down is None else _down(self.down, x, ctx)
+        return conv_bn(self.conv2, self.bn2, out, ctx, residual=sc, relu=True, link=link)
 
 
 class Bottleneck(Module):
@@ -135,11 +140,10 @@ class Bottleneck(Module):
 
     def forward(self, x, ctx):
         link = _residual_link(self, x, ctx)
-        out = self.bn1.forward(self.conv1.forward(x, ctx, link=link), ctx)
-        out = self.bn2.forward(self.conv2.forward(out, ctx), ctx)
-        out = self.conv3.forward(out, ctx)
-        sc = x if self.down is None else self.down.forward(x, ctx)
-        return self.bn3.forward(out, ctx, residual=sc, relu=True, link=link)
+        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link)
+        out = conv_bn(self.conv2, self.bn2, out, ctx)
+        sc = x if self.down is None else _down(self.down, x, ctx)
+        return conv_bn(self.conv3, self.bn3, out, ctx, residual=sc, relu=True, link=link)
 
 
 class ResNetNet(Module):
@@ -168,7 +172,7 @@ class ResNetNet(Module):
         self.child("fc", Linear(c, classes))
 
     def forward(self, x, ctx):
-        x = self.bn1.forward(self.conv1.forward(x, ctx), ctx)
+        x = conv_bn(self.conv1, self.bn1, x, ctx)
         if not self.cifar_stem:
             x = self.maxpool.forward(x, ctx)
         for s in self.stages:

@@ -10,6 +10,8 @@ even when the op's activation input does not need a gradient (e.g. the stem conv
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import backend, ref
@@ -32,18 +34,43 @@ class ResidualLink:
         self.grad = None
 
 
+# DLS_BN_EPILOGUE_STATS=0: BatchNorm computes its statistics in its own pass (A/B switch)
+EPILOGUE_BN_STATS = os.environ.get("DLS_BN_EPILOGUE_STATS", "1") != "0"
+
+
+class BNStats:
+    """Hands a BatchNorm's batch statistics from the conv that produces its input: the fp32 conv
+    epilogue writes per-32-row Σy / Σy² partials (of the first `valid[k]` samples' rows) and the
+    BN consumes them instead of re-reading y in a statistics pass. `part` stays None when the
+    producing conv could not provide them (CPU oracle, bf16 kernels, LDS-DMA path)."""
+
+    __slots__ = ("valid", "part")
+
+    def __init__(self, valid=None):
+        self.valid = valid
+        self.part = None
+
+
 class _Conv(torch.autograd.Function):
     """Conv2d over the client dim. If the input carries more channels than the weight (image
     data stored zero-padded to 8 channels), the weight is zero-padded to match and only the
     real channels' gradient is written back."""
 
     @staticmethod
-    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None):
+    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None, stats=None):
         be = _be(x)
         ci = w.shape[-1]
         if x.shape[-1] > ci:
             w = torch.nn.functional.pad(w, (0, x.shape[-1] - ci))
-        y = be.conv_fwd(x, w, stride, pad, bias=b)
+        if stats is not None and be is not ref and x.dtype == torch.float32 and EPILOGUE_BN_STATS:
+            K, B, H, W = x.shape[:4]
+            KH = w.shape[2]
+            OH, OW = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - w.shape[3]) // stride + 1
+            stats.part = torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
+                                     device=x.device)
+            y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid)
+        else:
+            y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         ctx.link = link
@@ -79,15 +106,17 @@ class _Conv(torch.autograd.Function):
                     be.bias_grad(dy, ctx.gb)
             if padded:
                 ctx.gw.copy_(gw[..., : ctx.ci])
-        return dx, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None
 
 
-def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None, link: ResidualLink | None = None):
+def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None, link: ResidualLink | None = None,
+           stats: BNStats | None = None):
     """`link`: this conv's input is also the identity shortcut of a residual BN fed the same
-    link (its gradient then arrives through the dgrad epilogue)."""
+    link (its gradient then arrives through the dgrad epilogue). `stats`: the output feeds a
+    BatchNorm given the same holder (its statistics come from this conv's epilogue)."""
     if link is not None:
         assert stride == 1 and w.shape[-1] == x.shape[-1], "residual link needs a stride-1, unpadded conv"
-    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link)
+    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link, stats)
 
 
 # --------------------------------------------------------------------------- linear
@@ -180,7 +209,7 @@ def linear_shared_input(x, token, w, gw):
 # ------------------------------------------------------------------------ batchnorm
 class _BN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link=None):
+    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link=None, stats=None):
         be = _be(x)
         K = x.shape[0]
         C = x.shape[-1]
@@ -190,7 +219,10 @@ class _BN(torch.autograd.Function):
         if be is ref:
             y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
         else:  # native: 1-bit ReLU mask so the backward need not re-read y
-            y, mean, rstd, mask = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True)
+            pre = stats.part if stats is not None else None
+            y, mean, rstd, mask = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True, pre_stats=pre)
+            if stats is not None:
+                stats.part = None
         ctx.save_for_backward(x3, y, mean, rstd, gamma)
         ctx.relu_mask = mask
         ctx.valid_rows, ctx.relu, ctx.has_res = valid_rows, relu, residual is not None
@@ -216,12 +248,12 @@ class _BN(torch.autograd.Function):
         if dres is not None and ctx.link is not None:
             ctx.link.grad = dres  # delivered by the block's first conv (ResidualLink)
             dres = None
-        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres, None
+        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres, None, None
 
 
 def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False, residual=None,
-               link: ResidualLink | None = None):
-    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link)
+               link: ResidualLink | None = None, stats: BNStats | None = None):
+    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link, stats)
 
 
 # ------------------------------------------------------------------------ layernorm

@@ -142,9 +142,16 @@ def _gl(K: int, M: int, N: int, C: int, taps: int) -> bool:
     return bool(_C.conv_gl_wanted(K, M, N, C, taps, mode))
 
 
-def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None):
+def conv_stats_parts(M: int) -> int:
+    """Partial-sum rows per client of the conv-epilogue BN statistics (one per 32 GEMM rows)."""
+    return (M + 31) // 32
+
+
+def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats=None, stats_valid=None):
     """`x` may be a channel slice of a wider buffer, `out` (optional) a channel slice to write
-    into (DenseNet block buffer): both are read / written in place through channel strides."""
+    into (DenseNet block buffer): both are read / written in place through channel strides.
+    `stats` (fp32 only): a [K, conv_stats_parts(M), 2, Co] fp32 buffer the epilogue fills with the
+    BN partial sums Σy, Σy² over the rows of the first `stats_valid[k]` samples (bn_fwd(pre_stats=))."""
     K, B, H, W, C = x.shape
     x, ldx = _pix_stride(x)
     f32 = _f32(x)
@@ -166,13 +173,19 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None):
         assert bias.dtype == x.dtype
         b_cs, _ = _client_view(bias, K)
     M = B * OH * OW
+    if stats is not None:
+        assert f32 and stats.dtype == torch.float32 and stats.is_contiguous()
+        assert stats.shape == (K, conv_stats_parts(M), 2, Co), stats.shape
+        if stats_valid is not None:
+            stats_valid = stats_valid.to(torch.int32).contiguous()
+            assert stats_valid.shape == (K,)
     if not f32 and ldx == C and ldy == Co and _gl(K, M, Co, C, KH * KW):
         _C.conv_gl_fwd(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, K, rep, B, H, W, C, OH, OW,
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), x.stride(0), y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
                pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32,
-               _s(), ldx, ldy)
+               _s(), ldx, ldy, _p(stats), _p(stats_valid))
     return y
 
 
@@ -248,7 +261,7 @@ def linear_fwd(x, w, b=None, relu=False, acc=None):
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0)
+               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL)
     return y
 
 
@@ -266,7 +279,8 @@ def linear_dgrad(dy, w, gate=None):
         assert gate.shape == dx.shape and gate.dtype == dy.dtype and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
-               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0)
+               1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0,
+               NULL, NULL)
     return dx
 
 
@@ -289,10 +303,12 @@ def linear_wgrad(dy, x, gw, gb=None):
 
 
 # ------------------------------------------------------------------------ batchnorm
-def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False):
+def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False, pre_stats=None):
     """Returns (y, mean, rstd); with_mask=True (ReLU, C % 8 == 0) also returns the 1-bit ReLU
     mask [K, R, C/8] uint8 that bn_bwd can read instead of y. `x` (and `residual`) may be
-    channel slices of a wider buffer ([K, R, C] at row stride ld); y is contiguous."""
+    channel slices of a wider buffer ([K, R, C] at row stride ld); y is contiguous.
+    `pre_stats`: [K, parts, 2, C] Σx / Σx² partials written by the producing conv's epilogue
+    (conv_fwd(stats=)) — the statistics pass over x is skipped."""
     K, R, C = x.shape
     x, ldx = _pix_stride(x)
     assert x.stride(0) == R * ldx, "client stride of a strided BN input must be R*ld"
@@ -305,12 +321,16 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
         residual = residual.contiguous() if ldx == C else residual
         assert _pix_stride(residual)[1] == ldx and residual.stride() == x.stride()
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    if pre_stats is not None:
+        assert pre_stats.dtype == torch.float32 and pre_stats.is_contiguous()
+        assert pre_stats.shape[0] == K and pre_stats.shape[2:] == (2, C), pre_stats.shape
     mask = None
     if with_mask and relu and C % 8 == 0 and ldx % 8 == 0:
         mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
     assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
-              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx)
+              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx, _p(pre_stats),
+              0 if pre_stats is None else pre_stats.shape[1])
     if with_mask:
         return y, mean, rstd, mask
     return y, mean, rstd

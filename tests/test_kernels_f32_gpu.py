@@ -87,7 +87,7 @@ def test_conv_f32_every_variant(hip, case):
     for v in range(hip._C.conv_nt_f32_num_variants()):
         y = torch.empty_like(dy)
         hip._C.conv_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, B * H * W * Ci, M * Co, w.stride(0), 0, B, H, W,
-                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0)
+                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0, 0, 0)
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
@@ -342,3 +342,32 @@ def test_embedding_scale_pe_and_seq_mean(hip, dtype, tol):
     _close(hip.seq_mean_fwd(x, lengths), ref.seq_mean_fwd(_d(x), lengths.cpu()), tol)
     dp = _f(K, B, D).to(dtype)
     _close(hip.seq_mean_bwd(dp, lengths, L), ref.seq_mean_bwd(_d(dp), lengths.cpu(), L), tol)
+
+
+@pytest.mark.parametrize("case", [(3, 4, 8, 8, 16, 64, 3, 1, 1), (2, 5, 9, 9, 64, 128, 3, 2, 1),
+                                  (2, 3, 8, 8, 32, 256, 1, 1, 0)])
+def test_conv_epilogue_bn_stats(hip, case):
+    """fp32 conv epilogue writes the BN partial sums (per 32 GEMM rows, valid samples only):
+    their totals match fp64 sums over y, and bn_fwd(pre_stats=) equals bn_fwd's own pass."""
+    K, B, H, W, Ci, Co, k, s, p = case
+    x = _f(K, B, H, W, Ci)
+    w = _f(K, Co, k, k, Ci, scale=0.2)
+    valid = torch.tensor([B, B - 2, 1][:K], dtype=torch.int32, device=DEV)
+    OH = (H + 2 * p - k) // s + 1
+    M = B * OH * OH
+    stats = torch.full((K, hip.conv_stats_parts(M), 2, Co), float("nan"), device=DEV)
+    y = hip.conv_fwd(x, w, s, p, stats=stats, stats_valid=valid)
+    assert torch.isfinite(stats).all()  # every partial slot written
+    y3 = _d(y).reshape(K, M, Co)
+    for kk in range(K):
+        rows = int(valid[kk]) * OH * OH
+        _close(stats[kk, :, 0].double().sum(0), y3[kk, :rows].sum(0), 1e-5)
+        _close(stats[kk, :, 1].double().sum(0), (y3[kk, :rows] ** 2).sum(0), 1e-5)
+    g = torch.rand(K, Co, device=DEV) + 0.5
+    b = _f(K, Co)
+    vr = valid * OH * OH
+    ya, ma, ra, mka = hip.bn_fwd(y.reshape(K, M, Co), g, b, vr, True, None, with_mask=True)
+    yb, mb, rb, mkb = hip.bn_fwd(y.reshape(K, M, Co), g, b, vr, True, None, with_mask=True, pre_stats=stats)
+    _close(mb, ma, 1e-5)
+    _close(rb, ra, 1e-4)
+    _close(yb, ya, 1e-4)
