@@ -209,6 +209,12 @@ PYBIND11_MODULE(_dls_hip, m) {
                     P<const float>(lse), P<const int>(kv), P<void>(dq), P<void>(dk), P<void>(dv), P<float>(delta), KBH,
                     H, L, DH, f32, S(s), ldqkv, ldo);
   });
+  m.def("neighbor_sample", [](ptr rowptr, ptr col, ptr owner, ptr is_val, ptr nodes, ptr clients, int n, int fanout,
+                              unsigned long long seed_h, ptr out_nbr, ptr out_cnt, ptr s) {
+    neighbor_sample(P<const int>(rowptr), P<const int>(col), P<const int>(owner), P<const uint8_t>(is_val),
+                    P<const int64_t>(nodes), P<const int64_t>(clients), n, fanout, seed_h, P<int>(out_nbr),
+                    P<int>(out_cnt), S(s));
+  });
   m.def("spmm", [](ptr rowptr, ptr col, ptr val, ptr x, ptr y, int K, int N, int Nx, int F, long x_cs, long y_cs,
                    int f32, ptr s) {
     spmm(P<const int>(rowptr), P<const int>(col), P<const float>(val), P<const void>(x), P<void>(y), K, N, Nx, F, x_cs,

@@ -163,6 +163,15 @@ void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* 
 void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStream_t s);
 
 // ------------------------------------------------------------- FL / optimiser
+// ---------------------------------------------------------------- graph (graph.hip)
+// Federated-GNN neighbour sampling: per frontier row (nodes[t] expanded for client clients[t])
+// the `fanout` (<= 32) in-neighbours with the smallest hash keys; out_nbr [n][fanout] (-1 pad).
+// seed_h = hmix(step seed) (data/graph.py). rowptr / col: int32 in-neighbour CSR, owner [N]
+// client id of each training node (-1 otherwise), is_val [N].
+void neighbor_sample(const int* rowptr, const int* col, const int* owner, const uint8_t* is_val, const int64_t* nodes,
+                     const int64_t* clients, int n, int fanout, unsigned long long seed_h, int* out_nbr, int* out_cnt,
+                     hipStream_t s);
+
 void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
               const uint8_t* first, int K, long P, long ld, float wd, float momentum, float dampening, int nesterov,
               hipStream_t s);

@@ -1,28 +1,73 @@
-"""Synthetic graph datasets (node classification) + per-client graph views for federated GNNs.
+"""Synthetic graph datasets (node classification) and the federated-GNN batch machinery:
+device client graphs, device neighbour sampling, per-client subgraphs and the boundary-row
+(halo) exchange.
 
 Shapes follow the datasets named by the reference configs (`conf/fed_gnn/*`, `conf/fed_aas/*`:
 Coauthor_CS, Cora, PubMed, DBLP, Yelp, AmazonProducts, Reddit): node count, feature width,
 class count and average degree. Graphs are stochastic-block-model-like
 (edges mostly within a class), features are class-dependent sparse bag-of-words + noise.
 
-Per-client views reproduce the reference's `GraphWorker` edge rules
-(`worker/graph_worker.py:179-241,252-269`):
-* training nodes are split among clients (node-split federated GNN);
-* client k keeps in-client edges (both ends in T_k; Bernoulli-dropped with `edge_drop_rate`),
-  cross-client edges (src in T_k, dst in another client's training set) and validation edges;
-* with `share_feature`, layer 0 propagates over local edges only, layers ≥ 1 over all kept
-  edges with other clients' boundary embeddings substituted (zeros where unavailable,
-  `_get_cross_deivce_embedding`); without it every layer uses local edges only.
-Propagation uses GCN normalisation D^-½(A+I)D^-½ of each client's edge set; the K clients'
-edge sets are concatenated with a client offset so one gather/scatter covers the cohort.
+Federated node-split GNN, reference `worker/graph_worker.py` + `algorithm/graph_algorithm.py`:
+
+* Client graph (`ClientGraph`, reference `__clear_unrelated_edges` / `_clear_cross_client_edges`,
+  graph_worker.py:197-250). Training nodes are split among clients. Client k keeps:
+  - in-client edges (both ends in T_k), dropped per directed edge with `edge_drop_rate`;
+  - cross-client edges (a T_k node and another client's training node), with `share_feature`;
+  - validation edges.
+  Every training node has ONE owner, so all clients' views are a single in-neighbour CSR over
+  the N nodes. Row v holds:
+  - for an owned v: its owner's kept neighbours;
+  - for a validation v: its validation neighbours.
+  Client k may expand v iff v ∈ T_k or v is a validation node. The whole CSR is built on
+  device with vectorised filters (no per-client host loops).
+* Neighbour sampling (`sample_neighbors`; reference `batch_number` / `num_neighbor` loader,
+  graph_worker.py:95-101). Per hop, each frontier node keeps up to `fanout` in-neighbours
+  without replacement (all of them for `fanout` < 0): the `fanout` smallest of a hash key over
+  (step seed, client, node, position). The HIP kernel (csrc/graph.hip) and the torch version
+  below select identical sets in identical order, on any device and any rank layout. New nodes
+  are deduplicated and relabelled per client on device (sort + searchsorted).
+* Subgraph batch (`Subgraph`). The K clients' sampled subgraphs are padded to one
+  [K, Nmax] node table (seeds first: logits = rows [:, :B]). Their edges form one
+  block-diagonal edge set over K·Nmax rows for the native SpMM. GCN normalisation (+ self
+  loops) is per subgraph, as PyG GCNConv on a sampled batch. Layer 0 sees local-node edges only
+  (reference `_clear_cross_client_edge_on_the_fly`); layers ≥ 1 see every sampled edge.
+* Halo (`HaloExchange`, reference `_pass_node_feature` / `_get_cross_deivce_embedding` and the
+  server relay `graph_algorithm.py:66-88`). Before each layer ≥ 1:
+  - a client publishes its own boundary nodes present in its batch;
+  - every other client's row for such a node gets the owner's (detached) embedding;
+  - every non-own row without one is zeroed.
+  Within a rank this is a device gather over the cohort. Across ranks the requested rows travel
+  with `all_to_all_single`: request counts, then node ids to the owner's rank, then the rows back.
+  Only the rows somebody asked for cross xGMI, as the reference server relays only requested
+  nodes.
 """
 
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 
 import torch
+
+_M31 = 0x7FFFFFFF
+_HMUL = 0x45D9F3B
+
+
+# ------------------------------------------------------------------------ hashing
+def hmix(h: torch.Tensor) -> torch.Tensor:
+    """31-bit integer mixer on int64 tensors (same arithmetic as `hmix` in csrc/graph.hip)."""
+    h = h & _M31
+    h = h ^ (h >> 16)
+    h = (h * _HMUL) & _M31
+    h = h ^ (h >> 16)
+    h = (h * _HMUL) & _M31
+    return h ^ (h >> 16)
+
+
+def hkey(seed: int, *xs: torch.Tensor) -> torch.Tensor:
+    h = hmix(torch.as_tensor(seed & _M31, dtype=torch.int64))
+    for x in xs:
+        h = hmix(h + x.long())
+    return h
 
 
 def _coalesce(src: torch.Tensor, dst: torch.Tensor, n: int):
@@ -30,9 +75,10 @@ def _coalesce(src: torch.Tensor, dst: torch.Tensor, n: int):
     return (key // n), (key % n)
 
 
+# ------------------------------------------------------------------------ edge sets
 @dataclass
 class EdgeSet:
-    """Concatenated normalised edges of K client graphs over N nodes (flat ids k*N+i)."""
+    """Normalised edges of K graphs over N nodes each (flat ids k*N+i; K = 1: one shared graph)."""
 
     src: torch.Tensor  # int64 [E]
     dst: torch.Tensor  # int64 [E]
@@ -41,8 +87,7 @@ class EdgeSet:
     N: int
 
     def csr(self) -> "CSRPair":
-        """CSR of Â (rows = dst, over K·N flat rows, or N when the graph is shared) and of Âᵀ
-        (for the backward), built once per edge set for the native SpMM kernel."""
+        """CSR of Â (rows = dst) and of Âᵀ (for the backward), built once per edge set."""
         cached = getattr(self, "_csr", None)
         if cached is None:
             rows = self.N * self.K
@@ -69,9 +114,10 @@ def _to_csr(row: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_rows: int
     return rowptr, col[order].to(torch.int32), val[order].float()
 
 
-def gcn_norm(src: torch.Tensor, dst: torch.Tensor, n: int):
-    """Self loops + symmetric normalisation (PyG `gcn_norm`); messages flow src -> dst."""
-    loops = torch.arange(n, device=src.device)
+def gcn_norm(src: torch.Tensor, dst: torch.Tensor, n: int, rows: torch.Tensor | None = None):
+    """Self loops + symmetric normalisation (PyG `gcn_norm`); messages flow src -> dst. `rows`:
+    the node ids that get a self loop (default all n)."""
+    loops = torch.arange(n, device=src.device) if rows is None else rows
     s = torch.cat([src, loops])
     d = torch.cat([dst, loops])
     deg = torch.zeros(n, device=src.device).index_add_(0, d, torch.ones_like(d, dtype=torch.float32))
@@ -79,6 +125,15 @@ def gcn_norm(src: torch.Tensor, dst: torch.Tensor, n: int):
     return s, d, dinv[s] * dinv[d]
 
 
+def _csr_from_edges(src: torch.Tensor, dst: torch.Tensor, n: int):
+    """In-neighbour CSR (row = dst, col = src), int64 rowptr."""
+    order = torch.argsort(dst, stable=True)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dst.device)
+    rowptr[1:] = torch.bincount(dst, minlength=n).cumsum(0)
+    return rowptr, src[order]
+
+
+# ------------------------------------------------------------------------ dataset
 class GraphDataset:
     def __init__(self, spec, seed: int, device, dtype=torch.float32):
         self.spec = spec
@@ -89,29 +144,30 @@ class GraphDataset:
         self.num_nodes = N
         y = torch.randint(0, C, (N,), generator=g)
         E = max(N, N * max(spec.avg_degree, 2) // 2)
-        E = min(E, 20_000_000)
+        E = min(E, 40_000_000)
         u = torch.randint(0, N, (E,), generator=g)
-        # 80 % of edges stay within the source node's class
-        by_class = [torch.nonzero(y == c).flatten() for c in range(C)]
+        # 80 % of edges stay within the source node's class: class-sorted node table, one draw
         same = torch.rand(E, generator=g) < 0.8
         v = torch.randint(0, N, (E,), generator=g)
-        for c in range(C):
-            sel = same & (y[u] == c)
-            cnt = int(sel.sum())
-            if cnt and by_class[c].numel():
-                v[sel] = by_class[c][torch.randint(0, by_class[c].numel(), (cnt,), generator=g)]
+        order = torch.argsort(y, stable=True)
+        cnt = torch.bincount(y, minlength=C)
+        start = torch.cumsum(cnt, 0) - cnt
+        cu = y[u]
+        r = (torch.rand(E, generator=g) * cnt[cu].clamp(min=1)).long().clamp(max=(cnt[cu] - 1).clamp(min=0))
+        v = torch.where(same & (cnt[cu] > 0), order[start[cu] + r], v)
         keep = u != v
         u, v = u[keep], v[keep]
         src, dst = _coalesce(torch.cat([u, v]), torch.cat([v, u]), N)  # undirected
         self.src, self.dst = src, dst
-        # features: class-specific active words + random words
+        # features: class-specific active words + random words, row-normalised
         words = max(F // (4 * C), 1)
         proto = torch.zeros(C, F)
         for c in range(C):
             proto[c, torch.randint(0, F, (words,), generator=g)] = 1.0
-        x = proto[y] * 1.0 + (torch.rand(N, F, generator=g) < (2.0 / max(F, 1))).float()
+        x = proto[y] + (torch.rand(N, F, generator=g) < (2.0 / max(F, 1))).float()
         x = x / x.sum(1, keepdim=True).clamp(min=1)
         self.x = x.to(self.device, dtype)
+        del x
         self.labels_cpu = y.to(torch.int32)
         self.labels_dev = self.labels_cpu.to(self.device)
         perm = torch.randperm(N, generator=g)
@@ -122,27 +178,33 @@ class GraphDataset:
         self.n = ntr
         # the "labels" used by the partitioners are those of the training nodes
         self.labels = self.labels_cpu[self.train_nodes]
-        fs, fd, fv = gcn_norm(src, dst, N)
-        self.full = EdgeSet(fs.to(self.device), fd.to(self.device), fv.to(self.device), 1, N)
-        self.views: ClientGraphViews | None = None
+        self._full: EdgeSet | None = None
+        self.client_graph: ClientGraph | None = None
+        self.sampler = None  # SubgraphSampler of the running round (GraphWorker)
+        self.halo = None  # HaloExchange of the running round (GraphWorker)
+
+    @property
+    def full(self) -> EdgeSet:
+        """The whole graph, GCN-normalised (server-side evaluation)."""
+        if self._full is None:
+            fs, fd, fv = gcn_norm(self.src.to(self.device), self.dst.to(self.device), self.num_nodes)
+            self._full = EdgeSet(fs, fd, fv, 1, self.num_nodes)
+        return self._full
 
     # partitioners work on positions inside train_nodes -> map to node ids
     def node_ids(self, positions: torch.Tensor) -> torch.Tensor:
         return self.train_nodes[positions.long()]
 
     def gather_labels(self, idx):
-        return self.labels_dev.index_select(0, idx.reshape(-1).long()).reshape(idx.shape)
+        return self.labels_dev.index_select(0, idx.reshape(-1).long().clamp(min=0)).reshape(idx.shape)
 
     def labels_for(self, idx):
         return self.gather_labels(idx)
 
     # ---- trainer hooks (input_kind == "graph")
     def batch(self, idx: torch.Tensor) -> "GraphBatch":
-        v = self.views
-        assert v is not None, "client graph views not built (GraphWorker._before_training)"
-        return GraphBatch(self.x, v.l0, v.l1, idx, v, self.comm)
-
-    comm = None
+        assert self.sampler is not None, "no subgraph sampler (GraphWorker sets one per round)"
+        return GraphBatch(self.x, None, self.sampler.sample(idx), self.halo)
 
     @torch.no_grad()
     def evaluate(self, trainer, theta_rows: torch.Tensor, shard=(0, 1)):
@@ -159,7 +221,7 @@ class GraphDataset:
         params = BoundParams(trainer.layout, compute, None, K=M)
         ctx = RunCtx(params, None, training=False)
         seeds = nodes.unsqueeze(0).expand(M, -1)
-        logits = trainer.model.forward(GraphBatch(self.x, self.full, self.full, seeds, None), ctx)
+        logits = trainer.model.forward(GraphBatch(self.x, self.full, None, None, seeds), ctx)
         labels = self.gather_labels(seeds)
         valid = torch.full((M,), seeds.shape[1], dtype=torch.int32, device=self.device)
         loss, correct = Fn.cross_entropy(logits.contiguous(), labels, valid)
@@ -167,83 +229,314 @@ class GraphDataset:
         return loss * seeds.shape[1], correct, n_total
 
 
-class ClientGraphViews:
-    """Edge sets of a cohort of clients (wave), built once per wave on device."""
+# ------------------------------------------------------------------------ client graph
+class ClientGraph:
+    """All clients' kept edges as one device in-neighbour CSR (see module doc)."""
 
-    def __init__(self, ds: GraphDataset, owner: torch.Tensor, clients: list[int], share_feature: bool,
-                 edge_drop_rate: float | None, seed: int):
-        N = ds.num_nodes
+    def __init__(self, ds: GraphDataset, owner: torch.Tensor, share_feature: bool, edge_drop_rate: float | None,
+                 seed: int, worker_number: int):
         dev = ds.device
-        self.ds = ds
-        self.clients = clients
-        self.K = len(clients)
+        N = ds.num_nodes
+        self.N = N
         self.share_feature = share_feature
-        src, dst = ds.src, ds.dst
-        val_mask = torch.zeros(N, dtype=torch.bool)
-        val_mask[ds.val_nodes] = True
-        is_train = owner >= 0
-        l0_s, l0_d, l1_s, l1_d = [], [], [], []
-        self.stats = []
-        keep_masks = []
-        for i, c in enumerate(clients):
-            own = owner == c
-            in_client = own[src] & own[dst]
-            orig_in = int(in_client.sum())
-            if edge_drop_rate:
-                g = torch.Generator().manual_seed(seed * 7919 + c)
-                in_client &= torch.rand(in_client.shape, generator=g) >= edge_drop_rate
-            cross = own[src] & is_train[dst] & ~own[dst]
-            val_e = val_mask[src] & val_mask[dst]
-            local = in_client | val_e
-            full = local | cross
-            self.stats.append({"original_in_client_training_edge_cnt": orig_in,
-                               "in_client_training_edge_cnt": int(in_client.sum()),
-                               "cross_client_training_edge_cnt": int(cross.sum()),
-                               "training_node_cnt": int(own.sum()),
-                               "validation_node_cnt": int(val_mask.sum())})
-            # messages flow src -> dst; a client aggregates into its own nodes
-            s0, d0, v0 = gcn_norm(dst[local], src[local], N)
-            s1, d1, v1 = gcn_norm(dst[full], src[full], N)
-            l0_s.append((s0, d0, v0))
-            l1_s.append((s1, d1, v1))
-            keep_masks.append(own)
-        self.l0 = self._concat(l0_s, N, dev)
-        self.l1 = self._concat(l1_s if share_feature else l0_s, N, dev)
-        # halo substitution plan for layers >= 1 (reference `_get_cross_deivce_embedding`):
-        # own training nodes keep their embedding; other clients' boundary nodes that this
-        # client's kept edges touch get the owner's embedding; every other node gets zero.
-        boundary = torch.zeros(N, dtype=torch.bool)
-        cross_all = is_train[src] & is_train[dst] & (owner[src] != owner[dst])
-        boundary[src[cross_all]] = True  # training nodes with an edge into another client
-        self.boundary_nodes = torch.nonzero(boundary).flatten()
-        self.owner = owner
-        own_rows = torch.stack(keep_masks)  # [K, N]
-        remote = torch.zeros((self.K, N), dtype=torch.bool)
-        for i, c in enumerate(clients):
-            own = owner == c
-            cross = own[src] & is_train[dst] & ~own[dst]
-            req = torch.zeros(N, dtype=torch.bool)
-            req[dst[cross]] = True
-            remote[i] = req & boundary
-        self.keep = own_rows.to(dev)
-        self.remote = remote.to(dev)
-        self.boundary_nodes_dev = self.boundary_nodes.to(dev)
-        pos = torch.full((N,), -1, dtype=torch.int64)
-        for i, c in enumerate(clients):
-            pos[owner == c] = i
-        self.client_pos = pos.to(dev)
-        self.boundary_cnt = [int((own_rows[i] & boundary).sum()) for i in range(self.K)]
+        src, dst = ds.src.to(dev), ds.dst.to(dev)  # directed, both orientations; message u=src -> v=dst
+        own = owner.to(dev)
+        is_val = torch.zeros(N, dtype=torch.bool, device=dev)
+        is_val[ds.val_nodes.to(dev)] = True
+        ov, ou = own[dst], own[src]
+        in_client = (ov >= 0) & (ou == ov)
+        W = worker_number
 
-    @staticmethod
-    def _concat(parts, N, dev) -> EdgeSet:
-        src = torch.cat([p[0] + i * N for i, p in enumerate(parts)])
-        dst = torch.cat([p[1] + i * N for i, p in enumerate(parts)])
-        val = torch.cat([p[2] for p in parts])
-        return EdgeSet(src.to(dev), dst.to(dev), val.to(dev), len(parts), N)
+        def per_client(mask):
+            return torch.bincount(ov[mask], minlength=W).cpu().tolist()
+
+        orig_in = per_client(in_client)
+        if edge_drop_rate:
+            thr = int(float(edge_drop_rate) * (_M31 + 1))
+            in_client = in_client & (hkey(seed * 7919 + 13, src, dst) >= thr)
+        cross = (ov >= 0) & (ou >= 0) & (ou != ov)
+        val_e = is_val[src] & is_val[dst]
+        keep = in_client | val_e | (cross if share_feature else torch.zeros_like(cross))
+        self.rowptr, self.col = _csr_from_edges(src[keep], dst[keep], N)
+        self.rowptr32 = self.rowptr.to(torch.int32)
+        self.col32 = self.col.to(torch.int32)
+        self.owner = own
+        self.owner32 = own.to(torch.int32)
+        self.is_val = is_val
+        self.is_val_u8 = is_val.to(torch.uint8)
+        # training nodes with a neighbour owned by another client (reference training_node_boundary)
+        self.boundary = torch.zeros(N, dtype=torch.bool, device=dev)
+        self.boundary[src[cross]] = True
+        n_train = torch.bincount(own[own >= 0], minlength=W).cpu().tolist()
+        in_cnt, cross_cnt = per_client(in_client), per_client(cross)
+        n_val = int(is_val.sum())
+        self.stats = [{"original_in_client_training_edge_cnt": orig_in[c], "in_client_training_edge_cnt": in_cnt[c],
+                       "cross_client_training_edge_cnt": cross_cnt[c], "training_node_cnt": n_train[c],
+                       "validation_node_cnt": n_val} for c in range(W)]
+        del src, dst, ov, ou
 
 
+# ------------------------------------------------------------------------ sampling
+def sample_neighbors_torch(cg: ClientGraph, nodes: torch.Tensor, clients: torch.Tensor, fanout: int, seed: int):
+    """(neighbour ids, frontier row) of every kept sample; see module doc for the rule."""
+    allowed = (cg.owner[nodes] == clients) | cg.is_val[nodes]
+    start = cg.rowptr[nodes]
+    deg = torch.where(allowed, cg.rowptr[nodes + 1] - start, torch.zeros_like(start))
+    total = int(deg.sum())
+    dev = nodes.device
+    if total == 0:
+        e = torch.empty(0, dtype=torch.int64, device=dev)
+        return e, e
+    row = torch.repeat_interleave(torch.arange(nodes.numel(), device=dev), deg)
+    off = torch.cumsum(deg, 0) - deg
+    pos = torch.arange(total, device=dev) - off[row]
+    nbr = cg.col[start[row] + pos]
+    if fanout < 0:
+        return nbr, row
+    key = hkey(seed, clients[row], nodes[row], pos)
+    order = torch.argsort(row * (_M31 + 1) + key, stable=True)  # by row, then key, then position
+    rank = torch.arange(total, device=dev) - off[row[order]]
+    sel = order[rank < fanout]
+    return nbr[sel], row[sel]
+
+
+def sample_neighbors(cg: ClientGraph, nodes: torch.Tensor, clients: torch.Tensor, fanout: int, seed: int):
+    from ..ops import backend
+
+    if 0 < fanout <= 32 and backend.using_hip(cg.rowptr):
+        from ..ops import hip
+
+        return hip.neighbor_sample(cg.rowptr32, cg.col32, cg.owner32, cg.is_val_u8, nodes, clients, fanout, seed)
+    return sample_neighbors_torch(cg, nodes, clients, fanout, seed)
+
+
+@dataclass
+class Subgraph:
+    """K clients' sampled subgraphs over one padded node table (see module doc)."""
+
+    nid: torch.Tensor  # [K, Nmax] global node ids (-1: padding)
+    count: torch.Tensor  # [K] nodes per client
+    B: int  # seed slots (rows [:, :B])
+    l0: EdgeSet  # layer 0: local-node edges
+    l1: EdgeSet  # layers >= 1: all sampled edges
+    own: torch.Tensor  # [K, Nmax] node owned by the row's client
+    publish: torch.Tensor  # [K, Nmax] own boundary node (its embedding is sent)
+    remote: torch.Tensor  # [K, Nmax] another client's training node (embedding requested)
+    K: int
+    nmax: int
+
+
+def build_subgraph(cg: ClientGraph, seeds: torch.Tensor, clients: torch.Tensor, fanouts: list[int],
+                   seed: int) -> Subgraph:
+    """seeds [K, B] global ids (-1: empty slot), clients [K] client ids, one fanout per hop."""
+    K, B = seeds.shape
+    N = cg.N
+    dev = seeds.device
+    rowk = torch.arange(K, device=dev).unsqueeze(1).expand(K, B)
+    slot = torch.arange(B, device=dev).unsqueeze(0).expand(K, B)
+    ok = seeds >= 0
+    keys = (rowk * N + seeds)[ok]
+    order = torch.argsort(keys)
+    tab_keys, tab_local = keys[order], slot[ok][order]
+    count = torch.full((K,), B, dtype=torch.int64, device=dev)
+    fr_k, fr_g, fr_l = rowk[ok], seeds[ok], slot[ok]
+    es, ed, ek, eg_s, eg_d = [], [], [], [], []
+    for hop, f in enumerate(fanouts):
+        if fr_g.numel() == 0:
+            break
+        nb_g, nb_row = sample_neighbors(cg, fr_g, clients[fr_k], int(f), seed + 7919 * hop)
+        if nb_g.numel() == 0:
+            break
+        nb_k = fr_k[nb_row]
+        nkeys = nb_k * N + nb_g
+        uniq = torch.unique(nkeys)
+        p = torch.searchsorted(tab_keys, uniq).clamp(max=tab_keys.numel() - 1)
+        new = uniq[tab_keys[p] != uniq]
+        new_k = new // N
+        cnt_new = torch.bincount(new_k, minlength=K)
+        first = torch.cumsum(cnt_new, 0) - cnt_new
+        new_local = count[new_k] + torch.arange(new.numel(), device=dev) - first[new_k]
+        count = count + cnt_new
+        tab_keys, o = torch.sort(torch.cat([tab_keys, new]))
+        tab_local = torch.cat([tab_local, new_local])[o]
+        src_l = tab_local[torch.searchsorted(tab_keys, nkeys)]
+        es.append(src_l)
+        ed.append(fr_l[nb_row])
+        ek.append(nb_k)
+        eg_s.append(nb_g)
+        eg_d.append(fr_g[nb_row])
+        fr_k, fr_g, fr_l = new_k, new % N, new_local
+    nmax = int(count.max()) if K else B
+    nid = torch.full((K, nmax), -1, dtype=torch.int64, device=dev)
+    nid[tab_keys // N, tab_local] = tab_keys % N
+    cl = clients.unsqueeze(1)
+    g = nid.clamp(min=0)
+    real = nid >= 0
+    own = real & (cg.owner[g] == cl)
+    publish = own & cg.boundary[g]
+    remote = real & (cg.owner[g] >= 0) & ~own
+    cat = (lambda xs: torch.cat(xs)) if es else (lambda xs: torch.empty(0, dtype=torch.int64, device=dev))
+    src_l, dst_l, e_k, gs, gd = cat(es), cat(ed), cat(ek), cat(eg_s), cat(eg_d)
+    flat_s, flat_d = e_k * nmax + src_l, e_k * nmax + dst_l
+    loops = torch.nonzero(real.flatten()).flatten()
+    total = K * nmax
+    s1, d1, v1 = gcn_norm(flat_s, flat_d, total, loops)
+    if cg.share_feature:
+        ck = clients[e_k]
+        local = ((cg.owner[gs] == ck) | cg.is_val[gs]) & ((cg.owner[gd] == ck) | cg.is_val[gd])
+        s0, d0, v0 = gcn_norm(flat_s[local], flat_d[local], total, loops)
+        l0 = EdgeSet(s0, d0, v0, K, nmax)
+    else:
+        l0 = None
+    l1 = EdgeSet(s1, d1, v1, K, nmax)
+    return Subgraph(nid, count, B, l0 if l0 is not None else l1, l1, own, publish, remote, K, nmax)
+
+
+class SubgraphSampler:
+    """Per-round sampler: every `sample(idx)` call is one training batch of the cohort."""
+
+    def __init__(self, cg: ClientGraph, clients: list[int], fanouts: list[int], seed: int, valid_fn=None):
+        self.cg = cg
+        self.clients = torch.tensor(clients, dtype=torch.int64, device=cg.owner.device)
+        self.fanouts = fanouts
+        self.seed = seed
+        self.calls = 0
+        self.valid_fn = valid_fn  # step -> [K] valid seed counts (padded schedule slots are empty)
+
+    def sample(self, idx: torch.Tensor) -> Subgraph:
+        seeds = idx.to(self.cg.owner.device).long()
+        if self.valid_fn is not None:
+            n = self.valid_fn(self.calls)
+            if n is not None:
+                slot = torch.arange(seeds.shape[1], device=seeds.device).unsqueeze(0)
+                seeds = torch.where(slot < n.to(seeds.device).unsqueeze(1), seeds, torch.full_like(seeds, -1))
+        sub = build_subgraph(self.cg, seeds, self.clients, self.fanouts, (self.seed + 104_729 * self.calls) & _M31)
+        self.calls += 1
+        return sub
+
+
+# ------------------------------------------------------------------------ halo exchange
+class HaloExchange:
+    """Boundary-embedding exchange before every GCN layer ≥ 1 of a training batch."""
+
+    def __init__(self, cg: ClientGraph, comm, client_rank: torch.Tensor | None, policy=None):
+        self.cg = cg
+        self.comm = comm
+        self.client_rank = client_rank  # [W] rank hosting each client this round (-1: not active)
+        self.policy = policy  # fed_aas: decides per batch whether to exchange (None: always)
+        self.sent_rows = torch.zeros((), dtype=torch.float64, device=cg.owner.device)  # Σ published rows·width
+        self.skipped_rows = torch.zeros((), dtype=torch.float64, device=cg.owner.device)
+        self.last_skip = False
+
+    def begin_batch(self) -> bool:
+        """Collective decision for this batch (all ranks call it once per batch)."""
+        self.last_skip = bool(self.policy is not None and self.policy.skip())
+        return not self.last_skip
+
+    def __call__(self, h: torch.Tensor, sub: Subgraph) -> torch.Tensor:
+        K, nmax, F = h.shape
+        flat = h.detach().reshape(K * nmax, F)
+        nid = sub.nid.reshape(-1)
+        own = sub.own.reshape(-1)
+        n_pub = sub.publish.sum()
+        if self.last_skip:
+            self.skipped_rows += n_pub.double() * F
+            return torch.where(sub.own.unsqueeze(-1), h, torch.zeros_like(h))
+        self.sent_rows += n_pub.double() * F
+        N = self.cg.N
+        pub_rows = torch.nonzero(sub.publish.reshape(-1)).flatten()
+        table = torch.full((N,), -1, dtype=torch.int64, device=h.device)
+        table[nid[pub_rows]] = pub_rows
+        vals = torch.zeros_like(flat)
+        rem = torch.nonzero(sub.remote.reshape(-1)).flatten()
+        rem_g = nid[rem]
+        src = table[rem_g]
+        hit = src >= 0
+        vals[rem[hit]] = flat[src[hit]]
+        if self.comm is not None and self.comm.world > 1:
+            self._exchange(flat, table, rem[~hit], rem_g[~hit], vals)
+        if self.policy is not None:
+            self.policy.observe(flat[pub_rows], self.comm)
+        return torch.where(own.view(K, nmax, 1), h, vals.view(K, nmax, F))
+
+    def _exchange(self, flat, table, rows, gids, vals):
+        """Rows owned by clients on other ranks: ids to the owner's rank, embeddings back."""
+        comm = self.comm
+        W, me = comm.world, comm.rank
+        dev = flat.device
+        F = flat.shape[1]
+        owner_rank = self.client_rank[self.cg.owner[gids]]
+        far = (owner_rank >= 0) & (owner_rank != me)  # (owners not active this round: zeros)
+        gids_far, rows_far = gids[far], rows[far]
+        need, inv = torch.unique(gids_far, return_inverse=True)  # one request per node
+        need_rank = self.client_rank[self.cg.owner[need]]
+        order = torch.argsort(need_rank, stable=True)
+        need, need_rank = need[order], need_rank[order]
+        pos_of = torch.empty_like(order)
+        pos_of[order] = torch.arange(order.numel(), device=dev)
+        send_cnt = torch.bincount(need_rank, minlength=W)
+        recv_cnt = torch.empty_like(send_cnt)
+        comm.all_to_all_single(recv_cnt, send_cnt)
+        sc, rc = send_cnt.cpu().tolist(), recv_cnt.cpu().tolist()
+        req_in = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+        comm.all_to_all_single(req_in, need.contiguous(), rc, sc)
+        # answer: the owner's published row, zeros when the node is not in the owner's batch
+        src = table[req_in]
+        ans = torch.zeros((req_in.numel(), F), dtype=flat.dtype, device=dev)
+        okr = src >= 0
+        ans[okr] = flat[src[okr]]
+        got = torch.empty((need.numel(), F), dtype=flat.dtype, device=dev)
+        comm.all_to_all_single(got, ans, sc, rc)
+        if rows_far.numel():
+            vals[rows_far] = got[pos_of[inv]]
+
+
+class AdaptiveSkipPolicy:
+    """fed_aas (defined here — the reference ships only its configs): the boundary-embedding
+    exchange runs every `period` batches. After each exchange the relative change of the mean
+    published-embedding norm (all ranks' rows, one all-reduce) is compared with `threshold`:
+    below it the period doubles (up to `max_period`), above it halves. A skipped batch drops
+    cross-client edges for that batch (reference `_clear_cross_client_edge_on_the_fly`, whose
+    skipped bytes it records). The decision is identical on every rank."""
+
+    def __init__(self, threshold: float = 0.05, max_period: int = 8):
+        self.threshold = float(threshold)
+        self.max_period = int(max_period)
+        self.period = 1
+        self.step = 0
+        self.last_norm = None
+        self._pending: list = []
+
+    def skip(self) -> bool:
+        s = self.step
+        self.step += 1
+        if self._pending:
+            self._update()
+        return (s % self.period) != 0
+
+    def observe(self, rows: torch.Tensor, comm) -> None:
+        t = torch.stack([rows.double().norm(dim=1).sum() if rows.numel() else rows.new_zeros((), dtype=torch.float64),
+                         torch.tensor(float(rows.shape[0]), dtype=torch.float64, device=rows.device)])
+        if comm is not None and comm.world > 1:
+            comm.all_reduce_(t)
+        self._pending.append(t)
+
+    def _update(self) -> None:
+        t = torch.stack(self._pending).sum(0).cpu().tolist()
+        self._pending.clear()
+        norm = t[0] / max(t[1], 1.0)
+        if self.last_norm is not None and self.last_norm > 0:
+            rel = abs(norm - self.last_norm) / self.last_norm
+            if rel < self.threshold:
+                self.period = min(self.period * 2, self.max_period)
+            else:
+                self.period = max(1, self.period // 2)
+        self.last_norm = norm
+
+
+# ------------------------------------------------------------------------ batches
 def propagate(h: torch.Tensor, es: EdgeSet) -> torch.Tensor:
-    """out[k, i] = Σ_j Â_k[i, j] h[k, j]  (h [K, N, F]); differentiable gather + index_add."""
+    """out[k, i] = Σ_j Â_k[i, j] h[k, j]  (h [K, N, F]); native CSR SpMM or gather + index_add."""
     K, N, F = h.shape
     from ..ops import backend
 
@@ -265,33 +558,10 @@ def propagate(h: torch.Tensor, es: EdgeSet) -> torch.Tensor:
     return out.view(K, N, F)
 
 
-def substitute_halo(h: torch.Tensor, views: "ClientGraphViews", comm=None) -> torch.Tensor:
-    """Layer ≥ 1 input of client k: own training nodes keep h[k]; other clients' boundary
-    nodes that k's cross edges reach get the OWNER's embedding (detached: the reference ships
-    them through the server without gradient); every other node is zeroed.
-    Across ranks the boundary rows are merged with one all-reduce (M6/M8 → collective)."""
-    K, N, F = h.shape
-    hd = h.detach()
-    # boundary embeddings as computed by their owners (rows of the owning client)
-    pos = views.client_pos  # [N] row of the owning client in this cohort (-1 if remote/none)
-    bnd = views.boundary_nodes_dev
-    table = torch.zeros((N, F), dtype=h.dtype, device=h.device)
-    local_owned = pos[bnd] >= 0
-    rows = bnd[local_owned]
-    if rows.numel():
-        table[rows] = hd[pos[rows].long(), rows]
-    if comm is not None and comm.world > 1:
-        comm.all_reduce_(table)
-    keep = views.keep.unsqueeze(-1)
-    remote = views.remote.unsqueeze(-1)
-    return torch.where(keep, h, torch.where(remote, table.unsqueeze(0).expand(K, N, F), torch.zeros_like(h)))
-
-
 @dataclass
 class GraphBatch:
     x: torch.Tensor  # [N, F] shared node features
-    l0: EdgeSet
-    l1: EdgeSet
-    seeds: torch.Tensor | None  # [K, B] node ids whose logits are returned (None = all)
-    views: "ClientGraphViews | None" = None  # halo plan (None: no substitution)
-    comm: object = None
+    full: EdgeSet | None  # evaluation: the whole graph (shared by the K models)
+    sub: Subgraph | None  # training: the cohort's sampled subgraphs
+    halo: HaloExchange | None = None
+    seeds: torch.Tensor | None = None  # evaluation: [K, B] node ids whose logits are returned

@@ -1,19 +1,28 @@
-"""Federated GNN (node-split): `fed_gnn`, `fed_gcn` (share_feature forced) and the
-config-only `fed_aas` (treated as fed_gnn with its configs' defaults).
+"""Federated GNN (node-split): `fed_gnn`, `fed_gcn` (share_feature forced) and `fed_aas`
+(adaptive skipping of the embedding exchange).
 
 Reference `worker/graph_worker.py` + `algorithm/graph_algorithm.py` + `server/graph_server.py`
-(SURVEY C16/C19/C22, §3.6): training nodes are split among clients; each client trains a GCN
-on its kept edges; with `share_feature`, message-passing layers ≥ 1 see the boundary-node
-embeddings computed by the other clients (exchanged every batch, every layer); GCN weights are
-FedAvg-aggregated per round; `graph_worker_stat.json` records edge counts and per-round
-communicated / skipped embedding bytes.
+(SURVEY C16/C19/C22, §3.6):
+- Training nodes are split among clients. Each client keeps its edge subset, trains a GCN on
+  `batch_number` neighbour-sampled mini-batches per epoch (`num_neighbor` per hop; all
+  neighbours when unset).
+- With `share_feature`, message-passing layers ≥ 1 use the boundary-node embeddings that their
+  owners computed in the same batch.
+- GCN weights are FedAvg-aggregated per round.
+- `graph_worker_stat.json` records edge counts and per-round communicated / skipped embedding bytes.
 
-MI355X-native: all clients of a rank run the GCN together over one concatenated edge list
-(client-offset node ids → one gather/scatter per layer), the node features are shared and the
-first layer is ONE GEMM against the concatenated client weights; the per-batch halo exchange
-is an on-device gather, merged across ranks with one all-reduce of the boundary table.
-Full-graph propagation per batch (loss on the batch's seed nodes); neighbour sampling
-(`num_neighbor`) is accepted and recorded but not applied (parity unpinned).
+MI355X-native (data/graph.py):
+- The clients' edge views are one device in-neighbour CSR.
+- Sampling is a HIP kernel, and the batch is the cohort's padded subgraphs (one batched GEMM
+  and one block-diagonal SpMM per layer).
+- The embedding relay is an on-device gather within the rank, plus an all-to-all of only the
+  requested boundary rows across ranks.
+
+fed_aas: the reference registers no implementation (its configs carry the fed_gnn keys). It
+is defined here as fed_gnn with an adaptive exchange period (`AdaptiveSkipPolicy`). Keys:
+`aas_threshold`, default 0.05; `aas_max_period`, default 8. Skipped batches drop cross-client
+edges and record skipped bytes (reference `_clear_cross_client_edge_on_the_fly`,
+graph_worker.py:252-269). Parity is unpinned.
 """
 
 from __future__ import annotations
@@ -25,7 +34,7 @@ import os
 import torch
 
 from ...algorithm.fed_avg_algorithm import FedAVGAlgorithm
-from ...data.graph import ClientGraphViews
+from ...data.graph import AdaptiveSkipPolicy, ClientGraph, HaloExchange, SubgraphSampler
 from ...server.aggregation_server import AggregationServer
 from ...utils.logging import get_logger
 from ...worker.aggregation_worker import AggregationWorker
@@ -42,73 +51,103 @@ class GraphWorker(AggregationWorker):
             else self.force_share_feature
         self._batch_number = int(ak.get("batch_number", 1) or 1)
         self._edge_drop_rate = ak.get("edge_drop_rate")
-        self._views: dict = {}
-        self._owner = None
+        nn = ak.get("num_neighbor", config.extra_hyper_parameters.get("num_neighbor", -1))
+        layers = len(session.model.root.convs)
+        self._fanouts = [int(f) for f in nn] if isinstance(nn, (list, tuple)) else [int(nn)] * layers
+        self._cg: ClientGraph | None = None
+        self._policy = None
+        self._schedule = None
         self._communicated_embedding_bytes = 0
+        self._skipped_embedding_bytes = 0
         self._aggregated_bytes = 0
         self._round_communicated_bytes: dict = {}
         self._round_skipped_bytes: dict = {}
         self._stats: dict = {}
-        ds = session.dc.graph
-        ds.comm = session.comm
 
     def shards(self, client_ids):
         ds = self.session.dc.graph
         return [ds.node_ids(self.session.practitioners[c].indices(self.session.dc.spec.name)) for c in client_ids]
 
-    def _ensure_owner(self):
-        if self._owner is None:
+    def _client_graph(self) -> ClientGraph:
+        if self._cg is None:
             ds = self.session.dc.graph
             owner = torch.full((ds.num_nodes,), -1, dtype=torch.int64)
             for c in range(self.config.worker_number):
                 owner[self.shards([c])[0]] = c
-            self._owner = owner
+            self._cg = ClientGraph(ds, owner, self._share_feature, self._edge_drop_rate, self.config.seed,
+                                   self.config.worker_number)
             if self.session.is_main:
-                get_logger().info("%s feature", "share" if self._share_feature else "not share")
+                get_logger().warning("%s feature", "share" if self._share_feature else "not share")
+        return self._cg
 
-    def _views_for(self, wave):
-        key = tuple(wave)
-        if key not in self._views:
-            self._ensure_owner()
-            self._views[key] = ClientGraphViews(self.session.dc.graph, self._owner, list(wave), self._share_feature,
-                                                self._edge_drop_rate, self.config.seed)
-        return self._views[key]
+    def run_round(self, round_num, theta_g, client_ids):
+        """All of this rank's clients form ONE cohort: the halo exchange couples the clients of a
+        batch, and every rank runs the same batch sequence (its collectives pair up)."""
+        self._round_num = round_num
+        if self._share_feature and self.session.comm.world > 1 and not client_ids:
+            raise RuntimeError("fed_gnn with share_feature needs at least one active client per rank")
+        if client_ids:
+            yield self.train_wave(round_num, theta_g, list(client_ids))
+        self._own_init = False
 
     def build_schedule(self, round_num, wave):
-        shards = self.shards(wave)
-        ds = self.session.dc.graph
-        # every rank runs the same number of steps (the halo all-reduce is collective)
+        # every rank runs the same number of steps: batch size from the largest shard of all clients
         max_shard = max(self.session.practitioners[c].dataset_size(self.session.dc.spec.name)
                         for c in range(self.config.worker_number))
         B = max(1, math.ceil(max_shard / self._batch_number))
         saved = self.trainer.hyper.batch_size
         self.trainer.hyper.batch_size = B
         try:
-            return self.trainer.build_schedule(shards, self.local_epochs(),
-                                               seed=self.config.seed * 100_003 + round_num * 1009, client_ids=list(wave),
-                                               min_steps_per_epoch=self._batch_number)
+            self._schedule = self.trainer.build_schedule(
+                self.shards(wave), self.local_epochs(), seed=self.config.seed * 100_003 + round_num * 1009,
+                client_ids=list(wave), min_steps_per_epoch=self._batch_number)
         finally:
             self.trainer.hyper.batch_size = saved
+        return self._schedule
+
+    def _client_ranks(self) -> torch.Tensor:
+        W = self.config.worker_number
+        ranks = torch.full((W,), -1, dtype=torch.int64)
+        active = getattr(self.session, "round_active", None) or list(range(W))
+        world = self.session.comm.world
+        for i, c in enumerate(active):  # Session.local_clients: selected[rank::world]
+            ranks[c] = i % world
+        return ranks.to(self.session.device)
 
     def train_wave(self, round_num, theta_g, wave):
-        views = self._views_for(wave)
-        self.session.dc.graph.views = views
-        msg = super().train_wave(round_num, theta_g, wave)
-        # embedding exchange accounting: per step, every layer >= 1, each client sends its
-        # boundary rows (reference `_pass_node_feature`, fp32 element size)
-        layers = len(self.session.model.root.convs)
-        hidden = [c.lin.fout for c in self.session.model.root.convs[:-1]]
-        steps = self._batch_number * self.local_epochs()
-        if self._share_feature and layers > 1:
-            per_step = sum(cnt * sum(hidden[: layers - 1]) * 4 for cnt in views.boundary_cnt)
-            self._communicated_embedding_bytes += per_step * steps
-            msg.wire_bytes = [w for w in msg.wire_bytes]
-            msg.extra["embedding_bytes"] = per_step * steps
+        cg = self._client_graph()
+        ds = self.session.dc.graph
+
+        def valid(step):
+            sch = self._schedule
+            return sch.counts[step] if sch is not None and step < sch.counts.shape[0] else None
+
+        ds.sampler = SubgraphSampler(cg, list(wave), self._fanouts,
+                                     (self.config.seed * 1_000_003 + round_num * 10_007) & 0x7FFFFFFF, valid)
+        ds.halo = HaloExchange(cg, self.session.comm, self._client_ranks(), self._policy) if self._share_feature \
+            else None
+        try:
+            msg = super().train_wave(round_num, theta_g, wave)
+        finally:
+            halo = ds.halo
+            ds.sampler = ds.halo = None
+        # embedding traffic (reference `_pass_node_feature`: own boundary rows in the batch x
+        # layer-input width x fp32 bytes, every layer >= 1 of every batch), summed over ranks
+        t = torch.zeros(2, dtype=torch.float64, device=self.session.device)
+        if halo is not None:
+            t[0] = halo.sent_rows * 4
+            t[1] = halo.skipped_rows * 4
+        self.session.comm.all_reduce_(t)
+        sent, skipped = (int(v) for v in t.cpu().tolist())
+        self._communicated_embedding_bytes += sent
+        self._skipped_embedding_bytes += skipped
+        msg.extra["embedding_bytes"] = sent
+        msg.extra["skipped_embedding_bytes"] = skipped
         self._aggregated_bytes += int(sum(msg.wire_bytes))
         self._round_communicated_bytes[round_num] = self._aggregated_bytes + self._communicated_embedding_bytes
-        self._round_skipped_bytes[round_num] = 0
-        for c, st in zip(wave, views.stats):
-            self._stats[c] = st
+        self._round_skipped_bytes[round_num] = self._skipped_embedding_bytes
+        for c in wave:
+            self._stats[c] = cg.stats[c]
         return msg
 
     def _after_training(self) -> None:
@@ -119,7 +158,10 @@ class GraphWorker(AggregationWorker):
         stat = {"per_client": {str(k): v for k, v in self._stats.items()},
                 "skipped_embedding_bytes": self._round_skipped_bytes,
                 "communicated_bytes": self._round_communicated_bytes,
+                "fanouts": self._fanouts, "batch_number": self._batch_number,
                 "model_bytes": model_bytes}
+        if self._policy is not None:
+            stat["aas_final_period"] = self._policy.period
         with open(os.path.join(self.save_dir, "graph_worker_stat.json"), "wt", encoding="utf8") as f:
             json.dump(stat, f)
 
@@ -130,11 +172,20 @@ class FedGCNWorker(GraphWorker):
     force_share_feature = True
 
 
+class FedAASWorker(GraphWorker):
+    """fed_aas: fed_gnn whose embedding exchange runs on an adaptive period (see module doc)."""
+
+    def __init__(self, config, endpoint, session=None, **kwargs):
+        super().__init__(config, endpoint, session, **kwargs)
+        ak = config.algorithm_kwargs
+        self._policy = AdaptiveSkipPolicy(ak.get("aas_threshold", 0.05), ak.get("aas_max_period", 8))
+
+
 class GraphNodeServer(AggregationServer):
     """Reference `server/graph_server.py:5-7`: FedAvg of the GCN weights; the embedding
-    relay is the on-device halo table (no server round trip)."""
+    relay is the device halo exchange (no server round trip)."""
 
 
-for _name, _client in (("fed_gnn", GraphWorker), ("fed_gcn", FedGCNWorker), ("fed_aas", GraphWorker)):
+for _name, _client in (("fed_gnn", GraphWorker), ("fed_gcn", FedGCNWorker), ("fed_aas", FedAASWorker)):
     CentralizedAlgorithmFactory.register_algorithm(
         algorithm_name=_name, client_cls=_client, server_cls=GraphNodeServer, algorithm_cls=FedAVGAlgorithm)

@@ -392,20 +392,34 @@ class GCNNet(Module):
         self.convs = [self.child(f"conv{i + 1}", GCNConv(dims[i], dims[i + 1])) for i in range(layers)]
 
     def forward(self, batch, ctx):
-        from ..data.graph import substitute_halo
-
-        h = batch.x
         K = ctx.P.K
+        last = len(self.convs) - 1
+        if batch.sub is None:  # evaluation: the whole graph, shared by the K models
+            h = batch.x
+            for i, c in enumerate(self.convs):
+                h = c.forward(h, ctx, batch.full, K)
+                if i < last:
+                    h = torch.relu(h)
+            idx = batch.seeds.long().unsqueeze(-1).expand(-1, -1, h.shape[-1])
+            return torch.gather(h, 1, idx)
+        # training: the cohort's sampled subgraphs ([K, Nmax] node table, seeds in rows [:, :B])
+        sub, halo = batch.sub, batch.halo
+        share = halo is not None and halo.cg.share_feature
+        if share:
+            halo.begin_batch()  # (fed_aas: exchange or skip this batch, same on every rank)
+        real = (sub.nid >= 0).unsqueeze(-1)
+        h = batch.x.index_select(0, sub.nid.clamp(min=0).reshape(-1)).view(K, sub.nmax, -1)
+        h = torch.where(real, h, torch.zeros_like(h))
         for i, c in enumerate(self.convs):
-            if i > 0 and batch.views is not None and batch.views.share_feature:
-                h = substitute_halo(h, batch.views, batch.comm)
-            h = c.forward(h, ctx, batch.l0 if i == 0 else batch.l1, K)
-            if i + 1 < len(self.convs):
+            edges = sub.l0 if i == 0 else sub.l1
+            if i > 0 and share:
+                h = halo(h, sub)  # boundary embeddings of the other clients (detached)
+                if halo.last_skip:
+                    edges = sub.l0  # skipped exchange: no cross-client edges this batch
+            h = c.forward(h, ctx, edges, K)
+            if i < last:
                 h = torch.relu(h)
-        if batch.seeds is None:
-            return h
-        idx = batch.seeds.long().unsqueeze(-1).expand(-1, -1, h.shape[-1])
-        return torch.gather(h, 1, idx)
+        return h[:, : sub.B].contiguous()
 
 
 # --------------------------------------------------------------------------- build

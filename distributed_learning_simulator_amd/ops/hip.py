@@ -586,6 +586,34 @@ def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None):
     return dqkv
 
 
+# ---------------------------------------------------------------------- GNN sampling
+def _hmix_int(h: int) -> int:
+    h &= 0x7FFFFFFF
+    h ^= h >> 16
+    h = (h * 0x45D9F3B) & 0x7FFFFFFF
+    h ^= h >> 16
+    h = (h * 0x45D9F3B) & 0x7FFFFFFF
+    return h ^ (h >> 16)
+
+
+def neighbor_sample(rowptr32, col32, owner32, is_val_u8, nodes, clients, fanout: int, seed: int):
+    """csrc/graph.hip: per frontier row the `fanout` (<= 32) hash-smallest in-neighbours ->
+    (neighbour ids, frontier row) of the kept samples, row-major (data/graph.py rule)."""
+    assert 0 < fanout <= 32
+    n = nodes.numel()
+    nodes = nodes.long().contiguous()
+    clients = clients.long().contiguous()
+    assert rowptr32.dtype == col32.dtype == owner32.dtype == torch.int32 and is_val_u8.dtype == torch.uint8
+    assert nodes.device == rowptr32.device and clients.shape == nodes.shape
+    out = torch.empty((n, fanout), dtype=torch.int32, device=nodes.device)
+    cnt = torch.empty(n, dtype=torch.int32, device=nodes.device)
+    _C.neighbor_sample(_p(rowptr32), _p(col32), _p(owner32), _p(is_val_u8), _p(nodes), _p(clients), n, fanout,
+                       _hmix_int(seed), _p(out), _p(cnt), _s())
+    keep = out >= 0
+    rows = torch.arange(n, device=nodes.device).unsqueeze(1).expand(n, fanout)
+    return out[keep].long(), rows[keep]
+
+
 # ----------------------------------------------------------------------------- SpMM
 def spmm(rowptr, col, val, x):
     """CSR (shared graph, fp32 values) times per-client dense x [K,Nx,F] → [K,N,F] (x's dtype)."""

@@ -266,6 +266,7 @@ class Session:
         failed = self._failed_clients(r, selected)
         active = [c for c in selected if c not in set(failed)]
         local = self.local_clients(active)
+        self.round_active = active  # (client -> rank map of the round: fed_gnn halo exchange)
         if server.algorithm is not None:
             server.algorithm.expected_kind = (worker.upload_kind() if hasattr(worker, "upload_kind") else
                                               "delta" if getattr(worker, "_send_parameter_diff", True) else "parameter")

@@ -1,0 +1,225 @@
+"""Federated-GNN machinery (data/graph.py): the client-graph edge rules, device neighbour
+sampling, subgraph relabelling, the halo (boundary-embedding) exchange, fed_aas skipping, and
+multi-rank runs (gloo) with sampling against the single-rank run."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from distributed_learning_simulator_amd.data import graph as G
+
+
+class _Spec:
+    def __init__(self, n=400, c=4, f=16, deg=6):
+        self.num_nodes, self.num_classes, self.num_features, self.avg_degree = n, c, f, deg
+
+
+def _toy(share=True, drop=None, W=3, seed=0):
+    ds = G.GraphDataset(_Spec(), seed, "cpu")
+    owner = torch.full((ds.num_nodes,), -1, dtype=torch.int64)
+    owner[ds.train_nodes] = torch.arange(ds.train_nodes.numel()) % W
+    return ds, owner, G.ClientGraph(ds, owner, share, drop, seed, W)
+
+
+def _allowed_neighbours(ds, owner, v, c, share, is_val):
+    """Reference edge rules for aggregation into v as seen by client c (module doc)."""
+    out = set()
+    for u, d in zip(ds.src.tolist(), ds.dst.tolist()):
+        if d != v:
+            continue
+        ov, ou = int(owner[v]), int(owner[u])
+        if ov == c and ou == c:
+            out.add(u)
+        elif share and ov == c and ou >= 0 and ou != c:
+            out.add(u)
+        elif is_val[u] and is_val[v]:
+            out.add(u)
+    return out
+
+
+@pytest.mark.parametrize("share", [True, False])
+def test_client_graph_rules(share):
+    ds, owner, cg = _toy(share)
+    is_val = cg.is_val
+    for v in ds.train_nodes[:15].tolist() + ds.val_nodes[:10].tolist():
+        c = int(owner[v]) if owner[v] >= 0 else 0
+        row = set(cg.col[cg.rowptr[v] : cg.rowptr[v + 1]].tolist())
+        if owner[v] >= 0 or is_val[v]:
+            assert row == _allowed_neighbours(ds, owner, v, c, share, is_val), v
+
+
+def test_edge_drop_rate_counts():
+    ds, owner, cg = _toy(True, drop=0.5)
+    for st in cg.stats:
+        assert 0 < st["in_client_training_edge_cnt"] < st["original_in_client_training_edge_cnt"]
+    _, _, cg2 = _toy(True, drop=0.5)
+    assert torch.equal(cg.col, cg2.col)  # hash-based: deterministic
+
+
+@pytest.mark.parametrize("fanout", [2, 5, -1])
+def test_sampler_without_replacement(fanout):
+    ds, owner, cg = _toy()
+    nodes = torch.cat([ds.train_nodes[:40], ds.val_nodes[:10], ds.test_nodes[:5]])
+    clients = torch.cat([owner[ds.train_nodes[:40]], torch.zeros(15, dtype=torch.int64)])
+    nb, row = G.sample_neighbors_torch(cg, nodes, clients, fanout, seed=11)
+    for i in range(nodes.numel()):
+        v, c = int(nodes[i]), int(clients[i])
+        got = nb[row == i].tolist()
+        allowed = (int(owner[v]) == c) or bool(cg.is_val[v])
+        full = set(cg.col[cg.rowptr[v] : cg.rowptr[v + 1]].tolist()) if allowed else set()
+        assert len(got) == len(set(got))  # without replacement
+        assert set(got) <= full
+        assert len(got) == (len(full) if fanout < 0 else min(fanout, len(full)))
+    nb2, row2 = G.sample_neighbors_torch(cg, nodes, clients, fanout, seed=11)
+    assert torch.equal(nb, nb2) and torch.equal(row, row2)
+    if fanout == 2:
+        nb3, _ = G.sample_neighbors_torch(cg, nodes, clients, fanout, seed=12)
+        assert not torch.equal(nb, nb3)
+
+
+def test_subgraph_relabel_and_edges():
+    ds, owner, cg = _toy()
+    W = 3
+    B = 6
+    seeds = torch.stack([ds.train_nodes[owner[ds.train_nodes] == c][:B] for c in range(W)])
+    seeds[2, 4:] = -1  # empty slots
+    clients = torch.arange(W)
+    sub = G.build_subgraph(cg, seeds, clients, [3, 3], seed=5)
+    assert torch.equal(sub.nid[:2, :B], seeds[:2]) and torch.equal(sub.nid[2, :4], seeds[2, :4])
+    for k in range(W):
+        n = int(sub.count[k])
+        real = sub.nid[k, :n]
+        real = real[real >= 0]
+        assert real.numel() == real.unique().numel()  # deduplicated per client
+    # every sampled edge of client k is an edge of k's view, in local ids
+    es = sub.l1
+    nid = sub.nid.reshape(-1)
+    self_loop = es.src == es.dst
+    s, d = nid[es.src[~self_loop]], nid[es.dst[~self_loop]]
+    k = es.dst[~self_loop] // sub.nmax
+    for a, b, kk in list(zip(s.tolist(), d.tolist(), k.tolist()))[:200]:
+        assert a in set(cg.col[cg.rowptr[b] : cg.rowptr[b + 1]].tolist())
+        assert int(owner[b]) == kk or bool(cg.is_val[b])
+    # layer 0: only local-node edges
+    e0 = sub.l0
+    l0 = e0.src != e0.dst
+    for a, b, kk in zip(nid[e0.src[l0]].tolist(), nid[e0.dst[l0]].tolist(), (e0.dst[l0] // sub.nmax).tolist()):
+        for g in (a, b):
+            assert int(owner[g]) == kk or bool(cg.is_val[g])
+
+
+def test_halo_substitution_semantics():
+    ds, owner, cg = _toy()
+    W = 3
+    seeds = torch.stack([ds.train_nodes[owner[ds.train_nodes] == c][:20] for c in range(W)])
+    sub = G.build_subgraph(cg, seeds, torch.arange(W), [-1, -1], seed=1)
+    K, nmax = sub.nid.shape
+    h = torch.randn(K, nmax, 4)
+    halo = G.HaloExchange(cg, None, None)
+    halo.begin_batch()
+    out = halo(h, sub)
+    for k in range(K):
+        for i in range(nmax):
+            g = int(sub.nid[k, i])
+            if g < 0:
+                continue
+            if sub.own[k, i]:
+                assert torch.equal(out[k, i], h[k, i])
+            elif sub.remote[k, i]:
+                o = int(owner[g])
+                rows = (sub.nid[o] == g) & sub.publish[o]
+                exp = h[o][rows][0] if rows.any() else torch.zeros(4)
+                assert torch.equal(out[k, i], exp)
+            else:  # validation / unowned: zero (reference _get_cross_deivce_embedding)
+                assert torch.equal(out[k, i], torch.zeros(4))
+    assert float(halo.sent_rows) == float(sub.publish.sum()) * 4
+    # gradients reach own rows only
+    h.requires_grad_(True)
+    halo(h, sub).sum().backward()
+    assert torch.equal(h.grad, sub.own.float().unsqueeze(-1).expand_as(h))
+
+
+def test_aas_policy_period_adapts():
+    p = G.AdaptiveSkipPolicy(threshold=0.5, max_period=4)
+    decisions = []
+    for _ in range(12):
+        skip = p.skip()
+        decisions.append(skip)
+        if not skip:
+            p.observe(torch.ones(3, 2), None)  # unchanged embeddings: the period grows
+    assert decisions[:2] == [False, False] and any(decisions) and p.period == 4
+
+
+# ------------------------------------------------------------------ multi-rank runs
+BASE = {"dataset_name": "Coauthor_CS", "model_name": "TwoGCN", "worker_number": 4, "round": 2, "epoch": 1,
+        "dataset_kwargs": {"scale": 0.05}, "optimizer_name": "Adam", "learning_rate": 0.01, "save_models": False,
+        "log_level": "WARNING", "seed": 3}
+
+
+def _cfg(algo, tmp, ak):
+    from distributed_learning_simulator_amd.config import config_from_dict
+
+    return config_from_dict(dict(BASE, distributed_algorithm=algo, save_dir=tmp, algorithm_kwargs=ak))
+
+
+def _worker(rank, world, port, algo, tmp, ak, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DLS_FORCE_CPU="1")
+    torch.set_num_threads(1)
+    from distributed_learning_simulator_amd.parallel import comm as commmod
+    from distributed_learning_simulator_amd.session import Session
+
+    commmod._COMM = None
+    c = commmod.init_distributed(prefer_gpu=False)
+    sess = Session(_cfg(algo, tmp, ak), comm=c)
+    sess.run()
+    w = sess.worker
+    q.put((rank, sess.server.global_parameter.clone(), w._communicated_embedding_bytes, w._skipped_embedding_bytes))
+    commmod.shutdown()
+
+
+def _single(algo, tmp, ak):
+    from distributed_learning_simulator_amd.parallel.comm import Comm
+    from distributed_learning_simulator_amd.session import Session
+
+    n = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        s = Session(_cfg(algo, tmp, ak), comm=Comm())
+        s.run()
+    finally:
+        torch.set_num_threads(n)
+    return s.server.global_parameter, s.worker._communicated_embedding_bytes, s.worker._skipped_embedding_bytes
+
+
+@pytest.mark.parametrize("algo,ak,world", [
+    ("fed_gnn", {"share_feature": True, "batch_number": 3, "num_neighbor": 4}, 2),
+    ("fed_aas", {"share_feature": True, "batch_number": 4, "num_neighbor": 5, "aas_threshold": 10.0}, 2),
+    ("fed_gnn", {"share_feature": False, "batch_number": 2, "num_neighbor": 3, "edge_drop_rate": 0.3}, 4),
+])
+def test_sampled_gnn_ranks_match_single_rank(tmp_path, algo, ak, world):
+    th1, sent1, skip1 = _single(algo, str(tmp_path / "s"), ak)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, algo, str(tmp_path / "d"), ak, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=600) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for o in outs[1:]:
+        torch.testing.assert_close(o[1], outs[0][1], rtol=0, atol=0)
+    torch.testing.assert_close(outs[0][1], th1, rtol=1e-4, atol=1e-5)
+    assert outs[0][2] == sent1 and outs[0][3] == skip1  # same traffic however clients are placed
+    if ak.get("share_feature"):
+        assert sent1 > 0
+    if algo == "fed_aas":
+        assert skip1 > 0  # a large threshold keeps doubling the period: batches are skipped
