@@ -209,6 +209,26 @@ PYBIND11_MODULE(_dls_hip, m) {
                     P<const float>(lse), P<const int>(kv), P<void>(dq), P<void>(dk), P<void>(dv), P<float>(delta), KBH,
                     H, L, DH, f32, S(s), ldqkv, ldo);
   });
+  m.def("quant_pack", [](ptr x, long ld, ptr seg, ptr seg_off, ptr seg_numel, ptr bits, ptr lo, ptr scale,
+                         ptr seg_byte_off, ptr row_off, int K, int nseg, long Pn, int stochastic, ptr seeds, ptr out,
+                         ptr s) {
+    quant_pack(P<const float>(x), ld, P<const int>(seg), P<const int64_t>(seg_off), P<const int64_t>(seg_numel),
+               P<const uint8_t>(bits), P<const float>(lo), P<const float>(scale), P<const int64_t>(seg_byte_off),
+               P<const int64_t>(row_off), K, nseg, Pn, stochastic, P<const uint32_t>(seeds), P<uint8_t>(out), S(s));
+  });
+  m.def("quant_unpack", [](ptr codes, ptr seg, ptr seg_off, ptr seg_numel, ptr bits, ptr lo, ptr scale,
+                           ptr seg_byte_off, ptr row_off, int K, int nseg, long Pn, ptr out, long ld, ptr s) {
+    quant_unpack(P<const uint8_t>(codes), P<const int>(seg), P<const int64_t>(seg_off), P<const int64_t>(seg_numel),
+                 P<const uint8_t>(bits), P<const float>(lo), P<const float>(scale), P<const int64_t>(seg_byte_off),
+                 P<const int64_t>(row_off), K, nseg, Pn, P<float>(out), ld, S(s));
+  });
+  m.def("quant_unpack_acc", [](ptr codes, ptr seg, ptr seg_off, ptr seg_numel, ptr bits, ptr lo, ptr scale,
+                               ptr seg_byte_off, ptr row_off, int K, int nseg, long Pn, ptr w, ptr acc, ptr s) {
+    quant_unpack_acc(P<const uint8_t>(codes), P<const int>(seg), P<const int64_t>(seg_off),
+                     P<const int64_t>(seg_numel), P<const uint8_t>(bits), P<const float>(lo), P<const float>(scale),
+                     P<const int64_t>(seg_byte_off), P<const int64_t>(row_off), K, nseg, Pn, P<const double>(w),
+                     P<double>(acc), S(s));
+  });
   m.def("neighbor_sample", [](ptr rowptr, ptr col, ptr owner, ptr is_val, ptr nodes, ptr clients, int n, int fanout,
                               unsigned long long seed_h, ptr out_nbr, ptr out_cnt, ptr s) {
     neighbor_sample(P<const int>(rowptr), P<const int>(col), P<const int>(owner), P<const uint8_t>(is_val),

@@ -154,6 +154,18 @@ __device__ __forceinline__ void split_vec(const float* f, bf16_t* hi, bf16_t* lo
   for (int i = 0; i < V; ++i) split2(f[i], hi[i], lo[i]);
 }
 
+// 32-bit hash of (index, seed): the per-element uniforms of masks and stochastic rounding
+// (identical to ops/fl.py `_mix`, so CPU and GPU draw the same numbers)
+__device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t seed) {
+  x ^= seed * 0x9E3779B9u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -163,6 +163,22 @@ void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* 
 void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStream_t s);
 
 // ------------------------------------------------------------- FL / optimiser
+// ---------------------------------------------------------------- compressed payloads (compress.hip)
+// Pack per-(client, tensor) b-bit codes (bits[k][s] ∈ [0, 8], 0 = tensor not sent) of rows x
+// [K][ld] into the ragged wire buffer out (client k at row_off[k], tensor s at seg_byte_off[k][s]);
+// stochastic rounding (seeds[k]) or round-to-nearest. Unpack to dense rows, or fused into the
+// fp64 server accumulator acc[i] += Σ_k w[k]·x̂_k[i]. P = padded flat size (multiple of 8).
+void quant_pack(const float* x, long ld, const int* seg, const int64_t* seg_off, const int64_t* seg_numel,
+                const uint8_t* bits, const float* lo, const float* scale, const int64_t* seg_byte_off,
+                const int64_t* row_off, int K, int nseg, long P, int stochastic, const uint32_t* seeds, uint8_t* out,
+                hipStream_t s);
+void quant_unpack(const uint8_t* codes, const int* seg, const int64_t* seg_off, const int64_t* seg_numel,
+                  const uint8_t* bits, const float* lo, const float* scale, const int64_t* seg_byte_off,
+                  const int64_t* row_off, int K, int nseg, long P, float* out, long ld, hipStream_t s);
+void quant_unpack_acc(const uint8_t* codes, const int* seg, const int64_t* seg_off, const int64_t* seg_numel,
+                      const uint8_t* bits, const float* lo, const float* scale, const int64_t* seg_byte_off,
+                      const int64_t* row_off, int K, int nseg, long P, const double* w, double* acc, hipStream_t s);
+
 // ---------------------------------------------------------------- graph (graph.hip)
 // Federated-GNN neighbour sampling: per frontier row (nodes[t] expanded for client clients[t])
 // the `fanout` (<= 32) in-neighbours with the smallest hash keys; out_nbr [n][fanout] (-1 pad).

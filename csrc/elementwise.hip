@@ -7,16 +7,6 @@
 
 namespace {
 
-__device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t seed) {
-  x ^= seed * 0x9E3779B9u;
-  x ^= x >> 16;
-  x *= 0x7FEB352Du;
-  x ^= x >> 15;
-  x *= 0x846CA68Bu;
-  x ^= x >> 16;
-  return x;
-}
-
 // ------------------------------------------------------------------ pooling (NHWC)
 // mode 0 = max (records argmax as flat input spatial index), 1 = average
 template <typename T>

@@ -54,15 +54,24 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         if msg.mask is not None:
             if self._w_elem is None:
                 self._w_elem = torch.zeros_like(self._acc)
-            fl.masked_weighted_sum(msg.data, msg.mask, w, self._acc, self._w_elem)
+            fl.masked_weighted_sum(msg.dense(), msg.mask, w, self._acc, self._w_elem)
         else:
-            fl.weighted_sum(msg.data, w, self._acc)
+            if msg.payload is not None:  # packed upload: dequantised inside the fp64 accumulation
+                msg.payload.accumulate(self._acc, w)
+            else:
+                fl.weighted_sum(msg.dense(), w, self._acc)
             if msg.block_mask is not None:
                 bw = (msg.block_mask.double() * w[:, None]).sum(0)
                 self._w_block = bw if self._w_block is None else self._w_block + bw
                 self._block_ids = msg.extra["block_ids"]
         self._w_total += w.sum()
         self._dataset_size += float(msg.dataset_sizes.sum().item()) if not msg.dataset_sizes.is_cuda else 0.0
+
+    @property
+    def fuses_payload(self) -> bool:
+        """Packed uploads are dequantised inside `_process` (not decoded by the endpoint) unless
+        a subclass replaces `_process`."""
+        return type(self)._process is FedAVGAlgorithm._process
 
     # set by the method/session so that a rank hosting no client this round still joins the
     # collectives with correctly shaped (zero) contributions

@@ -118,10 +118,21 @@ class CohortMessage(Message):
     wire_bytes: list[int] = field(default_factory=list)
     layout: Any = None  # engine.params.ParamLayout
     extra: dict = field(default_factory=dict)
+    # quantised uploads travel as a packed wire buffer (ops/compress.QuantPayload): `data` is
+    # None until the receiver decodes it (`dense()`), or never when the server's accumulation
+    # dequantises the payload directly
+    payload: Any = None
 
     @property
     def size(self) -> int:
         return len(self.client_ids)
+
+    def dense(self) -> torch.Tensor:
+        """Decoded [K, P] rows (decodes a pending payload in place, once)."""
+        if self.data is None and self.payload is not None:
+            self.data = self.payload.decode(out=self.extra.pop("decode_into", None))
+            self.payload = None
+        return self.data
 
     def client_message(self, i: int) -> ParameterMessageBase:
         """Materialise client i as a reference-style single-client message (API parity,

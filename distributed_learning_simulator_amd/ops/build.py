@@ -29,6 +29,10 @@ TARGET = os.path.join(PKG, "_dls_hip" + EXT_SUFFIX)
 
 COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-mcode-object-version=5",
                 "-ffp-contract=fast", "-Wno-unused-result"]
+# per-file overrides. compress.hip: the payload decoders must round lo + q·scale twice, like
+# the CPU oracle. Under -ffp-contract=fast the backend fuses every fmul+fadd into an FMA,
+# whatever the source pragmas say; "on" fuses only within one expression.
+FILE_FLAGS = {"compress.hip": ["-ffp-contract=on"]}
 
 
 def _headers() -> list[str]:
@@ -63,7 +67,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
         if f.endswith(".hip") or f.endswith(".cpp"):
             src = os.path.join(CSRC, f)
             obj = os.path.join(BUILD, f + ".o")
-            extra = [f"-I{CSRC}"]
+            extra = [f"-I{CSRC}", *FILE_FLAGS.get(f, [])]
             if f.endswith(".cpp"):
                 extra += [f"-I{pybind11.get_include()}", f"-I{py_inc}", "-x", "hip"]
             units.append((src, obj, extra))

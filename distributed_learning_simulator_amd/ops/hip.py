@@ -586,6 +586,33 @@ def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None):
     return dqkv
 
 
+# ------------------------------------------------------------- compressed payloads
+def _payload_args(p):
+    m = p.meta
+    return (_p(m.seg_ids), _p(m.seg_off), _p(m.seg_numel), _p(p.bits), _p(p.lo), _p(p.scale), _p(p.seg_byte_off),
+            _p(p.row_off))
+
+
+def quant_pack(p, x, seeds):
+    """csrc/compress.hip: codes of rows x [K, P] fp32 into p.codes (see ops/compress.py)."""
+    K, P = x.shape
+    assert x.dtype == torch.float32 and x.stride(1) == 1 and P == p.meta.P and K == p.K
+    sd = _seeds_dev(seeds) if seeds is not None else None
+    m = p.meta
+    _C.quant_pack(_p(x), x.stride(0), _p(m.seg_ids), _p(m.seg_off), _p(m.seg_numel), _p(p.bits), _p(p.lo),
+                  _p(p.scale), _p(p.seg_byte_off), _p(p.row_off), K, m.nseg, P, int(seeds is not None), _p(sd),
+                  _p(p.codes), _s())
+
+
+def quant_unpack(p, out):
+    _C.quant_unpack(_p(p.codes), *_payload_args(p), p.K, p.meta.nseg, p.meta.P, _p(out), out.stride(0), _s())
+
+
+def quant_unpack_acc(p, w, acc):
+    assert w.dtype == torch.float64 and w.numel() == p.K and acc.is_contiguous()
+    _C.quant_unpack_acc(_p(p.codes), *_payload_args(p), p.K, p.meta.nseg, p.meta.P, _p(w), _p(acc), _s())
+
+
 # ---------------------------------------------------------------------- GNN sampling
 def _hmix_int(h: int) -> int:
     h &= 0x7FFFFFFF

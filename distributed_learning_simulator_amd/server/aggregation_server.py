@@ -83,7 +83,7 @@ class AggregationServer(Server):
 
     # --------------------------------------------------------------- process
     def _process_worker_data(self, msg, worker_ids=None) -> None:
-        msg = self.endpoint.get(msg)
+        msg = self.endpoint.get(msg, defer_payload=bool(getattr(self._algorithm, "fuses_payload", False)))
         self._algorithm.process_worker_data(msg, self.global_parameter, worker_ids=worker_ids,
                                             save_dir=self.save_dir)
 

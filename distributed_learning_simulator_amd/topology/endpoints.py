@@ -20,7 +20,7 @@ from __future__ import annotations
 import torch
 
 from ..message import CohortMessage
-from ..ops import fl, quant
+from ..ops import compress, fl
 from ..utils.logging import get_logger
 
 
@@ -31,6 +31,7 @@ class _Ctx:
         self.seed = seed
         self.seg_ids = layout.segment_ids(device)
         self.seg_sizes = layout.segment_sizes(device)
+        self.meta = compress.LayoutMeta.of(layout, device)
         self.dense_bytes = layout.num_params * 4
 
 
@@ -81,7 +82,11 @@ class ServerEndpoint:
     def bind(self, layout, device, seed: int) -> None:
         self.ctx = _Ctx(layout, device, seed)
 
-    def get(self, msg: CohortMessage | None) -> CohortMessage | None:
+    def get(self, msg: CohortMessage | None, defer_payload: bool = False) -> CohortMessage | None:
+        """Receive: a packed payload is decoded here, unless the consumer dequantises it
+        itself (`defer_payload`: FedAvg's fused accumulation)."""
+        if msg is not None and msg.payload is not None and not defer_payload:
+            msg.dense()
         return msg
 
     def encode_broadcast(self, params: torch.Tensor, seed: int) -> tuple[torch.Tensor, int]:
@@ -99,8 +104,18 @@ class ServerEndpoint:
 
 
 # ------------------------------------------------------------------ quantised
+def _attach(msg: CohortMessage, payload) -> CohortMessage:
+    """The upload becomes the packed payload: the dense rows are no longer part of the message
+    (kept only as the receiver's decode target)."""
+    msg.payload = payload
+    msg.extra["decode_into"] = msg.data
+    msg.data = None
+    msg.wire_bytes = payload.row_bytes()
+    return msg
+
+
 class QuantClientEndpoint(ClientEndpoint):
-    """Quantise uploads; optionally dequantise server data (`dequant_server_data`)."""
+    """Quantise uploads into a wire payload; optionally dequantise server data."""
 
     def quantize(self, msg: CohortMessage, seed: int) -> CohortMessage:
         raise NotImplementedError
@@ -116,20 +131,15 @@ class QuantServerEndpoint(ServerEndpoint):
 
 
 class StochasticQuantClientEndpoint(QuantClientEndpoint):
-    """FedPAQ / fed_obd_sq upload: 255-level stochastic quantisation
+    """FedPAQ / fed_obd_sq upload: 255-level stochastic quantisation into an 8-bit payload
     (reference `quantized_endpoint.py:74-77`)."""
 
     levels = 255
 
     def quantize(self, msg, seed):
         seeds = fl.row_seeds(seed, msg.client_ids)
-        dq, wire = quant.stochastic_quantize(msg.data, self.ctx.seg_ids, self.ctx.seg_sizes, seeds, self.levels)
-        msg.data.copy_(dq)
-        if msg.block_mask is not None:
-            frac = self._dense_wire(msg)
-            wire = [int(round(w * f / self.ctx.dense_bytes)) for w, f in zip(wire, frac)]
-        msg.wire_bytes = wire
-        return msg
+        p = compress.pack_stochastic(msg.data, self.ctx.meta, seeds, msg.extra.get("segment_mask"), self.levels)
+        return _attach(msg, p)
 
 
 class StochasticQuantServerEndpoint(QuantServerEndpoint):
@@ -138,9 +148,8 @@ class StochasticQuantServerEndpoint(QuantServerEndpoint):
     def encode_broadcast(self, params, seed):
         if not self.quant_broadcast:
             return params, self.ctx.dense_bytes
-        dq, wire = quant.stochastic_quantize(params.unsqueeze(0), self.ctx.seg_ids, self.ctx.seg_sizes,
-                                             fl.row_seeds(seed, [-1]), self.levels)
-        return dq[0], wire[0]
+        p = compress.pack_stochastic(params.unsqueeze(0), self.ctx.meta, fl.row_seeds(seed, [-1]), None, self.levels)
+        return p.decode()[0], p.row_bytes()[0]
 
 
 class NNADQClientEndpoint(QuantClientEndpoint):
@@ -155,14 +164,12 @@ class NNADQClientEndpoint(QuantClientEndpoint):
     def quantize(self, msg, seed):
         if self.weight is None:
             return super().quantize(msg, seed)
-        seg_mask = msg.extra.get("segment_mask")
-        dq, wire, _ = quant.nnadq_quantize(msg.data, self.ctx.seg_ids, self.ctx.seg_sizes, self.weight, seg_mask)
-        msg.data.copy_(dq)
         dense = self._dense_wire(msg)
-        msg.wire_bytes = wire
-        for cid, w, d in zip(msg.client_ids, wire, dense):
+        p = compress.pack_nnadq(msg.data, self.ctx.meta, self.weight, msg.extra.get("segment_mask"))
+        msg = _attach(msg, p)
+        for cid, w, d in zip(msg.client_ids, msg.wire_bytes, dense):
             get_logger().debug("worker %d NNABQ compression ratio is %s", cid, w / max(d, 1))
-        msg.extra["compression_ratio"] = [w / max(d, 1) for w, d in zip(wire, dense)]
+        msg.extra["compression_ratio"] = [w / max(d, 1) for w, d in zip(msg.wire_bytes, dense)]
         return msg
 
 
@@ -174,7 +181,7 @@ class NNADQServerEndpoint(QuantServerEndpoint):
     def encode_broadcast(self, params, seed):
         if not self.quant_broadcast or self.weight is None:
             return params, self.ctx.dense_bytes
-        dq, wire, _ = quant.nnadq_quantize(params.unsqueeze(0), self.ctx.seg_ids, self.ctx.seg_sizes, self.weight)
-        ratio = wire[0] / self.ctx.dense_bytes
-        get_logger().info("broadcast NNABQ compression ratio is %s", ratio)
-        return dq[0], wire[0]
+        p = compress.pack_nnadq(params.unsqueeze(0), self.ctx.meta, self.weight)
+        wire = p.row_bytes()[0]
+        get_logger().info("broadcast NNABQ compression ratio is %s", wire / self.ctx.dense_bytes)
+        return p.decode()[0], wire
