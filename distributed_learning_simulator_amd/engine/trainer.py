@@ -31,6 +31,7 @@ import torch
 from ..models.layers import RunCtx
 from ..ops import fl
 from ..ops import functional as Fn
+from ..utils.tracing import trace
 from .hooks import ExecutorHookPoint, HookRegistry, StopExecutingException
 from .params import BoundParams, CohortBuffers
 
@@ -333,7 +334,7 @@ class CohortTrainer:
             for s in range(schedule.steps):
                 for (a, b), st in zip(parts, streams):
                     ctx = torch.cuda.stream(st) if multi else _nullctx()
-                    with ctx:
+                    with ctx, trace(f"step {s} rows {a}:{b}"):
                         self._train_step(schedule, ds, s, e, a, b, stats, executor)
                 if self.hooks.has_hook(ExecutorHookPoint.AFTER_BATCH):
                     if multi:

@@ -91,6 +91,38 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     return TARGET
 
 
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-Xarch_host",
+             "-fno-omit-frame-pointer", "-g"]
+HOST_CHECK = os.path.join(ROOT, "build", "host_asan", "host_check")
+
+
+def build_host_check(jobs: int = 0) -> str:
+    """tests/native/host_check.cpp + every csrc/*.hip with host-side ASan/UBSan:
+    the host launch-planning code under sanitizers. Device code is compiled as usual (GPU
+    sanitizers are not used). Incremental like `build`."""
+    out_dir = os.path.dirname(HOST_CHECK)
+    os.makedirs(out_dir, exist_ok=True)
+    units = []
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith(".hip"):
+            units.append((os.path.join(CSRC, f), os.path.join(out_dir, f + ".o"),
+                          [f"-I{CSRC}", *FILE_FLAGS.get(f, []), *SAN_FLAGS]))
+    main_src = os.path.join(ROOT, "tests", "native", "host_check.cpp")
+    units.append((main_src, os.path.join(out_dir, "host_check.o"), [f"-I{CSRC}", "-x", "hip", *SAN_FLAGS]))
+    todo = [u for u in units if _needs(u[1], u[0])]
+    jobs = jobs or min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8) or 1
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            list(ex.map(lambda u: _compile(*u), todo))
+    objs = [u[1] for u in units]
+    if todo or not os.path.exists(HOST_CHECK) or any(os.path.getmtime(o) > os.path.getmtime(HOST_CHECK) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-fsanitize=address,undefined", "-o", HOST_CHECK, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return HOST_CHECK
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")

@@ -135,7 +135,12 @@ class EmulatedRankComm(Comm):
 _COMM: Comm | None = None
 
 
-def init_distributed(prefer_gpu: bool = True, timeout_s: int = 1800) -> Comm:
+def init_distributed(prefer_gpu: bool = True, timeout_s: int | None = None) -> Comm:
+    """One rank of the job (torchrun / parallel.launch environment). Collectives time out after
+    `timeout_s` (default `DLS_COLLECTIVE_TIMEOUT` or 1800 s): a dead peer ends the job with an
+    error instead of a silent hang."""
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("DLS_COLLECTIVE_TIMEOUT", "1800"))
     """Initialise from torchrun-style env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
     global _COMM
     if _COMM is not None:

@@ -35,6 +35,7 @@ from .parallel.comm import Comm, get_comm, init_distributed
 from .practitioner import create_practitioners
 from .sampler import get_partition
 from .utils.logging import get_logger
+from .utils.tracing import Watchdog, round_timeout, trace
 
 
 def resolve_dtype(config, device) -> torch.dtype:
@@ -255,6 +256,12 @@ class Session:
         return out
 
     def run_one_round(self, theta_recv: torch.Tensor) -> torch.Tensor:
+        """One FL round under the round watchdog (utils/tracing.py), inside a roctx range."""
+        with Watchdog(round_timeout(self.config), f"round {self.server.round_number}"), \
+                trace(f"round {self.server.round_number}"):
+            return self._run_one_round(theta_recv)
+
+    def _run_one_round(self, theta_recv: torch.Tensor) -> torch.Tensor:
         server, worker = self.server, self.worker
         if hasattr(server, "run_round"):  # methods with their own round structure (sign-SGD)
             return server.run_round(self, theta_recv)
@@ -271,16 +278,19 @@ class Session:
             server.algorithm.expected_kind = (worker.upload_kind() if hasattr(worker, "upload_kind") else
                                               "delta" if getattr(worker, "_send_parameter_diff", True) else "parameter")
         up0 = worker.endpoint.bytes_sent
-        for msg in worker.run_round(r, theta_recv, local):
-            server._process_worker_data(msg)
-        skipped = sorted(set(range(self.config.worker_number)) - set(active))
-        if skipped:
-            server._process_worker_data(None, worker_ids=skipped)
+        with trace("train"):
+            for msg in worker.run_round(r, theta_recv, local):
+                server._process_worker_data(msg)
+            skipped = sorted(set(range(self.config.worker_number)) - set(active))
+            if skipped:
+                server._process_worker_data(None, worker_ids=skipped)
         up_local = worker.endpoint.bytes_sent - up0
         self._mark(marks, "train_s")
-        result = server._aggregate_worker_data()
+        with trace("aggregate"):
+            result = server._aggregate_worker_data()
         self._mark(marks, "aggregate_s")
-        theta_recv, down = server.send_result(result)
+        with trace("eval_broadcast"):
+            theta_recv, down = server.send_result(result)
         self._mark(marks, "eval_broadcast_s")
         up = self._sum_scalar(up_local)
         if self.config.debug:

@@ -5,6 +5,7 @@
 #   scripts/gpu.sh tests              pytest -m gpu (every kernel vs its oracle, GPU sessions)
 #   scripts/gpu.sh bench [ARGS...]    bench.py ARGS  -> gpurun_out/bench.json
 #   scripts/gpu.sh prof  [ARGS...]    rocprofv3 --kernel-trace --stats of bench.py ARGS
+#   scripts/gpu.sh marker [ARGS...]  roctx phase ranges + kernel stats (DLS_ROCTX=1)
 #   scripts/gpu.sh pmc   COUNTERS [ARGS...]   one rocprofv3 --pmc pass (counter limits: see guide)
 #   scripts/gpu.sh pmcset [ARGS...]  MFMA/LDS/HBM counter passes -> gpurun_out/pmc_summary.csv
 #   scripts/gpu.sh kbench [ARGS...]   bench/kernel_bench.py ARGS
@@ -39,6 +40,19 @@ case "$mode" in
     [ -n "$stats" ] && cp "$stats" gpurun_out/prof_kernel_stats.csv
     rm -rf gpurun_out/prof
     [ -f gpurun_out/prof_kernel_stats.csv ] && cut -c1-200 gpurun_out/prof_kernel_stats.csv | head -25
+    exit $rc
+    ;;
+  marker)
+    # roctx phase ranges (DLS_ROCTX=1: round / train / aggregate / eval_broadcast / step) next to
+    # the kernel trace; keeps the range summary and the kernel stats only
+    DLS_ROCTX=1 timeout -k 10 1000 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
+      -d gpurun_out/marker -o run -- python -u bench.py "$@" > gpurun_out/marker_bench.log 2>&1
+    rc=$?
+    python scripts/marker_summary.py gpurun_out/marker gpurun_out/marker_ranges.csv
+    stats=$(find gpurun_out/marker -name '*kernel_stats.csv' | head -1)
+    [ -n "$stats" ] && cp "$stats" gpurun_out/marker_kernel_stats.csv
+    rm -rf gpurun_out/marker
+    head -20 gpurun_out/marker_ranges.csv
     exit $rc
     ;;
   pmc)
