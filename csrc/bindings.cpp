@@ -20,8 +20,11 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
                       int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s, int ldx, int ldy,
-                      ptr stats, ptr stats_valid) {
+                      ptr stats, ptr stats_valid, ptr drop_seeds, float drop_p, float out_scale) {
     ConvNTParams p{};
+    p.drop_seeds = P<const uint32_t>(drop_seeds);
+    p.drop_p = drop_p;
+    p.out_scale = out_scale;
     p.stats = P<float>(stats);
     p.stats_valid = P<const int>(stats_valid);
     p.f32 = f32;
@@ -208,6 +211,10 @@ PYBIND11_MODULE(_dls_hip, m) {
     return attn_bwd(P<const void>(dout), P<const void>(q), P<const void>(k), P<const void>(v), P<const void>(o),
                     P<const float>(lse), P<const int>(kv), P<void>(dq), P<void>(dk), P<void>(dv), P<float>(delta), KBH,
                     H, L, DH, f32, S(s), ldqkv, ldo);
+  });
+  m.def("dropout_apply", [](ptr x, ptr out, int K, long rows, int N, long ld, ptr seeds, float p, float scale,
+                            int f32, ptr s) {
+    dropout_apply(P<const void>(x), P<void>(out), K, rows, N, ld, P<const uint32_t>(seeds), p, scale, f32, S(s));
   });
   m.def("quant_pack", [](ptr x, long ld, ptr seg, ptr seg_off, ptr seg_numel, ptr bits, ptr lo, ptr scale,
                          ptr seg_byte_off, ptr row_off, int K, int nseg, long Pn, int stochastic, ptr seeds, ptr out,

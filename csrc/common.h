@@ -166,6 +166,13 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t seed) {
   return x;
 }
 
+// dropout keep-decision of element (m, n) of an [M][N] output of client row k (GEMM epilogues,
+// dropout_apply): mix32(m·N + n, seed_k) >= p·2^32
+__device__ __forceinline__ bool drop_keep(uint32_t seed, long m, int N, int n, float p) {
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.f, 4294967040.f);
+  return mix32((uint32_t)(m * (long)N + n), seed) >= thr;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

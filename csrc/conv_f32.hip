@@ -283,6 +283,10 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
   const float* accp = p.acc ? reinterpret_cast<const float*>(p.acc) + (long)client * p.y_cs : nullptr;
   const float* gatep = p.gate ? reinterpret_cast<const float*>(p.gate) + (long)client * p.y_cs : nullptr;
   const float* bias = p.bias ? reinterpret_cast<const float*>(p.bias) + (long)(client / p.rep) * p.b_cs : nullptr;
+  // epilogue scale (dropout's 1/(1-p), or the dgrad gate's) and dropout mask of this client row
+  const bool drop = p.drop_p > 0.f && p.drop_seeds != nullptr;
+  const uint32_t dseed = drop ? p.drop_seeds[client] : 0u;
+  const float oscale = (p.out_scale != 0.f ? p.out_scale : 1.f) * (drop ? 1.f / (1.f - p.drop_p) : 1.f);
   float bvals[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -329,6 +333,11 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
       for (int e = 0; e < 16; ++e) {
         float v = acc[i][j][e] + bvals[j];
         if (p.relu) v = fmaxf(v, 0.f);
+        v *= oscale;
+        if (drop) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          if (!drop_keep(dseed, m0 + wm0 + i * 32 + rr, p.N, n0 + wn0 + j * 32 + (lane & 31), p.drop_p)) v = 0.f;
+        }
         slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = v;
       }
     }

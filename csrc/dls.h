@@ -58,6 +58,12 @@ struct ConvNTParams {
   // (parts = cdiv(M, 32)), so BN skips its own statistics pass over y
   float* stats;
   const int* stats_valid;  // [K] valid samples per client (nullptr: all rows)
+  // epilogue scale / dropout (Transformer training): v = out_scale·(acc·W + bias) (0 = 1); with
+  // drop_p > 0, v = keep(k, m, n) ? v / (1 − drop_p) : 0 before the residual add, where
+  // keep = mix32(m·N + n, drop_seeds[k]) ≥ drop_p·2³² (same rule as ops: dropout_apply)
+  const uint32_t* drop_seeds;
+  float drop_p;
+  float out_scale;
 };
 
 struct ConvTNParams {
@@ -178,6 +184,11 @@ void quant_unpack(const uint8_t* codes, const int* seg, const int64_t* seg_off, 
 void quant_unpack_acc(const uint8_t* codes, const int* seg, const int64_t* seg_off, const int64_t* seg_numel,
                       const uint8_t* bits, const float* lo, const float* scale, const int64_t* seg_byte_off,
                       const int64_t* row_off, int K, int nseg, long P, const double* w, double* acc, hipStream_t s);
+
+// out[k][r][c] = keep(k, r, c) ? x·scale : 0 over [K][rows][N] (row stride ld), the dropout rule of
+// the GEMM epilogue; seeds [K]. f32: fp32 (else bf16) tensors.
+void dropout_apply(const void* x, void* out, int K, long rows, int N, long ld, const uint32_t* seeds, float p,
+                   float scale, int f32, hipStream_t s);
 
 // ---------------------------------------------------------------- graph (graph.hip)
 // Federated-GNN neighbour sampling: per frontier row (nodes[t] expanded for client clients[t])

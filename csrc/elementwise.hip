@@ -2,6 +2,8 @@
 // the fused optimiser steps over flat [K, P] client buffers, FedAvg weighted row reductions,
 // and the transport-compression kernels (dropout masks, stochastic quantisation, 1-bit sign
 // pack / majority vote). All vectorised to 16-B accesses where the layout allows.
+#include <algorithm>
+
 #include "common.h"
 #include "dls.h"
 
@@ -486,6 +488,22 @@ __global__ void nnadq_qdq_kernel(float* __restrict__ x, const int* __restrict__ 
   }
 }
 
+// dropout on [K][rows][N] (row stride ld): the GEMM epilogue's mask rule (common.h drop_keep)
+template <typename T>
+__global__ void dropout_apply_kernel(const T* __restrict__ x, T* __restrict__ out, long rows, int N, long ld,
+                                     const uint32_t* __restrict__ seeds, float p, float scale) {
+  const int k = blockIdx.y;
+  const uint32_t seed = seeds[k];
+  const long total = rows * (long)N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / N;
+    const int n = (int)(i - m * N);
+    const long o = ((long)k * rows + m) * ld + n;
+    const float v = ldf(x + o);
+    stf(out + o, drop_keep(seed, m, N, n, p) ? v * scale : 0.f);
+  }
+}
+
 __global__ void sign_pack_kernel(const float* __restrict__ g, uint8_t* __restrict__ out, long P, long ld,
                                  long nbytes) {
   const int k = blockIdx.y;
@@ -752,4 +770,17 @@ void gather_rows(const void* src, const int* idx, void* dst, long n, long row_by
   const long v16 = row_bytes / 16;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(cdiv(n * v16, 256)), dim3(256), 0, s, static_cast<const uint4*>(src), idx,
                      static_cast<uint4*>(dst), n, v16);
+}
+
+void dropout_apply(const void* x, void* out, int K, long rows, int N, long ld, const uint32_t* seeds, float p,
+                   float scale, int f32, hipStream_t s) {
+  const long total = rows * (long)N;
+  if (total == 0 || K == 0) return;
+  const dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 4096), K);
+  if (f32)
+    hipLaunchKernelGGL(dropout_apply_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(x),
+                       static_cast<float*>(out), rows, N, ld, seeds, p, scale);
+  else
+    hipLaunchKernelGGL(dropout_apply_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                       static_cast<bf16_t*>(out), rows, N, ld, seeds, p, scale);
 }

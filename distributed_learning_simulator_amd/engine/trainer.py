@@ -80,6 +80,8 @@ class RoundSchedule:
     # [S, K, B + 4] int32: idx | count | active | first | lr (fp32 bits) — one row per step, the
     # single copy a graph-replayed step needs (see CohortTrainer._train_graphed)
     packed: torch.Tensor | None = None
+    client_ids: torch.Tensor | None = None  # [K] int64 (device): dropout masks follow the client
+    seed: int = 0
 
 
 class _StepGraph:
@@ -214,18 +216,20 @@ class CohortTrainer:
         if self._graphs_enabled():
             packed = torch.cat([idx, counts[..., None], active.to(torch.int32)[..., None],
                                 first.to(torch.int32)[..., None], lr.view(torch.int32)[..., None]], dim=2).to(dev)
+        ids = torch.tensor(client_ids if client_ids is not None else list(range(K)), dtype=torch.int64, device=dev)
         return RoundSchedule(idx.to(dev), counts.to(dev), active.to(dev), first.to(dev), lr.to(dev),
-                             epoch_end, S, K, packed)
+                             epoch_end, S, K, packed, ids, int(seed))
 
     # --------------------------------------------------------------------- train
-    def forward_loss(self, K: int, x, labels, valid, shared: bool = False, grad_rows=None, row0: int = 0):
+    def forward_loss(self, K: int, x, labels, valid, shared: bool = False, grad_rows=None, row0: int = 0,
+                     client_ids=None, step_seed: int = 0):
         """shared=True: all K clients use parameter row 0 (synchronous-gradient methods such as
         sign-SGD, where every client holds the same model); per-client gradients still land in
         separate rows of `grad_rows` (default grad[row0:row0+K])."""
         b = self.buffers
         grad = grad_rows if grad_rows is not None else b.grad[row0 : row0 + K]
         params = BoundParams(self.layout, b.compute[:1] if shared else b.compute[row0 : row0 + K], grad, K=K)
-        ctx = RunCtx(params, valid, training=True)
+        ctx = RunCtx(params, valid, training=True, client_ids=client_ids, seed=step_seed)
         logits = self.model.forward(x, ctx)
         loss, correct = Fn.cross_entropy(logits, labels, valid)
         return loss, correct
@@ -364,7 +368,9 @@ class CohortTrainer:
         x = self._gather(ds, idx)
         labels = ds.gather_labels(idx) if self.model.input_kind != "graph" else self.graph.labels_for(idx)
         valid = schedule.counts[s, a:b]
-        loss, correct = self.forward_loss(K, x, labels, valid, row0=a)
+        ids = schedule.client_ids[a:b] if schedule.client_ids is not None else None
+        loss, correct = self.forward_loss(K, x, labels, valid, row0=a, client_ids=ids,
+                                          step_seed=(schedule.seed * 7919 + s * 104_729) & 0x7FFFFFFF)
         loss.sum().backward()
         if self.debug and not bool(torch.isfinite(loss).all()):  # synchronising NaN scan
             bad = [a + i for i in (~torch.isfinite(loss)).nonzero().flatten().tolist()]

@@ -18,11 +18,27 @@ from ..ops import functional as Fn
 class RunCtx:
     """Per-pass context: bound params + per-client valid sample counts."""
 
-    def __init__(self, params, valid: torch.Tensor | None = None, training: bool = True):
+    def __init__(self, params, valid: torch.Tensor | None = None, training: bool = True,
+                 client_ids: torch.Tensor | None = None, seed: int = 0):
         self.P = params
         self.valid = valid  # [K] int32 number of real samples of each client this step
         self.training = training
+        self.client_ids = client_ids  # [K] int64: dropout masks keyed by client, not cohort row
+        self.seed = seed  # per training step
+        self._site = 0
         self._rows_cache: dict[int, torch.Tensor] = {}
+
+    def dropout_seeds(self) -> torch.Tensor:
+        """[K] int32 mask seeds of the next dropout site of this step: hash(step seed, site,
+        client id), so a client's masks do not depend on the rank / cohort row hosting it."""
+        from ..ops.fl import _mix
+
+        self._site += 1
+        ids = self.client_ids
+        if ids is None:
+            ids = torch.arange(self.P.K, device=self.P.compute.device)
+        h = _mix(ids.long(), (self.seed * 1_000_003 + self._site * 7919) & 0xFFFFFFFF)
+        return (h - (h >= 2**31).long() * 2**32).to(torch.int32).contiguous()
 
     @property
     def token(self):

@@ -271,29 +271,41 @@ class MultiheadAttention(Module):
         self.child("in_proj", Linear(d, 3 * d))
         self.child("out_proj", Linear(d, d))
 
-    def forward(self, x, ctx, key_valid, residual=None):
-        """Returns out_proj(attention) (+ residual, added in the projection's epilogue)."""
+    def forward(self, x, ctx, key_valid, residual=None, **drop):
+        """Returns out_proj(attention) (+ residual, added in the projection's epilogue; `drop`:
+        dropout of the projection output before that add)."""
         K, B, L, D = x.shape
         qkv = self.in_proj.forward(x, ctx)
         if Fn.packed_attention_ok(qkv, L, D // self.h):
             # heads read / written in place in the projections' row layouts (no permute copies)
             o = Fn.attention_packed(qkv, key_valid, self.h)
-            return self.out_proj.forward(o, ctx, residual=residual)
+            return self.out_proj.forward(o, ctx, residual=residual, **drop)
         qkv = qkv.reshape(K, B, L, 3, self.h, D // self.h)
         qkv = qkv.permute(3, 0, 1, 4, 2, 5)  # 3,K,B,H,L,dh
         o = Fn.attention(qkv[0].contiguous(), qkv[1].contiguous(), qkv[2].contiguous(), key_valid)
         o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
-        return self.out_proj.forward(o, ctx, residual=residual)
+        return self.out_proj.forward(o, ctx, residual=residual, **drop)
 
 
 class TransformerEncoderLayer(Module):
-    """Post-norm encoder layer, PyTorch `nn.TransformerEncoderLayer` defaults (ReLU FFN).
-    Dropout is not simulated (deterministic cohort execution)."""
+    """Post-norm encoder layer, PyTorch `nn.TransformerEncoderLayer` defaults (ReLU FFN,
+    dropout 0.1 in training), the reference's TransformerClassificationModel blocks.
+
+    Dropout sites: x + dropout(self_attn(x)), the FFN's dropout(relu(linear1)), x + dropout(ff).
+    All three are masks inside the GEMM epilogues:
+    - residual branches are masked before the residual add;
+    - the FFN ReLU output is masked in linear1's epilogue, and linear2's ReLU'-gated dgrad
+      epilogue (h > 0 iff kept and positive) carries the 1/(1-p).
+    Masks come from (step seed, site, client id) hashes (RunCtx.dropout_seeds), so they do not
+    depend on which rank or cohort row trains a client. Attention-probability dropout (nn.MHA's
+    own `dropout`) is not simulated: a per-score mask would cost more than the attention itself
+    on the MFMA path."""
 
     kind = "TransformerEncoderLayer"
 
-    def __init__(self, d, h, ff):
+    def __init__(self, d, h, ff, dropout: float = 0.1):
         super().__init__()
+        self.dropout = float(dropout)
         self.child("self_attn", MultiheadAttention(d, h))
         self.child("linear1", Linear(d, ff))
         self.child("linear2", Linear(ff, d))
@@ -301,20 +313,28 @@ class TransformerEncoderLayer(Module):
         self.child("norm2", LayerNorm(d))
 
     def forward(self, x, ctx, key_valid):
-        # residual adds and the FFN ReLU (forward and backward) ride in the GEMM epilogues
-        x = self.norm1.forward(self.self_attn.forward(x, ctx, key_valid, residual=x), ctx)
-        h = self.linear1.forward(x, ctx, relu=True, premasked=True)
-        return self.norm2.forward(self.linear2.forward(h, ctx, gate_input=True, residual=x), ctx)
+        p = self.dropout if ctx.training else 0.0
+
+        def drop():
+            return {"drop_p": p, "drop_seeds": ctx.dropout_seeds()} if p else {}
+
+        # residual adds, the FFN ReLU and the dropout masks (forward and backward) ride in the
+        # GEMM epilogues
+        x = self.norm1.forward(self.self_attn.forward(x, ctx, key_valid, residual=x, **drop()), ctx)
+        h = self.linear1.forward(x, ctx, relu=True, premasked=True, **drop())
+        y = self.linear2.forward(h, ctx, gate_input=True, residual=x, gate_scale=1.0 / (1.0 - p), **drop())
+        return self.norm2.forward(y, ctx)
 
 
 class TransformerClassifier(Module):
     kind = "TransformerClassificationModel"
 
-    def __init__(self, vocab, d, h, layers, ff, classes, max_len):
+    def __init__(self, vocab, d, h, layers, ff, classes, max_len, dropout: float = 0.1):
         super().__init__()
         self.d, self.max_len = d, max_len
         self.child("embedding", Embedding(vocab, d))
-        self.layers = [self.child(f"encoder.layers.{i}", TransformerEncoderLayer(d, h, ff)) for i in range(layers)]
+        self.layers = [self.child(f"encoder.layers.{i}", TransformerEncoderLayer(d, h, ff, dropout))
+                       for i in range(layers)]
         self.child("classifier", Linear(d, classes))
         pe = torch.zeros(max_len, d)
         pos = torch.arange(max_len).float()[:, None]
@@ -465,7 +485,8 @@ def build_model(name: str, dataset_spec, model_kwargs: dict | None = None) -> Co
             return CohortModel(
                 TransformerClassifier(dataset_spec.vocab_size, d, int(kw.get("nhead", 5)),
                                       int(kw.get("num_encoder_layer", 2)), int(kw.get("dim_feedforward", 2048)),
-                                      classes, int(kw.get("max_len", dataset_spec.max_len))),
+                                      classes, int(kw.get("max_len", dataset_spec.max_len)),
+                                      float(kw.get("dropout", 0.1))),
                 name, "tokens", classes)
     if dataset_spec.kind == "graph":
         layers = {"onegcn": 1, "twogcn": 2, "simplegcn": 2, "gcn": 2}.get(n)

@@ -127,28 +127,39 @@ class _Linear(torch.autograd.Function):
                 so this backward takes dy as d(pre-activation) directly;
     gate_input— x is a ReLU output: dX leaves through ReLU' (zeroed where x <= 0) in the dgrad
                 epilogue, one pass instead of a separate threshold-backward;
-    residual  — y += residual in the epilogue (its gradient is dy, passed straight through)."""
+    residual  — y += residual in the epilogue (its gradient is dy, passed straight through);
+    drop_p    — dropout of the GEMM output (after the ReLU, before the residual add) in the
+                epilogue, mask from `drop_seeds` [K] (ops dropout_apply rule); the backward masks
+                the GEMM branch's gradient once (premasked outputs leave that to the consumer);
+    gate_scale— the 1/(1-p) of the producer's dropout, applied with the gate_input ReLU'."""
 
     @staticmethod
-    def forward(ctx, x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False):
+    def forward(ctx, x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False,
+                drop_p=0.0, drop_seeds=None, gate_scale=1.0):
         be = _be(x)
-        y = be.linear_fwd(x, w, b, relu=relu, acc=residual)
+        y = be.linear_fwd(x, w, b, relu=relu, acc=residual, drop_p=drop_p, drop_seeds=drop_seeds)
         mask_dy = relu and not premasked
-        ctx.save_for_backward(x, w, y if mask_dy else None)
+        ctx.save_for_backward(x, w, y if mask_dy else None, drop_seeds if drop_p else None)
         ctx.gw, ctx.gb = gw, gb
         ctx.mask_dy, ctx.gate_input, ctx.has_res = mask_dy, gate_input, residual is not None
+        ctx.drop_p, ctx.premasked, ctx.gate_scale = drop_p, premasked, gate_scale
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
+        x, w, y, seeds = ctx.saved_tensors
         be = _be(dy)
         dy = dy.contiguous()
         dres = dy if ctx.has_res else None
         if ctx.mask_dy:
+            # y > 0 iff the unit was kept AND its pre-activation was positive
             dy = dy * (y > 0).to(dy.dtype)
+            if ctx.drop_p:
+                dy = dy * (1.0 / (1.0 - ctx.drop_p))
+        elif ctx.drop_p and not ctx.premasked:
+            dy = be.dropout_apply(dy, seeds, ctx.drop_p)  # the GEMM branch's gradient
         gate = x.contiguous() if ctx.gate_input else None
-        dx = be.linear_dgrad(dy, w, gate=gate) if ctx.needs_input_grad[0] else None
+        dx = be.linear_dgrad(dy, w, gate=gate, gate_scale=ctx.gate_scale) if ctx.needs_input_grad[0] else None
         if ctx.gw is not None:
             if be is ref:
                 dw, db = ref.linear_wgrad(dy.float(), x.float(), ctx.gb is not None)
@@ -157,17 +168,18 @@ class _Linear(torch.autograd.Function):
                     ctx.gb.copy_(db)
             else:
                 be.linear_wgrad(dy, x, ctx.gw, ctx.gb)
-        return dx, None, None, None, None, None, dres, None, None, None
+        return dx, None, None, None, None, None, dres, None, None, None, None, None, None
 
 
-def linear(x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False):
+def linear(x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False,
+           drop_p: float = 0.0, drop_seeds=None, gate_scale: float = 1.0):
     """x [K, N, Fi] -> [K, N, Fo]; any extra middle dims are flattened. Epilogue fusions: see
-    _Linear (relu / premasked / gate_input / residual)."""
+    _Linear (relu / premasked / gate_input / residual / dropout)."""
     assert not (relu and residual is not None), "ReLU and residual epilogues are not combined"
     shp = x.shape
     x3 = x.reshape(shp[0], -1, shp[-1])
     r3 = residual.reshape(shp[0], x3.shape[1], -1).contiguous() if residual is not None else None
-    y = _Linear.apply(x3, token, w, b, gw, gb, r3, relu, premasked, gate_input)
+    y = _Linear.apply(x3, token, w, b, gw, gb, r3, relu, premasked, gate_input, drop_p, drop_seeds, gate_scale)
     return y.reshape(*shp[:-1], y.shape[-1])
 
 

@@ -185,7 +185,7 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
         return y
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), x.stride(0), y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
                pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32,
-               _s(), ldx, ldy, _p(stats), _p(stats_valid))
+               _s(), ldx, ldy, _p(stats), _p(stats_valid), NULL, 0.0, 0.0)
     return y
 
 
@@ -248,8 +248,10 @@ def bias_grad(dy, gb):
 
 
 # --------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b=None, relu=False, acc=None):
-    """y = x Wᵀ + b, optionally ReLU'd and/or + `acc` (a residual branch) in the epilogue."""
+def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_seeds=None):
+    """y = x Wᵀ + b, optionally ReLU'd, dropped out (`drop_p`, per-client-row `drop_seeds`
+    [K] int32: the epilogue mask of `dropout_apply`) and/or + `acc` (a residual branch), in the
+    epilogue."""
     K, N, Fi = x.shape
     x = x.contiguous()
     f32 = _f32(x)
@@ -261,13 +263,15 @@ def linear_fwd(x, w, b=None, relu=False, acc=None):
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
-               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL)
+               int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL,
+               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0)
     return y
 
 
-def linear_dgrad(dy, w, gate=None):
+def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0):
     """dX = dY W, zeroed where `gate` <= 0 when given (gate = the ReLU output this layer read:
-    the gradient then leaves already through the ReLU)."""
+    the gradient then leaves already through the ReLU), times `gate_scale` (the 1/(1-p) of a
+    dropout folded into that ReLU output)."""
     K, N, Fo = dy.shape
     dy = dy.contiguous()
     f32 = _f32(dy)
@@ -280,8 +284,28 @@ def linear_dgrad(dy, w, gate=None):
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
                1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0,
-               NULL, NULL)
+               NULL, NULL, NULL, 0.0, float(gate_scale))
     return dx
+
+
+def _drop_seeds(seeds, K: int, p: float):
+    if not p:
+        return None
+    assert seeds is not None and seeds.dtype == torch.int32 and seeds.numel() == K and seeds.is_contiguous()
+    return seeds
+
+
+def dropout_apply(x, seeds, p: float):
+    """out = keep ? x / (1-p) : 0 over x [K, rows, N] — the GEMM epilogue's dropout mask (the
+    backward of a dropout fused into a linear's output)."""
+    K = x.shape[0]
+    N = x.shape[-1]
+    x = x.contiguous()
+    rows = x.numel() // (K * N)
+    out = torch.empty_like(x)
+    _C.dropout_apply(_p(x), _p(out), K, rows, N, N, _p(_drop_seeds(seeds, K, p)), float(p), 1.0 / (1.0 - p),
+                     _f32(x), _s())
+    return out
 
 
 def linear_wgrad(dy, x, gw, gb=None):

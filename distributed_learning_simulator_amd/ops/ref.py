@@ -75,7 +75,26 @@ def conv_wgrad(dy, x, w_shape, stride: int, pad: int):
 
 
 # ---------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b=None, relu=False, acc=None):
+def dropout_keep(K: int, rows: int, N: int, seeds, p: float) -> torch.Tensor:
+    """[K, rows, N] keep mask of the GEMM-epilogue dropout (common.h drop_keep):
+    mix32(m·N + n, seed_k) >= p·2^32."""
+    import numpy as np
+
+    from .fl import _mix
+
+    thr = int(min(float(np.float32(p) * np.float32(4294967296.0)), 4294967040.0))
+    idx = torch.arange(rows * N, dtype=torch.int64, device=seeds.device).view(1, rows * N)
+    sk = (seeds.long() & 0xFFFFFFFF).view(K, 1)
+    return (_mix(idx, sk) >= thr).view(K, rows, N)
+
+
+def dropout_apply(x, seeds, p: float):
+    K, N = x.shape[0], x.shape[-1]
+    keep = dropout_keep(K, x.numel() // (K * N), N, seeds.to(x.device), p).view(x.shape)
+    return torch.where(keep, x * (1.0 / (1.0 - p)), torch.zeros_like(x))
+
+
+def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_seeds=None):
     K = x.shape[0]
     w = _match(w, K)
     y = torch.bmm(x, w.transpose(1, 2))
@@ -84,15 +103,19 @@ def linear_fwd(x, w, b=None, relu=False, acc=None):
         y = y + b[:, None, :]
     if relu:
         y = torch.relu(y)
+    if drop_p:
+        y = dropout_apply(y, drop_seeds, drop_p)
     if acc is not None:
         y = y.to(acc.dtype) + acc
     return y
 
 
-def linear_dgrad(dy, w, gate=None):
+def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0):
     K = dy.shape[0]
     w = _match(w, K)
     dx = torch.bmm(dy, w)
+    if gate_scale != 1.0:
+        dx = dx * gate_scale
     return dx if gate is None else dx * (gate > 0).to(dx.dtype)
 
 

@@ -87,7 +87,7 @@ def test_conv_f32_every_variant(hip, case):
     for v in range(hip._C.conv_nt_f32_num_variants()):
         y = torch.empty_like(dy)
         hip._C.conv_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, B * H * W * Ci, M * Co, w.stride(0), 0, B, H, W,
-                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0, 0, 0)
+                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0, 0, 0, 0, 0.0, 0.0)
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
@@ -371,3 +371,25 @@ def test_conv_epilogue_bn_stats(hip, case):
     _close(mb, ma, 1e-5)
     _close(rb, ra, 1e-4)
     _close(yb, ya, 1e-4)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_linear_epilogue_dropout_matches_cpu_rule(hip, dtype, tol):
+    """Dropout in the GEMM epilogue (before the residual add) and the standalone dropout_apply
+    use exactly the CPU oracle's keep rule (ref.dropout_keep); the dgrad gate carries the scale."""
+    K, N, Fi, Fo, p = 3, 200, 96, 64, 0.3
+    x, w, b, r = _f(K, N, Fi).to(dtype), _f(K, Fo, Fi, scale=0.1).to(dtype), _f(K, Fo).to(dtype), _f(K, N, Fo).to(dtype)
+    seeds = torch.tensor([5, -7, 123456789], dtype=torch.int32, device=DEV)
+    y = hip.linear_fwd(x, w, b, acc=r, drop_p=p, drop_seeds=seeds)
+    exp = ref.linear_fwd(_d(x), _d(w), _d(b), acc=_d(r), drop_p=p, drop_seeds=seeds.cpu())
+    _close(y, exp, tol)
+    keep = ref.dropout_keep(K, N, Fo, seeds.cpu(), p)
+    y0 = hip.linear_fwd(x, w, b, drop_p=p, drop_seeds=seeds)  # (no residual: drops are exact zeros)
+    assert torch.equal(y0.cpu() != 0, keep)  # dropped exactly where the rule says
+    d = _f(K, N, Fo).to(dtype)
+    torch.testing.assert_close(hip.dropout_apply(d, seeds, p).cpu().float(),
+                               ref.dropout_apply(d.cpu().float(), seeds.cpu(), p), rtol=tol, atol=tol)
+    gate = torch.relu(_f(K, N, Fi)).to(dtype)
+    dy = _f(K, N, Fo).to(dtype)
+    _close(hip.linear_dgrad(dy, w, gate=gate, gate_scale=1 / (1 - p)),
+           ref.linear_dgrad(_d(dy), _d(w), gate=_d(gate), gate_scale=1 / (1 - p)), tol)

@@ -148,7 +148,8 @@ def test_transformer_epilogue_fusions_match_unfused(monkeypatch):
     torch.manual_seed(0)
     spec = get_spec("imdb", {"max_len": 16})
     model = build_model("TransformerClassificationModel", spec,
-                        {"d_model": 16, "nhead": 2, "num_encoder_layer": 2, "max_len": 16, "dim_feedforward": 64})
+                        {"d_model": 16, "nhead": 2, "num_encoder_layer": 2, "max_len": 16, "dim_feedforward": 64,
+                         "dropout": 0.0})
     g = torch.Generator().manual_seed(3)
     theta = model.layout.init_flat(g).unsqueeze(0)
     tokens = torch.randint(1, spec.vocab_size if hasattr(spec, "vocab_size") else 100, (1, 3, 16))
@@ -213,3 +214,40 @@ def test_densenet_fused_block_matches_autograd_concat():
         got = layout.unflatten(grad[k])
         for kk, v in t.items():
             torch.testing.assert_close(got[kk], v.grad, rtol=1e-3, atol=1e-5, msg=kk)
+
+
+def test_transformer_dropout_epilogues_match_explicit_masks(monkeypatch):
+    """Dropout fused into the GEMM epilogues (residual branches, FFN ReLU output with the scaled
+    dgrad gate) == the plain composition with explicit masks (ref.dropout_apply, same seeds):
+    loss and every gradient. Different clients / steps get different masks."""
+    from distributed_learning_simulator_amd.models import zoo
+    from distributed_learning_simulator_amd.ops import ref
+
+    torch.manual_seed(0)
+    spec = get_spec("imdb", {"max_len": 16})
+    model = build_model("TransformerClassificationModel", spec,
+                        {"d_model": 16, "nhead": 2, "num_encoder_layer": 2, "max_len": 16, "dim_feedforward": 64,
+                         "dropout": 0.3})
+    K = 2
+    theta = torch.stack([model.layout.init_flat(torch.Generator().manual_seed(s)) for s in (3, 4)])
+    tokens = torch.randint(1, 100, (K, 3, 16))
+    lengths = torch.tensor([[16, 9, 4], [5, 16, 12]])
+    y = torch.randint(0, spec.num_classes, (K, 3))
+    fused = _run(model, (tokens, lengths), y, K, theta.clone())
+
+    def plain(self, x, ctx, key_valid):
+        p = self.dropout
+        a = self.self_attn.forward(x, ctx, key_valid)
+        x = self.norm1.forward(x + ref.dropout_apply(a, ctx.dropout_seeds(), p), ctx)
+        h = ref.dropout_apply(torch.relu(self.linear1.forward(x, ctx)), ctx.dropout_seeds(), p)
+        f = self.linear2.forward(h, ctx)
+        return self.norm2.forward(x + ref.dropout_apply(f, ctx.dropout_seeds(), p), ctx)
+
+    monkeypatch.setattr(zoo.TransformerEncoderLayer, "forward", plain)
+    explicit = _run(model, (tokens, lengths), y, K, theta.clone())
+    torch.testing.assert_close(fused[0], explicit[0])
+    torch.testing.assert_close(fused[1], explicit[1], rtol=1e-4, atol=1e-6)
+    # the masks really drop ~30 % and differ between clients
+    seeds = torch.tensor([11, 12], dtype=torch.int32)
+    keep = ref.dropout_keep(2, 48, 16, seeds, 0.3)
+    assert 0.6 < keep.float().mean().item() < 0.8 and not torch.equal(keep[0], keep[1])
