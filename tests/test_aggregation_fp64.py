@@ -63,7 +63,8 @@ def _worker(rank, world, port, q):
 
     commmod._COMM = None
     c = commmod.init_distributed(prefer_gpu=False)
-    q.put((rank,) + _aggregate(rank, world, list(range(100)), 3, c))
+    new32, new64 = _aggregate(rank, world, list(range(100)), 3, c)
+    q.put((rank, new32.numpy().copy(), new64.numpy().copy()))  # by value (see test_distributed)
     commmod.shutdown()
 
 
@@ -78,6 +79,7 @@ def test_fedavg_fp64_two_ranks_three_cohorts():
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    outs = [(r, torch.from_numpy(a), torch.from_numpy(b)) for r, a, b in outs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -50,7 +50,8 @@ def _worker(rank, world, port, algo, tmp, extra, q):
     c = commmod.init_distributed(prefer_gpu=False)
     sess = Session(_cfg(algo, tmp, extra), comm=c)
     res = sess.run()
-    q.put((rank, sess.server.global_parameter.clone(), res["performance"], res["bytes_up"], res.get("sv")))
+    # numpy pickles by value: a tensor would travel as a shared-memory fd that dies with this process
+    q.put((rank, sess.server.global_parameter.cpu().numpy().copy(), res["performance"], res["bytes_up"], res.get("sv")))
     commmod.shutdown()
 
 
@@ -65,6 +66,7 @@ def _run_world(world, algo, tmp, extra=None):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    out = [(o[0], torch.from_numpy(o[1]), *o[2:]) for o in out]
     return sorted(out, key=lambda t: t[0])
 
 

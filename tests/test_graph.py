@@ -177,7 +177,8 @@ def _worker(rank, world, port, algo, tmp, ak, q):
     sess = Session(_cfg(algo, tmp, ak), comm=c)
     sess.run()
     w = sess.worker
-    q.put((rank, sess.server.global_parameter.clone(), w._communicated_embedding_bytes, w._skipped_embedding_bytes))
+    q.put((rank, sess.server.global_parameter.cpu().numpy().copy(), w._communicated_embedding_bytes,
+           w._skipped_embedding_bytes))
     commmod.shutdown()
 
 
@@ -212,6 +213,7 @@ def test_sampled_gnn_ranks_match_single_rank(tmp_path, algo, ak, world):
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=600) for _ in procs], key=lambda t: t[0])
+    outs = [(o[0], torch.from_numpy(o[1]), *o[2:]) for o in outs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
