@@ -30,6 +30,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -120,6 +121,16 @@ def main() -> None:
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
+    # heartbeat: long rounds (GTG utilities, ResNet-50) stay visibly alive on stderr
+    t_start = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(60)
+            if comm.rank == 0:
+                print(f"[bench] alive {time.perf_counter() - t_start:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     for _ in range(args.warmup):
         theta = sess.run_one_round(theta)
         progress("warmup")
@@ -266,10 +277,12 @@ def workload_config(args, rounds: int) -> dict:
                 "data": "synthetic (AG-News-shaped token sequences, max_len 128, iid shards, random-init weights)"}
     if args.workload == "signsgd_resnet50":
         cfg = {"distributed_algorithm": "sign_SGD", "dataset_name": "ImageNet", "model_name": "Resnet50",
-               "dataset_kwargs": {"scale": 0.01}, "worker_number": 128, "epoch": 1, "batch_size": 128,
+               "dataset_kwargs": {"scale": 0.1}, "worker_number": 128, "epoch": 1, "batch_size": 128,
                "optimizer_name": "SGD", "learning_rate": 0.001, "momentum": 0.0, "distribute_init_parameters": False}
         return {"config": {**cfg, **common}, "metric": "FL rounds/sec (sign-SGD, 128 clients, ResNet-50, ImageNet-shaped)",
-                "data": "synthetic (ImageNet-shaped 224x224, 1% scale shards, random-init weights)",
+                # 10 % of ImageNet dealt to 128 clients (1,000 images each): a round is one local epoch,
+                # 8 synchronous steps of batch 128, each a 1-bit vote exchange across all clients
+                "data": "synthetic (ImageNet-shaped 224x224, 10% scale shards, random-init weights)",
                 "samples_per_round": shard_samples}
     # utility v(S) = test accuracy of the subset model on the FULL test split (reference
     # shapley_value_algorithm.py:67-76); 5 local epochs as conf/gtg_sv/cifar10.yaml

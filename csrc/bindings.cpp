@@ -216,6 +216,11 @@ PYBIND11_MODULE(_dls_hip, m) {
                             int f32, ptr s) {
     dropout_apply(P<const void>(x), P<void>(out), K, rows, N, ld, P<const uint32_t>(seeds), p, scale, f32, S(s));
   });
+  m.def("synth_images", [](ptr idx, long n, long npix, int C, int Cout, ptr source, ptr proto,
+                           unsigned long long salt, float sqrt6, float noise, ptr out, ptr s) {
+    synth_images(P<const int64_t>(idx), n, npix, C, Cout, P<const int>(source), P<const float>(proto), salt, sqrt6,
+                 noise, P<float>(out), S(s));
+  });
   m.def("quant_pack", [](ptr x, long ld, ptr seg, ptr seg_off, ptr seg_numel, ptr bits, ptr lo, ptr scale,
                          ptr seg_byte_off, ptr row_off, int K, int nseg, long Pn, int stochastic, ptr seeds, ptr out,
                          ptr s) {

@@ -190,6 +190,10 @@ void quant_unpack_acc(const uint8_t* codes, const int* seg, const int64_t* seg_o
 void dropout_apply(const void* x, void* out, int K, long rows, int N, long ld, const uint32_t* seeds, float p,
                    float scale, int f32, hipStream_t s);
 
+// procedural synthetic images (data/datasets.py, bit-identical to the torch generator): out [n][npix/C·Cout]
+void synth_images(const int64_t* idx, long n, long npix, int C, int Cout, const int* source, const float* proto,
+                  unsigned long long salt, float sqrt6, float noise, float* out, hipStream_t s);
+
 // ---------------------------------------------------------------- graph (graph.hip)
 // Federated-GNN neighbour sampling: per frontier row (nodes[t] expanded for client clients[t])
 // the `fanout` (<= 32) in-neighbours with the smallest hash keys; out_nbr [n][fanout] (-1 pad).

@@ -504,6 +504,42 @@ __global__ void dropout_apply_kernel(const T* __restrict__ x, T* __restrict__ ou
   }
 }
 
+// procedural synthetic images (data/datasets.py SyntheticImages._generate, bit-identical):
+// h = lowbias32(idx·0x9E3779B1 + p·0x85EBCA77 + salt), h2 = lowbias32(h + 0x68E31DA4),
+// x = proto[class][p] + ((h + h2)·2^-32 − 1)·√6·noise, channels zero-padded C → Cout
+__device__ __forceinline__ uint64_t lowbias32(uint64_t x) {
+  x &= 0xFFFFFFFFull;
+  x ^= x >> 16;
+  x = (x * 0x7FEB352Dull) & 0xFFFFFFFFull;
+  x ^= x >> 15;
+  x = (x * 0x846CA68Bull) & 0xFFFFFFFFull;
+  return x ^ (x >> 16);
+}
+
+__global__ void synth_images_kernel(const int64_t* __restrict__ idx, long n, long npix, int C, int Cout,
+                                    const int* __restrict__ source, const float* __restrict__ proto,
+                                    unsigned long long salt, float sqrt6, float noise, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  const long per = npix / C * Cout;
+  const long total = n * per;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long i = t / per, q = t - i * per;
+    const long px = q / Cout;
+    const int c = (int)(q - px * Cout);
+    if (c >= C) {
+      out[t] = 0.f;
+      continue;
+    }
+    const long p = px * C + c;
+    const uint64_t id = (uint64_t)idx[i];
+    const uint64_t h = lowbias32(id * 0x9E3779B1ull + (uint64_t)p * 0x85EBCA77ull + salt);
+    const uint64_t h2 = lowbias32(h + 0x68E31DA4ull);
+    const float u = ((float)h + (float)h2) * (1.f / 4294967296.f) - 1.f;
+    const float nz = (u * sqrt6) * noise;
+    out[t] = proto[(long)source[id] * npix + p] + nz;
+  }
+}
+
 __global__ void sign_pack_kernel(const float* __restrict__ g, uint8_t* __restrict__ out, long P, long ld,
                                  long nbytes) {
   const int k = blockIdx.y;
@@ -783,4 +819,12 @@ void dropout_apply(const void* x, void* out, int K, long rows, int N, long ld, c
   else
     hipLaunchKernelGGL(dropout_apply_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(x),
                        static_cast<bf16_t*>(out), rows, N, ld, seeds, p, scale);
+}
+
+void synth_images(const int64_t* idx, long n, long npix, int C, int Cout, const int* source, const float* proto,
+                  unsigned long long salt, float sqrt6, float noise, float* out, hipStream_t s) {
+  const long total = n * (npix / C) * Cout;
+  if (total == 0) return;
+  hipLaunchKernelGGL(synth_images_kernel, dim3((unsigned)std::min<long>(cdiv(total, 256), 65536)), dim3(256), 0, s,
+                     idx, n, npix, C, Cout, source, proto, salt, sqrt6, noise, out);
 }

@@ -170,6 +170,17 @@ class ImageDataset:
         H, W, C = self.spec.shape
         npix = H * W * C
         idx = idx.to(device).long()
+        from ..ops import backend
+
+        if backend.using_hip(self.proto_dev):  # one fused pass (csrc/elementwise.hip synth_images)
+            from ..ops import hip
+
+            if getattr(self, "_proto32", None) is None:
+                self._proto32 = self.prototypes.to(device, torch.float32).contiguous()
+                self._source32 = self.source.to(device, torch.int32).contiguous()
+            img = hip.synth_images(idx.contiguous(), npix, C, self.channels, self._source32, self._proto32,
+                                   self.salt, math.sqrt(6.0), self.noise)
+            return img.view(-1, H, W, self.channels).to(dtype)
         pix = torch.arange(npix, device=device, dtype=torch.int64)
         h = _hash_u32(idx[:, None] * 0x9E3779B1 + pix[None, :] * 0x85EBCA77 + self.salt)
         h2 = _hash_u32(h + 0x68E31DA4)

@@ -610,6 +610,17 @@ def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None):
     return dqkv
 
 
+# -------------------------------------------------------------- synthetic data
+def synth_images(idx, npix: int, C: int, Cout: int, source32, proto32, salt: int, sqrt6: float, noise: float):
+    """Procedural synthetic images (data/datasets.py generator, bit-identical) -> fp32 [n, npix/C*Cout]."""
+    n = idx.numel()
+    assert idx.dtype == torch.int64 and source32.dtype == torch.int32 and proto32.dtype == torch.float32
+    out = torch.empty((n, npix // C * Cout), dtype=torch.float32, device=idx.device)
+    _C.synth_images(_p(idx), n, npix, C, Cout, _p(source32), _p(proto32), int(salt) & 0xFFFFFFFFFFFFFFFF,
+                    float(sqrt6), float(noise), _p(out), _s())
+    return out
+
+
 # ------------------------------------------------------------- compressed payloads
 def _payload_args(p):
     m = p.meta

@@ -393,3 +393,18 @@ def test_linear_epilogue_dropout_matches_cpu_rule(hip, dtype, tol):
     dy = _f(K, N, Fo).to(dtype)
     _close(hip.linear_dgrad(dy, w, gate=gate, gate_scale=1 / (1 - p)),
            ref.linear_dgrad(_d(dy), _d(w), gate=_d(gate), gate_scale=1 / (1 - p)), tol)
+
+
+def test_synthetic_image_generator_matches_cpu(hip):
+    """ImageNet-size synthetic images are generated by one HIP pass, bit-identical to the
+    torch generator the CPU path uses (same data on every device)."""
+    from distributed_learning_simulator_amd.data.datasets import ImageDataset, get_spec
+
+    spec = get_spec("ImageNet", {"scale": 0.0005})
+    cpu = ImageDataset(spec, "train", 3, torch.device("cpu"), torch.float32, materialize_limit=0, channels=8)
+    gpu = ImageDataset(spec, "train", 3, torch.device(DEV), torch.float32, materialize_limit=0, channels=8)
+    idx = torch.tensor([0, 5, 17, spec.n_train - 1])
+    a = gpu.gather(idx.to(DEV)).cpu()
+    b = cpu.gather(idx)
+    assert a.shape == b.shape == (4, 224, 224, 8)
+    assert torch.equal(a, b)
