@@ -52,6 +52,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--cohort", type=int, default=0)
+    ap.add_argument("--log-level", default="WARNING", help="simulator log level (INFO shows GTG progress)")
     ap.add_argument("--no-stage2", action="store_true", help="FedOBD workloads: skip timing the second phase")
     ap.add_argument("--amp", action="store_true",
                     help="bf16 fast mode (use_amp: true). Default: fp32, the reference's precision "
@@ -70,7 +71,7 @@ def main() -> None:
         sys.exit(launch.spawn_ranks(args.gpus))
     if args.backend == "torch":
         os.environ["DLS_BACKEND"] = "torch"
-    os.environ.setdefault("DLS_LOG_LEVEL", "WARNING")
+    os.environ.setdefault("DLS_LOG_LEVEL", args.log_level)
 
     import torch
     import torch.distributed as dist
@@ -209,7 +210,7 @@ def main() -> None:
 
 
 def workload_config(args, rounds: int) -> dict:
-    common = {"round": rounds + 1000, "save_models": False, "log_level": "WARNING", "cohort_size": args.cohort,
+    common = {"round": rounds + 1000, "save_models": False, "log_level": args.log_level, "cohort_size": args.cohort,
               "use_amp": bool(args.amp),
               "save_dir": os.path.join("/tmp", f"dls_bench_{os.getpid()}")}
 

@@ -62,8 +62,8 @@ __device__ __forceinline__ int swz(int r, int e) {
 }
 
 // ------------------------------------------------------------------------- NT (fwd / dgrad)
-template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int NBUF>
-__global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p) {
+template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int NBUF, int MINW = 1>
+__global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTParams p) {
   constexpr int T = WM * WN * 64;
   constexpr int TM = BM / (WM * 32);
   constexpr int TN = BN / (WN * 32);
@@ -388,16 +388,16 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_nt_f32_kernel(ConvNTParams p
 
 // VSET 0: the 32-B (8, 8) gathers of wide layers; 1: + 16-B (4, ·) widths (d_model = 100,
 // DenseNet's 12-channel growth); 2: every combination incl. scalar (stems, LeNet, tiny linears)
-template <int BM, int BN, int BK, int WM, int WN, int NBUF, int VSET>
+template <int BM, int BN, int BK, int WM, int WN, int NBUF, int VSET, int MINW = 1>
 bool launch_nt_f32_cfg(const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStream_t s) {
   const int grid = K * cdiv(p.M, BM) * cdiv(p.N, BN);
 #define NTF_CASE(A, B)                                                                                       \
   if (va == A && vb == B) {                                                                                  \
     if (bkm)                                                                                                 \
-      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, A, B, true, NBUF>), dim3(grid),             \
+      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, A, B, true, NBUF, MINW>), dim3(grid),             \
                          dim3(WM * WN * 64), 0, s, p);                                                       \
     else                                                                                                     \
-      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, A, B, false, NBUF>), dim3(grid),            \
+      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, A, B, false, NBUF, MINW>), dim3(grid),            \
                          dim3(WM * WN * 64), 0, s, p);                                                       \
     return true;                                                                                             \
   }
@@ -419,6 +419,9 @@ bool launch_nt_f32_variant(int v, const ConvNTParams& p, int K, int va, int vb, 
     case 5: return launch_nt_f32_cfg<128, 128, 64, 2, 2, 1, 0>(p, K, va, vb, bkm, s);  // 72 KB
     case 6: return launch_nt_f32_cfg<256, 64, 32, 4, 1, 1, 0>(p, K, va, vb, bkm, s);   // 50 KB, N <= 64
     case 7: return launch_nt_f32_cfg<64, 64, 32, 2, 2, 1, 1>(p, K, va, vb, bkm, s);    // 20 KB
+    // variants 1 / 6 compiled for 3 waves per SIMD (<= 168 registers) instead of 2
+    case 8: return launch_nt_f32_cfg<128, 128, 32, 2, 2, 1, 0, 3>(p, K, va, vb, bkm, s);
+    case 9: return launch_nt_f32_cfg<256, 64, 32, 4, 1, 1, 0, 3>(p, K, va, vb, bkm, s);
     default: return false;
   }
 }
@@ -664,7 +667,7 @@ void tn_f32_split(int K, int Co, int R, int M, int variant, int& splitk, int& mp
 
 }  // namespace
 
-int conv_nt_f32_num_variants() { return 8; }
+int conv_nt_f32_num_variants() { return 10; }
 
 void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
   const bool bkm = p.b_kmajor != 0;

@@ -211,10 +211,11 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
 //  fwd:  coef = {scale = γ·rstd, shift = β − mean·scale};  also publishes mean / rstd
 //  bwd:  dx = a·g + d + e·x  with a = γ·rstd, e = −a·rstd·Σgx̂/n, d = −a·Σg/n − e·mean;
 //        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
-// grid (cdiv(C, 32), K), 256 threads = 32 channels × 8 part-groups: the per-workgroup partial
+// grid (cdiv(C, 32), K), 1024 threads = 32 channels × 32 part-groups: the per-workgroup partial
 // sums of a client are reduced in a fixed order (deterministic) by 8 lanes per channel.
+constexpr int COEF_GROUPS = 32;  // partial-sum rows reduced in parallel per channel
 template <typename T>
-__global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ ws, int nparts,
+__global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const float* __restrict__ ws, int nparts,
                                                       const T* __restrict__ gamma,
                                                       const T* __restrict__ beta, const int* __restrict__ valid_rows,
                                                       const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -224,14 +225,14 @@ __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ 
                                                       float eps, int rep, int bwd) {
   // partials are summed in fp64 (the conv-epilogue statistics arrive as thousands of 32-row
   // partials per channel; Σx² − n·μ² then keeps its precision), in a fixed order
-  __shared__ double red[2][8][33];
+  __shared__ double red[2][COEF_GROUPS][33];
   const int k = blockIdx.y;
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   double d0 = 0.0, d1 = 0.0;
   if (c < C) {
     const float* part = ws + (long)k * nparts * 2 * C;
-    for (int b = grp; b < nparts; b += 8) {
+    for (int b = grp; b < nparts; b += COEF_GROUPS) {
       d0 += part[(long)b * 2 * C + c];
       d1 += part[(long)b * 2 * C + C + c];
     }
@@ -241,7 +242,7 @@ __global__ void __launch_bounds__(256) bn_coef_kernel(const float* __restrict__ 
   __syncthreads();
   if (grp != 0 || c >= C) return;
 #pragma unroll
-  for (int g2 = 1; g2 < 8; ++g2) {
+  for (int g2 = 1; g2 < COEF_GROUPS; ++g2) {
     d0 += red[0][g2][cl];
     d1 += red[1][g2][cl];
   }
@@ -542,7 +543,7 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
                                        nullptr, ca, ldx, ldx));
     }
     if (!counters || pre_part)
-      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, nparts, CP(gamma),
+      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, nparts, CP(gamma),
                          CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C,
                          eps, rep, 0);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
@@ -566,7 +567,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
     DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                      mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
     if (!counters)
-      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(256), 0, s, part, (int)grid.x, CP(gamma),
+      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, (int)grid.x, CP(gamma),
                          (const TT*)nullptr, valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs,
                          g_cs, K, R, C, 0.f, 1, 1);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),

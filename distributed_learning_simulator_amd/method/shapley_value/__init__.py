@@ -114,6 +114,7 @@ class ShapleyValueAlgorithm(FedAVGAlgorithm):
         else:
             self.sv_algorithm.reset_players(ids, last_metric)
         chunk = int(self.config.algorithm_kwargs.get("sv_eval_batch", 32))
+        self.sv_algorithm.eval_batch = chunk
 
         def batch_metric(subsets):
             # chunks are queued back to back; the host reads the utilities once at the end

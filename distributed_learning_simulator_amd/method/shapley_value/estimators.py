@@ -26,6 +26,7 @@ from __future__ import annotations
 import itertools
 import math
 import random
+import time
 from typing import Callable, Iterable
 
 from ...utils.logging import get_logger
@@ -102,7 +103,7 @@ class MultiRoundShapleyValue(_Base):
 class GTGShapleyValue(_Base):
     def __init__(self, players, last_round_metric=0.0, eps: float = 0.001, round_trunc_threshold: float = 0.001,
                  max_iterations: int = 30, min_iterations: int = 3, converge_threshold: float = 0.05, seed: int = 0,
-                 parallel_iterations: int = 4, **kwargs):
+                 parallel_iterations: int | None = None, **kwargs):
         super().__init__(players, last_round_metric, **kwargs)
         self.eps = eps
         self.round_trunc_threshold = round_trunc_threshold
@@ -113,8 +114,11 @@ class GTGShapleyValue(_Base):
         # iterations whose permutations advance together: one utility batch per position covers
         # them all (≤ parallel_iterations·n subset models). Results equal the one-iteration-at-a-
         # time order exactly (same permutations, convergence checked per iteration afterwards);
-        # iterations past the converged one are evaluated but discarded.
-        self.parallel_iterations = max(1, int(parallel_iterations))
+        # iterations past the converged one are evaluated but discarded. Default: just enough
+        # iterations to fill one utility batch (`eval_batch` subset models), so large player
+        # counts (one iteration = n permutations) waste nothing.
+        self.parallel_iterations = parallel_iterations
+        self.eval_batch = 32
 
     def _marginals(self, perms: list[list], v0: float, vN: float) -> list[list[tuple]]:
         """Position-by-position lock-step over `perms` with within-round truncation: one batched
@@ -151,8 +155,10 @@ class GTGShapleyValue(_Base):
         means = dict(sums)
         it = 0
         done = False
+        par = self.parallel_iterations or max(1, -(-int(self.eval_batch) // max(n, 1)))
+        t0 = time.perf_counter()
         while not done and it < self.max_iterations:
-            g = min(self.parallel_iterations, self.max_iterations - it)
+            g = min(par, self.max_iterations - it)
             perms = []
             for _ in range(g):
                 for first in players:  # guided sampling: each player leads one permutation
@@ -169,12 +175,15 @@ class GTGShapleyValue(_Base):
                         sums[p] += d
                         counts[p] += 1
                 means = {p: sums[p] / max(counts[p], 1) for p in players}
+                change = float("inf")
                 if prev_means is not None:
                     denom = sum(abs(v) for v in means.values()) / n + 1e-12
                     change = sum(abs(means[p] - prev_means[p]) for p in players) / n / denom
-                    if it >= self.min_iterations and change < self.converge_threshold:
-                        done = True
-                        break
+                get_logger().info("GTG round %s: iteration %d, %d evaluations, change %.4f, %.1fs",
+                                  round_number, it, self.evaluations, change, time.perf_counter() - t0)
+                if it >= self.min_iterations and change < self.converge_threshold:
+                    done = True
+                    break
                 prev_means = means
         get_logger().info("GTG round %s: %d iterations, %d subset evaluations", round_number, it, self.evaluations)
         self._finish(means)
