@@ -1,0 +1,137 @@
+"""Reference-equivalent baseline on the same GPU: the reference's execution model in plain PyTorch.
+
+The reference (`simulation_lib/training.py:105-125`, `worker/aggregation_worker.py`,
+`algorithm/fed_avg_algorithm.py:39-52`) trains its clients one at a time inside a process per
+GPU: each client loads the global state dict into a torch.nn model, builds a fresh SGD
+optimizer, runs its local epochs in eager fp32 (`conf/global.yaml` use_amp: false) and hands its
+parameters to the server, which averages them in fp64. The reference itself cannot run here
+(its engine, `cyy_torch_toolbox`, is not installed and there is no network), so this script
+re-creates exactly that loop with stock PyTorch-ROCm (MIOpen convs, rocBLAS/hipBLASLt GEMMs) to
+give the headline config (BASELINE.json config 2: FedAvg, 100 clients, ResNet-18 CIFAR stem,
+5 local epochs, batch 64, SGD lr 0.1 momentum 0.9, cosine) a measured reference-style number.
+
+`--clients-timed C` trains C of the round's clients and scales the time to the whole round
+(clients are identical in size, so the per-client time is constant). Output: one JSON line.
+
+    python bench/torch_reference_baseline.py --clients-timed 8 --warmup-clients 1
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import time
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, cin: int, cout: int, stride: int) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return F.relu(out + self.shortcut(x))
+
+
+class ResNet18(nn.Module):
+    """CIFAR-stem ResNet-18 (11,173,962 parameters, the same count models/zoo.py pins)."""
+
+    def __init__(self, classes: int = 10) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        layers, cin = [], 64
+        for cout, stride in ((64, 1), (128, 2), (256, 2), (512, 2)):
+            layers += [BasicBlock(cin, cout, stride), BasicBlock(cout, cout, 1)]
+            cin = cout
+        self.layers = nn.Sequential(*layers)
+        self.fc = nn.Linear(512, classes)
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)))
+        x = self.layers(x)
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def train_client(model, global_state, images, labels, args):
+    model.load_state_dict(global_state)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=args.epoch)
+    n = images.shape[0]
+    for _ in range(args.epoch):
+        perm = torch.randperm(n, device=images.device)
+        for s in range(0, n, args.batch):
+            idx = perm[s:s + args.batch]
+            loss = F.cross_entropy(model(images[idx]), labels[idx])
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+        sched.step()
+    return {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=100)
+    ap.add_argument("--clients-timed", type=int, default=8)
+    ap.add_argument("--warmup-clients", type=int, default=1)
+    ap.add_argument("--epoch", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--train-size", type=int, default=50000)
+    ap.add_argument("--channels-last", action="store_true")
+    args = ap.parse_args()
+
+    torch.backends.cudnn.benchmark = True
+    dev = torch.device("cuda:0")
+    per_client = args.train_size // args.clients
+    g = torch.Generator(device="cpu").manual_seed(0)
+    images = torch.randn(per_client, 3, 32, 32, generator=g).to(dev)
+    labels = torch.randint(0, 10, (per_client,), generator=g).to(dev)
+    fmt = torch.channels_last if args.channels_last else torch.contiguous_format
+    images = images.contiguous(memory_format=fmt)
+    model = ResNet18().to(dev).to(memory_format=fmt)
+    global_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    n_params = sum(p.numel() for p in model.parameters())
+
+    for _ in range(args.warmup_clients):
+        train_client(model, global_state, images, labels, args)
+    torch.cuda.synchronize()
+    acc = None
+    t0 = time.perf_counter()
+    for c in range(args.clients_timed):
+        state = train_client(model, global_state, images, labels, args)
+        # server side: fp64 weighted accumulation of the upload (fed_avg_algorithm.py:39-52)
+        if acc is None:
+            acc = {k: v.double() * per_client for k, v in state.items() if v.is_floating_point()}
+        else:
+            for k in acc:
+                acc[k] += state[k].double() * per_client
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    s_per_client = dt / args.clients_timed
+    s_round = s_per_client * args.clients
+    print(json.dumps({
+        "metric": "FL rounds/sec (FedAvg, 100 clients, ResNet-18, CIFAR-10-shaped) — reference-style PyTorch eager",
+        "value": 1.0 / s_round, "unit": "rounds/s", "s_per_round": s_round, "s_per_client": s_per_client,
+        "samples_per_s": per_client * args.epoch / s_per_client, "clients_timed": args.clients_timed,
+        "dtype": "fp32", "params": n_params, "channels_last": args.channels_last,
+        "config": {"model": "ResNet18", "clients": args.clients, "local_epochs": args.epoch,
+                   "per_client_batch": args.batch, "per_client_samples": per_client},
+        "torch": torch.__version__, "device": torch.cuda.get_device_name(0),
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,6 +22,7 @@ T_max = local epochs, stepped per epoch.
 from __future__ import annotations
 
 import contextlib
+import gc
 import math
 import os
 from dataclasses import dataclass
@@ -461,10 +462,19 @@ class CohortTrainer:
                     torch.cuda.synchronize(self.device)
                     torch.cuda.empty_cache()
                     g = torch.cuda.CUDAGraph()
-                    # thread-local capture: RCCL's watchdog thread keeps polling its events
-                    # while this rank captures (global mode would fail those calls)
-                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                        run_parts()
+                    # no cyclic GC while capturing: a collected cycle holding an older session's
+                    # graph or tensors would free device memory inside the capture (HIP aborts);
+                    # torch.cuda.graph collects once on entry
+                    gc_was_enabled = gc.isenabled()
+                    gc.disable()
+                    try:
+                        # thread-local capture: RCCL's watchdog thread keeps polling its events
+                        # while this rank captures (global mode would fail those calls)
+                        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                            run_parts()
+                    finally:
+                        if gc_was_enabled:
+                            gc.enable()
                     sg.graph = g
                     g.replay()
                 if s + 1 == schedule.epoch_end[e]:
