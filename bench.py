@@ -37,6 +37,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+# The reference publishes no numbers. Its execution model — clients trained one
+# after another per GPU in eager PyTorch fp32, fp64 server average — re-created with stock
+# PyTorch-ROCm (bench/torch_reference_baseline.py) and measured on one MI355X, in rounds/s for
+# the default (headline) config; profiles/r2_torch_eager_reference_baseline_resnet18.json.
+# With N GPUs the reference would deal the clients over N processes: N x this rate at best.
+REFERENCE_STYLE_ROUNDS_PER_S = {"fedavg_resnet18": 0.05827}
+
+
+def vs_baseline(args, value: float, n_gpus: int, fp32: bool):
+    ref = REFERENCE_STYLE_ROUNDS_PER_S.get(args.workload)
+    default_cfg = (args.algo == "fed_avg" and args.model == "ResNet18" and args.clients == 100 and args.epoch == 5
+                   and args.batch == 64 and not args.emulate_world)
+    if ref is None or not fp32 or not default_cfg:
+        return None
+    return value / (ref * n_gpus)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,7 +197,10 @@ def main() -> None:
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
+            "vs_baseline": vs_baseline(args, args.steps / elapsed, comm.world, sess.compute_dtype != torch.bfloat16),
+            "baseline": ("reference-style PyTorch eager fp32 on MI355X, sequential clients "
+                         "(bench/torch_reference_baseline.py), x n_gpus"
+                         if args.workload in REFERENCE_STYLE_ROUNDS_PER_S else None),
             "dtype": "bf16" if sess.compute_dtype == torch.bfloat16 else "fp32",
             # fp32: activations/weights/gradients fp32; GEMMs as split-bf16 (hi+lo) MFMA with fp32
             # accumulation (≤1e-5 relative vs fp64, tests/test_kernels_f32_gpu.py)

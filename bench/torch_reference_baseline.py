@@ -64,6 +64,39 @@ class ResNet18(nn.Module):
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
+class DenseNet40(nn.Module):
+    """DenseNet-40 (growth 12, stem 24, BN-ReLU-Conv layers, 1x1 transitions + 2x2 average
+    pool; 1,059,298 parameters as models/zoo.py pins), written the usual torch.cat way."""
+
+    def __init__(self, classes: int = 10, growth: int = 12) -> None:
+        super().__init__()
+        c = 2 * growth
+        self.conv1 = nn.Conv2d(3, c, 3, 1, 1, bias=False)
+        self.blocks = nn.ModuleList()
+        self.trans = nn.ModuleList()
+        for b in range(3):
+            layers = nn.ModuleList()
+            for _ in range(12):
+                layers.append(nn.ModuleDict({"bn": nn.BatchNorm2d(c), "conv": nn.Conv2d(c, growth, 3, 1, 1, bias=False)}))
+                c += growth
+            self.blocks.append(layers)
+            if b < 2:
+                self.trans.append(nn.ModuleDict({"bn": nn.BatchNorm2d(c), "conv": nn.Conv2d(c, c, 1, bias=False)}))
+        self.bn = nn.BatchNorm2d(c)
+        self.fc = nn.Linear(c, classes)
+
+    def forward(self, x):
+        x = self.conv1(x)
+        for b, layers in enumerate(self.blocks):
+            for lay in layers:
+                x = torch.cat([x, lay["conv"](F.relu(lay["bn"](x)))], 1)
+            if b < 2:
+                t = self.trans[b]
+                x = F.avg_pool2d(t["conv"](F.relu(t["bn"](x))), 2)
+        x = F.relu(self.bn(x))
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
 def train_client(model, global_state, images, labels, args):
     model.load_state_dict(global_state)
     opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9)
@@ -91,6 +124,7 @@ def main() -> None:
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--model", default="ResNet18", choices=["ResNet18", "densenet40"])
     args = ap.parse_args()
 
     torch.backends.cudnn.benchmark = True
@@ -101,7 +135,7 @@ def main() -> None:
     labels = torch.randint(0, 10, (per_client,), generator=g).to(dev)
     fmt = torch.channels_last if args.channels_last else torch.contiguous_format
     images = images.contiguous(memory_format=fmt)
-    model = ResNet18().to(dev).to(memory_format=fmt)
+    model = (ResNet18() if args.model == "ResNet18" else DenseNet40()).to(dev).to(memory_format=fmt)
     global_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
     n_params = sum(p.numel() for p in model.parameters())
 
@@ -123,11 +157,12 @@ def main() -> None:
     s_per_client = dt / args.clients_timed
     s_round = s_per_client * args.clients
     print(json.dumps({
-        "metric": "FL rounds/sec (FedAvg, 100 clients, ResNet-18, CIFAR-10-shaped) — reference-style PyTorch eager",
+        "metric": f"FL rounds/sec (FedAvg, {args.clients} clients, {'ResNet-18' if args.model == 'ResNet18' else 'DenseNet-40'}, "
+                  "CIFAR-10-shaped) — reference-style PyTorch eager",
         "value": 1.0 / s_round, "unit": "rounds/s", "s_per_round": s_round, "s_per_client": s_per_client,
         "samples_per_s": per_client * args.epoch / s_per_client, "clients_timed": args.clients_timed,
         "dtype": "fp32", "params": n_params, "channels_last": args.channels_last,
-        "config": {"model": "ResNet18", "clients": args.clients, "local_epochs": args.epoch,
+        "config": {"model": args.model, "clients": args.clients, "local_epochs": args.epoch,
                    "per_client_batch": args.batch, "per_client_samples": per_client},
         "torch": torch.__version__, "device": torch.cuda.get_device_name(0),
     }), flush=True)

@@ -639,6 +639,9 @@ bool launch_tn_f32_variant(int v, const ConvTNParams& p, int va, int vb, int gri
 int tn_f32_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
   if (Co <= 32 || R <= 64) return 5;
+  // K <= 8 (8 ranks x 3 streams): the 64x64 tile beats the split-K 128 tiles on every ResNet-18
+  // layer (K = 4: l4a 143 vs 103, l2a 129 vs 94, l4 178 vs 157 TFLOP/s); at K = 13 it loses
+  if (K <= 8) return 5;
   if (Co <= 64) return 1;
   if (Co >= 512 && tiles(256, 128) >= 1024) return 3;
   return 2;
@@ -679,6 +682,13 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     // other's split (VALU) and global-load phases: 128x128 fwd/dgrad 275-299 TFLOP/s on l2-l4
     // (80 KB double-buffered v0: 262-276), 256x64 for N <= 64 (l1 fwd 211 vs 184, dgrad 209 vs 181)
     variant = p.N <= 64 ? 6 : 1;
+    // few clients per launch (8 ranks x 3 sub-cohort streams: K = 4-5) or short reductions:
+    // the 20-KB 64x64 tile. Measured (kernel_bench --f32 --sweep, K = 4 / 13): l4 / l4a fwd
+    // and dgrad at K = 4 (<= 128 big tiles) 142-154 vs 95-105 TFLOP/s; 1x1 shortcut convs
+    // (R <= 128) 63-117 vs 41-107; stride-2 dgrad parity classes onto 64 channels 114-138 vs
+    // 91-125. At K >= 13 the big tiles win the 3x3 layers (l4 269 vs 198).
+    const long big = (long)K * cdiv(p.M, variant == 6 ? 256 : 128) * cdiv(p.N, variant == 6 ? 64 : 128);
+    if (big <= 192 || p.R <= 128 || (p.out_s > 1 && p.N <= 64)) variant = 7;
   }
   // variants without the requested vector widths fall back to the all-widths 64x64 tile
   const bool v88 = va == 8 && vb == 8;

@@ -214,8 +214,43 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
 // grid (cdiv(C, 32), K), 1024 threads = 32 channels × 32 part-groups: the per-workgroup partial
 // sums of a client are reduced in a fixed order (deterministic) by 8 lanes per channel.
 constexpr int COEF_GROUPS = 32;  // partial-sum rows reduced in parallel per channel
-template <typename T>
-__global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const float* __restrict__ ws, int nparts,
+
+// First stage for the conv-epilogue statistics, which arrive as one partial per 32 GEMM rows
+// (2,048 per client on a 32x32x64 layer): a single (32-channel, client) workgroup reading them
+// one after another took ~0.4 ms per BN layer (latency-bound: 2 x 33 workgroups on 256 CUs).
+// This stage folds FOLD consecutive partials of every (client, 2C column) into one fp64 value
+// with grid (cdiv(nparts, FOLD), K) — thousands of workgroups, plain coalesced row reads, a
+// fixed summation order (deterministic) — and bn_coef then reduces the few fp64 folds.
+constexpr int FOLD = 64;
+__global__ void __launch_bounds__(256) part_fold_kernel(const float* __restrict__ part, int nparts, int C2,
+                                                        double* __restrict__ out, int nfold) {
+  __shared__ double red[256];
+  const int k = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  const int b0 = g * FOLD, nb = min(FOLD, nparts - b0);
+  const float* src = part + ((long)k * nparts + b0) * C2;
+  double* dst = out + ((long)k * nfold + g) * C2;
+  // ctn lanes across columns, S = 256 / ctn sub-groups across the partial rows
+  for (int c0 = 0; c0 < C2; c0 += 256) {
+    const int ctn = min(256, C2 - c0);
+    const int S = 256 / ctn;
+    const int cc = tid % ctn, sg = tid / ctn;
+    double a = 0.0;
+    if (sg < S) {
+#pragma unroll 8
+      for (int b = sg; b < nb; b += S) a += (double)src[(long)b * C2 + c0 + cc];
+    }
+    red[tid] = a;
+    __syncthreads();
+    if (sg == 0) {
+      for (int j = 1; j < S; ++j) a += red[j * ctn + cc];
+      dst[c0 + cc] = a;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T, typename PT>
+__global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const PT* __restrict__ ws, int nparts,
                                                       const T* __restrict__ gamma,
                                                       const T* __restrict__ beta, const int* __restrict__ valid_rows,
                                                       const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -231,7 +266,7 @@ __global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const float* 
   const int c = blockIdx.x * 32 + cl;
   double d0 = 0.0, d1 = 0.0;
   if (c < C) {
-    const float* part = ws + (long)k * nparts * 2 * C;
+    const PT* part = ws + (long)k * nparts * 2 * C;
     for (int b = grp; b < nparts; b += COEF_GROUPS) {
       d0 += part[(long)b * 2 * C + c];
       d1 += part[(long)b * 2 * C + C + c];
@@ -517,9 +552,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
 #define CP(p) static_cast<const TT*>(p)
 #define MP(p) static_cast<TT*>(p)
 
-long bn_workspace_floats(int K, long R, int C) {
+// fp32 offset of the fp64 fold area (even: 8-B aligned in the 256-B aligned workspace)
+static long bn_fold_offset(int K, long R, int C) {
   const long parts = (R + rows_per_block(R, K) - 1) / rows_per_block(R, K);
-  return (long)K * 3 * C + (long)K * parts * 2 * C;
+  return ((long)K * 3 * C + (long)K * parts * 2 * C + 1) & ~1L;
+}
+
+long bn_workspace_floats(int K, long R, int C) {
+  // + the fp64 folds of conv-epilogue partials (at most one per 32 rows, FOLD per fold)
+  const long nfold = cdiv((int)cdiv((int)R, 32), FOLD);
+  return bn_fold_offset(K, R, C) + (long)K * nfold * 2 * C * 2;
 }
 
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
@@ -542,10 +584,19 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
                                        nullptr, nullptr, valid_rows, R, C, 0, ws + (long)3 * C * K, (long)2 * C, rpb,
                                        nullptr, ca, ldx, ldx));
     }
-    if (!counters || pre_part)
-      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, nparts, CP(gamma),
-                         CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, K, R, C,
-                         eps, rep, 0);
+    if (pre_part && nparts > FOLD && nparts <= cdiv(R, 32)) {
+      // thousands of epilogue partials per client: fold them wide first (part_fold_kernel)
+      const int nfold = cdiv(nparts, FOLD);
+      double* folds = reinterpret_cast<double*>(ws + bn_fold_offset(K, R, C));
+      hipLaunchKernelGGL(part_fold_kernel, dim3(nfold, K), dim3(256), 0, s, pre_part, nparts, 2 * C, folds, nfold);
+      hipLaunchKernelGGL((bn_coef_kernel<TT, double>), dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s,
+                         (const double*)folds, nfold, CP(gamma), CP(beta), valid_rows, nullptr, nullptr, mean, rstd,
+                         coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+    } else if (!counters || pre_part) {
+      hipLaunchKernelGGL((bn_coef_kernel<TT, float>), dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, nparts,
+                         CP(gamma), CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs,
+                         K, R, C, eps, rep, 0);
+    }
     DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
                                      valid_rows, coef, R, C, relu, rpb, rmask, ldx));
   });
@@ -567,7 +618,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
     DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                      mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
     if (!counters)
-      hipLaunchKernelGGL(bn_coef_kernel<TT>, dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, (int)grid.x, CP(gamma),
+      hipLaunchKernelGGL((bn_coef_kernel<TT, float>), dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, (int)grid.x, CP(gamma),
                          (const TT*)nullptr, valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs,
                          g_cs, K, R, C, 0.f, 1, 1);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
