@@ -40,15 +40,16 @@ sys.path.insert(0, ROOT)
 # The reference publishes no numbers. Its execution model — clients trained one
 # after another per GPU in eager PyTorch fp32, fp64 server average — re-created with stock
 # PyTorch-ROCm (bench/torch_reference_baseline.py) and measured on one MI355X, in rounds/s for
-# the default (headline) config; profiles/r2_torch_eager_reference_baseline_resnet18.json.
+# the default (headline) config and the reference's own DenseNet-40 config;
+# profiles/r2_torch_eager_reference_baseline_{resnet18,densenet40}.json.
 # With N GPUs the reference would deal the clients over N processes: N x this rate at best.
-REFERENCE_STYLE_ROUNDS_PER_S = {"fedavg_resnet18": 0.05827}
+REFERENCE_STYLE_ROUNDS_PER_S = {"fedavg_resnet18": 0.05827, "fedavg_densenet40": 0.03161}
 
 
 def vs_baseline(args, value: float, n_gpus: int, fp32: bool):
     ref = REFERENCE_STYLE_ROUNDS_PER_S.get(args.workload)
-    default_cfg = (args.algo == "fed_avg" and args.model == "ResNet18" and args.clients == 100 and args.epoch == 5
-                   and args.batch == 64 and not args.emulate_world)
+    default_cfg = (args.algo == "fed_avg" and args.clients == 100 and args.epoch == 5 and args.batch == 64
+                   and not args.emulate_world and (args.model == "ResNet18" or args.workload != "fedavg_resnet18"))
     if ref is None or not fp32 or not default_cfg:
         return None
     return value / (ref * n_gpus)

@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
+import threading
 import time
 
 import torch
@@ -125,9 +127,21 @@ def main() -> None:
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--model", default="ResNet18", choices=["ResNet18", "densenet40"])
+    ap.add_argument("--no-benchmark", action="store_true", help="torch.backends.cudnn.benchmark off")
     args = ap.parse_args()
 
-    torch.backends.cudnn.benchmark = True
+    # MIOpen auto-tuning per shape: on for ResNet-18 (11 conv shapes); DenseNet-40 has ~80 distinct
+    # conv shapes (every layer a new input width, plus the ragged last batch) and its exhaustive
+    # search alone ran > 8 minutes, so it runs with PyTorch's default (off)
+    torch.backends.cudnn.benchmark = args.model == "ResNet18" and not args.no_benchmark
+    t_start = time.perf_counter()
+
+    def beat():  # keeps a long MIOpen kernel search visibly alive
+        while True:
+            time.sleep(30)
+            print(f"[baseline] alive {time.perf_counter() - t_start:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     dev = torch.device("cuda:0")
     per_client = args.train_size // args.clients
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -139,13 +153,16 @@ def main() -> None:
     global_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
     n_params = sum(p.numel() for p in model.parameters())
 
-    for _ in range(args.warmup_clients):
+    for c in range(args.warmup_clients):
+        # (first client: MIOpen finds / compiles its kernels — minutes for DenseNet's many shapes)
         train_client(model, global_state, images, labels, args)
+        print(f"[baseline] warmup client {c + 1} done", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     acc = None
     t0 = time.perf_counter()
     for c in range(args.clients_timed):
         state = train_client(model, global_state, images, labels, args)
+        print(f"[baseline] client {c + 1}/{args.clients_timed} {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
         # server side: fp64 weighted accumulation of the upload (fed_avg_algorithm.py:39-52)
         if acc is None:
             acc = {k: v.double() * per_client for k, v in state.items() if v.is_floating_point()}
@@ -162,6 +179,7 @@ def main() -> None:
         "value": 1.0 / s_round, "unit": "rounds/s", "s_per_round": s_round, "s_per_client": s_per_client,
         "samples_per_s": per_client * args.epoch / s_per_client, "clients_timed": args.clients_timed,
         "dtype": "fp32", "params": n_params, "channels_last": args.channels_last,
+        "miopen_benchmark": torch.backends.cudnn.benchmark,
         "config": {"model": args.model, "clients": args.clients, "local_epochs": args.epoch,
                    "per_client_batch": args.batch, "per_client_samples": per_client},
         "torch": torch.__version__, "device": torch.cuda.get_device_name(0),

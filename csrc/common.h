@@ -147,6 +147,22 @@ __device__ __forceinline__ void split2(float x, bf16_t& hi, bf16_t& lo) {
   hi = __builtin_bit_cast(bf16_t, h);
   lo = __builtin_bit_cast(bf16_t, l);
 }
+// Two floats → packed (hi1:hi0) and (lo1:lo0) bf16 pairs in 2.5 VALU ops per element: one
+// v_cvt_pk_bf16_f32 for both hi (RNE), hi back to fp32 by a shift (element 0) and a mask
+// (element 1), one v_pk_add_f32 for both residuals, one v_cvt_pk_bf16_f32 for both lo.
+// (split2 per element compiles to cvt + shift + sub and a second packing cvt: 4 ops.)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  const f32x2_t v = {x0, x1};
+  const bf16x2_t h = __builtin_convertvector(v, bf16x2_t);
+  const uint32_t hb = __builtin_bit_cast(uint32_t, h);
+  const f32x2_t hf = {__uint_as_float(hb << 16), __uint_as_float(hb & 0xffff0000u)};
+  const f32x2_t r = v - hf;
+  hi = hb;
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2_t));
+}
+
 // V consecutive floats → V hi + V lo bf16 (V = 4: 8-B halves, V = 8: 16-B halves)
 template <int V>
 __device__ __forceinline__ void split_vec(const float* f, bf16_t* hi, bf16_t* lo) {

@@ -46,9 +46,15 @@ __device__ __forceinline__ void st_split(bf16_t* hi, bf16_t* lo, const FV<V>& f)
   union {
     TV v;
     bf16_t e[V];
+    uint32_t p[V / 2 > 0 ? V / 2 : 1];
   } h, l;
+  if constexpr (V % 2 == 0) {
 #pragma unroll
-  for (int i = 0; i < V; ++i) split2(f.v[i], h.e[i], l.e[i]);
+    for (int i = 0; i < V / 2; ++i) split_pair(f.v[2 * i], f.v[2 * i + 1], h.p[i], l.p[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) split2(f.v[i], h.e[i], l.e[i]);
+  }
   *reinterpret_cast<TV*>(hi) = h.v;
   *reinterpret_cast<TV*>(lo) = l.v;
 }
@@ -73,8 +79,11 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
   // made the stores straddle bank rows: 2-way, 20-35 % of LDS cycles in SQ_LDS_BANK_CONFLICT)
   constexpr int LDA = BK;
   constexpr int KCA = BK / VA, RPA = T / KCA, PA = BM / RPA;
-  constexpr int KCB = BK / VB, RPB = T / KCB, PB = BN / RPB;  // B row-major [n][k]
-  constexpr int CCB = BN / VB, RPK = T / CCB, PK = BK / RPK;  // B k-major [k][n]
+  // B row-major [n][k] / k-major [k][n]; a narrow B (BN = 32) has fewer rows than loader threads:
+  // one pass, threads past the last row idle (B_PART / K_PART)
+  constexpr int KCB = BK / VB, RPB = T / KCB, PB = RPB > BN ? 1 : BN / RPB;
+  constexpr int CCB = BN / VB, RPK = T / CCB, PK = RPK > BK ? 1 : BK / RPK;
+  constexpr bool B_PART = RPB > BN, K_PART = RPK > BK;
   constexpr int LDBK = BN + 32;                                // row bytes ≡ 64 (mod 256)
   constexpr int NB = BKM ? PK : PB;
   static_assert(PA >= 1 && NB >= 1, "tile too small for thread count");
@@ -99,10 +108,16 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
   const float* __restrict__ x = reinterpret_cast<const float*>(p.x) + (long)client * p.x_cs;
   const float* __restrict__ w = reinterpret_cast<const float*>(p.w) + (long)(client / p.rep) * p.w_cs;
 
-  // --- A loader: PA rows per thread, one fixed K sub-chunk, incremental im2col state
+  // --- operand windows as buffer resources: an out-of-range lane offset reads zeros, so image
+  // padding, M / N / R tails and idle loader threads cost a select instead of a branch
+  const auto xr = make_rsrc(x, (uint32_t)((long)p.B * p.H * p.W * p.ldx * 4));
+  const auto wr = make_rsrc(w, (uint32_t)((BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R) * 4));
+
+  // --- A loader: PA rows per thread, one fixed K sub-chunk, incremental im2col state. A row's
+  // element offset is a_off0[j] (its pixel window origin) + koff, the tap / channel part shared by
+  // every row of the thread and advanced with adds only
   const int kca = tid % KCA;
-  int a_ih0[PA], a_iw0[PA];
-  const float* a_ptr[PA];
+  int a_ih0[PA], a_iw0[PA], a_off0[PA];
   bool a_ok[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
@@ -115,7 +130,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
     const uint32_t ow = rem - oh * p.OW;
     a_ih0[j] = (int)oh * p.stride - p.pad;
     a_iw0[j] = (int)ow * p.stride - p.pad_w;
-    a_ptr[j] = x + (long)b * p.H * p.W * p.ldx;
+    a_off0[j] = (((int)b * p.H + a_ih0[j]) * p.W + a_iw0[j]) * p.ldx;
   }
   int r_cur = kca * VA;
   int kh, kw, c;
@@ -125,9 +140,39 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
     kw = (int)fdiv(rr, p.fd_c);
     c = rr - kw * p.C;
   }
+  int koff = (kh * p.W + kw) * p.ldx + c;
   const int kcb = tid % (BKM ? CCB : KCB);
   const int nk = (p.R + BK - 1) / BK;
   int k_next = 0;
+  // B row offsets (row-major B): -1 marks a row past N or an idle thread of a narrow tile
+  int b_row[BKM ? 1 : PB];
+  // k-major B (dgrad: the forward weight read in place, taps flipped / strided by parity class):
+  // each of the thread's PK k-rows keeps its (channel, tap column) position and element offset,
+  // advanced by BK per step with adds only
+  int bk_co[BKM ? PK : 1], bk_kw[BKM ? PK : 1], bk_off[BKM ? PK : 1];
+  const int nb0 = n0 + kcb * VB;
+  const bool b_live = BKM ? (!(K_PART && tid / CCB >= BK) && nb0 < p.N) : true;
+  if constexpr (!BKM) {
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int n = n0 + tid / KCB + j * RPB;
+      b_row[j] = (n < p.N && !(B_PART && tid / KCB >= BN)) ? n * p.R : -1;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < PK; ++j) {
+      const int k = tid / CCB + j * RPK;
+      const int kh2 = (int)fdiv(k, p.fd_kwc);
+      const int rr = k - kh2 * p.KW * p.C;
+      const int kw2 = (int)fdiv(rr, p.fd_c);
+      const int co = rr - kw2 * p.C;
+      const int khh = p.kh_off - p.kh_step * kh2, kww = p.kw_off - p.kw_step * kw2;
+      bk_co[j] = co;
+      bk_kw[j] = kw2;
+      bk_off[j] = ((co * p.wKH + khh) * p.wKW + kww) * p.N + nb0;
+    }
+  }
+  const int w_co_step = p.wKH * p.wKW * p.N;  // element offset of one input channel
 
   FV<VA> ra[PA];
   FV<VB> rb[NB];
@@ -138,47 +183,44 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
     const bool rok = r_cur < p.R;
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
-      fzero(ra[j]);
-      if (!(rok && a_ok[j])) continue;
-      int qh = a_ih0[j] + kh, qw = a_iw0[j] + kw;
-      if (p.dil > 1) {
-        if ((qh % p.dil) != 0 || (qw % p.dil) != 0) continue;
-        qh /= p.dil;
-        qw /= p.dil;
-      }
-      if (qh < 0 || qh >= p.H || qw < 0 || qw >= p.W) continue;
-      fload(ra[j], a_ptr[j] + ((long)qh * p.W + qw) * p.ldx + c);
+      const int qh = a_ih0[j] + kh, qw = a_iw0[j] + kw;
+      const bool ok = rok && a_ok[j] && (unsigned)qh < (unsigned)p.H && (unsigned)qw < (unsigned)p.W;
+      buf_load<VA>(ra[j].v, xr, ok ? (uint32_t)(a_off0[j] + koff) * 4u : OOB_OFF);
     }
     if constexpr (!BKM) {
       const int rB = k0 + kcb * VB;
 #pragma unroll
-      for (int j = 0; j < PB; ++j) {
-        const int n = n0 + tid / KCB + j * RPB;
-        fzero(rb[j]);
-        if (n < p.N && rB < p.R) fload(rb[j], w + (long)n * p.R + rB);
-      }
+      for (int j = 0; j < PB; ++j)
+        buf_load<VB>(rb[j].v, wr, (b_row[j] >= 0 && rB < p.R) ? (uint32_t)(b_row[j] + rB) * 4u : OOB_OFF);
     } else {
-      const int nb = n0 + kcb * VB;
 #pragma unroll
       for (int j = 0; j < PK; ++j) {
         const int k = k0 + tid / CCB + j * RPK;
-        fzero(rb[j]);
-        if (k >= p.R || nb >= p.N) continue;
-        const int kh2 = (int)fdiv(k, p.fd_kwc);
-        const int rr = k - kh2 * p.KW * p.C;
-        const int kw2 = (int)fdiv(rr, p.fd_c);
-        const int co = rr - kw2 * p.C;
-        const int khh = p.kh_off - p.kh_step * kh2, kww = p.kw_off - p.kw_step * kw2;
-        fload(rb[j], w + (((long)co * p.wKH + khh) * p.wKW + kww) * p.N + nb);
+        buf_load<VB>(rb[j].v, wr, (b_live && k < p.R) ? (uint32_t)bk_off[j] * 4u : OOB_OFF);
+        // advance this k-row by BK: channel, then tap column (kw_step apart in the weight), then
+        // tap row (kh_step apart)
+        bk_co[j] += BK;
+        bk_off[j] += BK * w_co_step;
+        while (bk_co[j] >= p.C) {
+          bk_co[j] -= p.C;
+          bk_off[j] -= p.C * w_co_step + p.kw_step * p.N;
+          if (++bk_kw[j] == p.KW) {
+            bk_kw[j] = 0;
+            bk_off[j] += (p.KW * p.kw_step - p.kh_step * p.wKW) * p.N;
+          }
+        }
       }
     }
     r_cur += BK;
     c += BK;
+    koff += BK;
     while (c >= p.C) {
       c -= p.C;
+      koff += p.ldx - p.C;
       if (++kw == p.KW) {
         kw = 0;
         ++kh;
+        koff += (p.W - p.KW) * p.ldx;
       }
     }
   };
@@ -193,12 +235,14 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
 #pragma unroll
       for (int j = 0; j < PB; ++j) {
         const int r = tid / KCB + j * RPB;
+        if (B_PART && r >= BN) continue;
         const int off = (buf * B_ROWS + r) * B_COLS + swz<BK>(r, kcb * VB);
         st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < PK; ++j) {
+        if (K_PART && tid / CCB >= BK) continue;
         const int off = (buf * B_ROWS + tid / CCB + j * RPK) * B_COLS + kcb * VB;
         st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
       }
@@ -422,11 +466,26 @@ bool launch_nt_f32_variant(int v, const ConvNTParams& p, int K, int va, int vb, 
     // variants 1 / 6 compiled for 3 waves per SIMD (<= 168 registers) instead of 2
     case 8: return launch_nt_f32_cfg<128, 128, 32, 2, 2, 1, 0, 3>(p, K, va, vb, bkm, s);
     case 9: return launch_nt_f32_cfg<256, 64, 32, 4, 1, 1, 0, 3>(p, K, va, vb, bkm, s);
+    // N <= 32 (DenseNet's 12-channel growth convs): a 32-wide B tile wastes 62 % of each MFMA
+    // instead of 81 % in the 64-wide ones, 36 KB
+    case 10: return launch_nt_f32_cfg<256, 32, 32, 4, 1, 1, 1>(p, K, va, vb, bkm, s);
     default: return false;
   }
 }
 
 int vw(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
+
+// DLS_F32_SMALLK: small-cohort tile rules, bit 0 the NT 64x64 rule, bit 1 the wgrad 64x64 rule.
+// Off by default: they win in isolation (kernel_bench at K = 4) but lose inside a round, where
+// the other sub-cohort stream fills the GPU and per-CU efficiency matters more than grid fill
+// (rank 0's share of an 8-rank round, 2 streams: off 743 ms, NT rule 757, wgrad rule 765)
+int small_k_rules() {
+  static const int v = [] {
+    const char* e = getenv("DLS_F32_SMALLK");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 
 // --------------------------------------------------------------------------- TN (wgrad)
 template <int BMc, int BNr, int BKT, int WM, int WN, int VA, int VB, int NBUF>
@@ -435,7 +494,10 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p
   constexpr int TM = BMc / (WM * 32), TN = BNr / (WN * 32);
   constexpr int LDA = BMc + 32;
   constexpr int LDB = BNr + 32;
-  constexpr int CCA = BMc / VA, RPA = T / CCA, PA = BKT / RPA;
+  // a 32-row dY tile (BMc = 32: DenseNet's 12-channel growth convs) with 8-wide vectors has more
+  // loader threads than k-rows: one pass, the extra threads idle (A_PART)
+  constexpr int CCA = BMc / VA, RPA = T / CCA, PA = RPA > BKT ? 1 : BKT / RPA;
+  constexpr bool A_PART = RPA > BKT;
   constexpr int CCB = BNr / VB, RPB = T / CCB, PB = BKT / RPB;
   static_assert(PA >= 1 && PB >= 1, "tile too small");
   constexpr int A_PLANE = NBUF * BKT * LDA, B_PLANE = NBUF * BKT * LDB;
@@ -474,6 +536,10 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p
 
   FV<VA> ra[PA];
   FV<VB> rb[PB];
+  // operand windows as buffer resources (out-of-range offset ⇒ zeros: no branches / zero fills)
+  const auto dyr = make_rsrc(dy, (uint32_t)((long)p.M * p.ldy * 4));
+  const auto xr = make_rsrc(x, (uint32_t)((long)p.B * p.H * p.W * p.ldx * 4));
+  const bool a_live = cok && !(A_PART && tid / CCA >= BKT);
   int k_next = mbeg;
   auto load = [&]() {
     const int k0 = k_next;
@@ -481,26 +547,25 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int m = k0 + tid / CCA + j * RPA;
-      fzero(ra[j]);
-      if (cok && m < mend) fload(ra[j], dy + (long)m * p.ldy + cocol);
+      buf_load<VA>(ra[j].v, dyr, (a_live && m < mend) ? (uint32_t)(m * p.ldy + cocol) * 4u : OOB_OFF);
     }
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int m = k0 + tid / CCB + j * RPB;
-      fzero(rb[j]);
-      if (!(rok && m < mend)) continue;
-      const uint32_t b = fdiv(m, p.fd_ohw);
-      const uint32_t rem = m - b * p.OH * p.OW;
+      const uint32_t mm = m < mend ? m : 0;
+      const uint32_t b = fdiv(mm, p.fd_ohw);
+      const uint32_t rem = mm - b * p.OH * p.OW;
       const uint32_t oh = fdiv(rem, p.fd_ow);
       const uint32_t ow = rem - oh * p.OW;
       const int ih = (int)oh * p.stride - p.pad + kh, iw = (int)ow * p.stride - p.pad + kw;
-      if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
-      fload(rb[j], x + (((long)b * p.H + ih) * p.W + iw) * p.ldx + c);
+      const bool ok = rok && m < mend && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      buf_load<VB>(rb[j].v, xr, ok ? (uint32_t)((((int)b * p.H + ih) * p.W + iw) * p.ldx + c) * 4u : OOB_OFF);
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
+      if (A_PART && tid / CCA >= BKT) continue;
       const int off = (buf * BKT + tid / CCA + j * RPA) * LDA + ca * VA;
       st_split(As + off, As + A_PLANE + off, ra[j]);
     }
@@ -617,7 +682,7 @@ bool launch_tn_f32_cfg(const ConvTNParams& p, int va, int vb, int grid, hipStrea
 struct TnTile {
   int bm, bn;
 };
-constexpr TnTile kTnF32Tiles[] = {{128, 128}, {64, 128}, {128, 128}, {256, 128}, {128, 256}, {64, 64}};
+constexpr TnTile kTnF32Tiles[] = {{128, 128}, {64, 128}, {128, 128}, {256, 128}, {128, 256}, {64, 64}, {32, 128}};
 constexpr int kTnF32Variants = sizeof(kTnF32Tiles) / sizeof(kTnF32Tiles[0]);
 constexpr int TN_BKT_MAX = 32;
 
@@ -629,6 +694,7 @@ bool launch_tn_f32_variant(int v, const ConvTNParams& p, int va, int vb, int gri
     case 3: return launch_tn_f32_cfg<256, 128, 32, 4, 2, 1, false>(p, va, vb, grid, s);  // 60 KB
     case 4: return launch_tn_f32_cfg<128, 256, 32, 2, 4, 1, false>(p, va, vb, grid, s);  // 60 KB
     case 5: return launch_tn_f32_cfg<64, 64, 32, 2, 2, 2, true>(p, va, vb, grid, s);    // 40 KB
+    case 6: return launch_tn_f32_cfg<32, 128, 32, 1, 4, 2, true>(p, va, vb, grid, s);   // 56 KB, Co <= 32
     default: return false;
   }
 }
@@ -638,10 +704,11 @@ bool launch_tn_f32_variant(int v, const ConvTNParams& p, int va, int vb, int gri
 // 256x128 tile only at Co >= 512 with enough tiles (l4 286 vs 273)
 int tn_f32_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
+  if (Co <= 32 && R > 64) return 6;
   if (Co <= 32 || R <= 64) return 5;
   // K <= 8 (8 ranks x 3 streams): the 64x64 tile beats the split-K 128 tiles on every ResNet-18
   // layer (K = 4: l4a 143 vs 103, l2a 129 vs 94, l4 178 vs 157 TFLOP/s); at K = 13 it loses
-  if (K <= 8) return 5;
+  if (K <= 8 && (small_k_rules() & 2)) return 5;
   if (Co <= 64) return 1;
   if (Co >= 512 && tiles(256, 128) >= 1024) return 3;
   return 2;
@@ -649,8 +716,9 @@ int tn_f32_default_variant(int K, int Co, int R) {
 
 int resolve_tn_f32_variant(int variant, int K, int Co, int R, int va, int vb) {
   if (variant < 0 || variant >= kTnF32Variants) variant = tn_f32_default_variant(K, Co, R);
-  if ((va != 8 || vb != 8) && !(variant == 0 || variant == 1 || variant == 5)) variant = Co <= 64 ? 1 : 0;
-  // (the all-widths tiles are the double-buffered 0 / 1 / 5)
+  if ((va != 8 || vb != 8) && !(variant == 0 || variant == 1 || variant == 5 || variant == 6))
+    variant = Co <= 64 ? 1 : 0;
+  // (the all-widths tiles are the double-buffered 0 / 1 / 5 / 6)
   return variant;
 }
 
@@ -670,10 +738,21 @@ void tn_f32_split(int K, int Co, int R, int M, int variant, int& splitk, int& mp
 
 }  // namespace
 
-int conv_nt_f32_num_variants() { return 10; }
+int conv_nt_f32_num_variants() { return 11; }
 
 void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
   const bool bkm = p.b_kmajor != 0;
+  // the loaders address each client's operand window with 32-bit buffer offsets
+  const long xb = (long)p.B * p.H * p.W * p.ldx * 4;
+  const long wb = (bkm ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R) * 4;
+  if (p.dil != 1) {  // (the dgrad launches use stride-1 parity classes, never input dilation)
+    fprintf(stderr, "conv_nt_f32: input dilation is not supported\n");
+    abort();
+  }
+  if (xb >= (long)OOB_OFF || wb >= (long)OOB_OFF) {
+    fprintf(stderr, "conv_nt_f32: per-client operand window over 2 GiB (x %ld B, w %ld B)\n", xb, wb);
+    abort();
+  }
   const int va = vw(std::gcd(p.C, p.ldx));
   int vb = bkm ? vw(p.N) : vw(p.R);
   if (variant < 0) {
@@ -688,14 +767,16 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     // (R <= 128) 63-117 vs 41-107; stride-2 dgrad parity classes onto 64 channels 114-138 vs
     // 91-125. At K >= 13 the big tiles win the 3x3 layers (l4 269 vs 198).
     const long big = (long)K * cdiv(p.M, variant == 6 ? 256 : 128) * cdiv(p.N, variant == 6 ? 64 : 128);
-    if (big <= 192 || p.R <= 128 || (p.out_s > 1 && p.N <= 64)) variant = 7;
+    if ((small_k_rules() & 1) && (big <= 192 || p.R <= 128 || (p.out_s > 1 && p.N <= 64))) variant = 7;
+    if (p.N <= 32) variant = 10;
   }
   // variants without the requested vector widths fall back to the all-widths 64x64 tile
   const bool v88 = va == 8 && vb == 8;
   const bool v84 = (va == 8 || va == 4) && (vb == 8 || vb == 4);
   if (!v88) {
     if (!v84 && variant != 3) variant = 3;
-    if (v84 && !(variant == 0 || variant == 3 || variant == 4 || variant == 7)) variant = p.N <= 64 ? 4 : 0;
+    if (v84 && !(variant == 0 || variant == 3 || variant == 4 || variant == 7 || variant == 10))
+      variant = p.N <= 64 ? 4 : 0;
   }
   if (!launch_nt_f32_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt_f32: bad variant %d\n", variant);
 }
@@ -703,6 +784,12 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
 int conv_tn_f32_num_variants() { return kTnF32Variants; }
 
 void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s) {
+  // the loaders address each client's operand window with 32-bit buffer offsets
+  const long dyb = (long)p.M * (p.ldy ? p.ldy : p.Co) * 4, xb = (long)p.B * p.H * p.W * (p.ldx ? p.ldx : p.C) * 4;
+  if (dyb >= (long)OOB_OFF || xb >= (long)OOB_OFF) {
+    fprintf(stderr, "conv_tn_f32: per-client operand window over 2 GiB (dy %ld B, x %ld B)\n", dyb, xb);
+    abort();
+  }
   const int va = vw(std::gcd(p.Co, p.ldy));
   const int vb = vw(std::gcd(p.C, p.ldx));
   variant = resolve_tn_f32_variant(variant, K, p.Co, p.R, va, vb);

@@ -127,7 +127,7 @@ class CohortTrainer:
         self.layout = model.layout
         self.buffers = CohortBuffers(self.layout, capacity, self.device, compute_dtype, hyper.optimizer_name)
         self.debug = False  # `debug` config: per-step NaN/Inf scan (synchronises every step)
-        self.num_streams = int(os.environ.get("DLS_STREAMS", "3"))  # concurrent sub-cohorts on GPU
+        self.num_streams = int(os.environ.get("DLS_STREAMS", "2"))  # concurrent sub-cohorts on GPU
         self._stream_pool: list = []
         # HIP-graph replay of whole training steps (DLS_GRAPHS=0 disables): a ResNet-18 step is
         # ≈400 launches per sub-cohort, which at the 8-GPU per-rank load (13 clients) costs more
@@ -286,10 +286,11 @@ class CohortTrainer:
 
     # ------------------------------------------------------------------ streams
     def _sub_cohorts(self, K: int) -> list[tuple[int, int]]:
-        """Row ranges trained concurrently on separate HIP streams. Sub-cohorts (3 by default)
-        overlap each other's kernel tails and small launches (BN coefficients, reductions);
-        measured on the 100-client ResNet-18 round: 1 stream 2.90 s, 2 streams 2.77 s, 3 streams
-        2.73 s (2 processes sharing one GPU gave the same gain); neutral at 13 clients."""
+        """Row ranges trained concurrently on separate HIP streams. Sub-cohorts (2 by default)
+        overlap each other's kernel tails and small launches (BN coefficients, reductions).
+        Measured at fp32 (scripts/ab_streams.sh): rank 0's 13-client share of an 8-rank round
+        1 stream 821 ms, 2 streams 743 ms, 3 streams 790 ms; the 100-client round 2 streams
+        5.23 s, 3 streams 5.28 s."""
         n = self.num_streams if self.device.type == "cuda" else 1
         n = max(1, min(n, K // 4))
         if n == 1:

@@ -70,7 +70,7 @@ def test_conv_f32(hip, case):
 
 
 @pytest.mark.parametrize("case", [(2, 2, 9, 9, 64, 128, 3, 2, 1), (2, 3, 8, 8, 128, 64, 3, 1, 1),
-                                  (2, 2, 6, 6, 24, 40, 3, 1, 1)])
+                                  (2, 2, 6, 6, 24, 40, 3, 1, 1), (3, 2, 8, 8, 36, 12, 3, 1, 1)])
 def test_conv_f32_every_variant(hip, case):
     """Every fp32 NT and TN tile configuration (the driver's fp32 `--variant` sweep ids)."""
     K, B, H, W, Ci, Co, k, s, p = case
@@ -345,10 +345,11 @@ def test_embedding_scale_pe_and_seq_mean(hip, dtype, tol):
 
 
 @pytest.mark.parametrize("case", [(3, 4, 8, 8, 16, 64, 3, 1, 1), (2, 5, 9, 9, 64, 128, 3, 2, 1),
-                                  (2, 3, 8, 8, 32, 256, 1, 1, 0)])
+                                  (2, 3, 8, 8, 32, 256, 1, 1, 0), (3, 41, 8, 8, 16, 24, 3, 1, 1)])
 def test_conv_epilogue_bn_stats(hip, case):
     """fp32 conv epilogue writes the BN partial sums (per 32 GEMM rows, valid samples only):
-    their totals match fp64 sums over y, and bn_fwd(pre_stats=) equals bn_fwd's own pass."""
+    their totals match fp64 sums over y, and bn_fwd(pre_stats=) equals bn_fwd's own pass (the
+    last case has 82 partials per client: the wide fp64 fold stage runs, with a ragged last fold)."""
     K, B, H, W, Ci, Co, k, s, p = case
     x = _f(K, B, H, W, Ci)
     w = _f(K, Co, k, k, Ci, scale=0.2)
