@@ -99,6 +99,22 @@ def main():
             for key in ab:
                 row[f"{key}_fwd_tflops"] = round(max(a for a, _ in ab[key]), 1)
                 row[f"{key}_dgrad_tflops"] = round(max(b for _, b in ab[key]), 1)
+        if args.f32 and k * k * Ci % 8 == 0 and Ci % 8 == 0:
+            # interleaved A/B in one process: weights pre-split into (hi, lo) bf16 planes (what a
+            # graphed training step reads, CohortBuffers.split) vs split per workgroup
+            n = Co * k * k * Ci
+            planes = torch.empty((K, 2, n), dtype=torch.bfloat16, device=dev)
+            hip.split_rows(w.reshape(K, n).contiguous(), planes)
+            ws = planes[:, 0].unflatten(1, (Co, k, k, Ci))
+            ab = {"split": [], "plain": []}
+            for _ in range(3):
+                for key, wsp in (("split", ws), ("plain", None)):
+                    tf_m = timeit(lambda: hip.conv_fwd(x, w, s, pad, w_split=wsp), args.iters)
+                    td_m = timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad, w_split=wsp), args.iters)
+                    ab[key].append((flops / tf_m / 1e12, flops / td_m / 1e12))
+            for key in ab:
+                row[f"{key}_fwd_tflops"] = round(max(a for a, _ in ab[key]), 1)
+                row[f"{key}_dgrad_tflops"] = round(max(b for _, b in ab[key]), 1)
         if args.sweep:
             # every NT tile configuration on this shape (fwd / dgrad TFLOP/s per variant id)
             sw = {}

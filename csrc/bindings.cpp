@@ -20,8 +20,12 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int B, int H, int W,
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
                       int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s, int ldx, int ldy,
-                      ptr stats, ptr stats_valid, ptr drop_seeds, float drop_p, float out_scale) {
+                      ptr stats, ptr stats_valid, ptr drop_seeds, float drop_p, float out_scale, ptr wsplit,
+                      long ws_cs, long ws_plane) {
     ConvNTParams p{};
+    p.wsplit = P<const bf16_t>(wsplit);
+    p.ws_cs = ws_cs;
+    p.ws_plane = ws_plane;
     p.drop_seeds = P<const uint32_t>(drop_seeds);
     p.drop_p = drop_p;
     p.out_scale = out_scale;
@@ -44,9 +48,9 @@ PYBIND11_MODULE(_dls_hip, m) {
   });
   m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, ptr acc, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
                          int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, ptr s, int ld_dy,
-                         long dy_cs) {
+                         long dy_cs, ptr wsplit, long ws_cs, long ws_plane) {
     conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), P<const bf16_t>(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
-               stride, pad, variant, f32, S(s), ld_dy, dy_cs);
+               stride, pad, variant, f32, S(s), ld_dy, dy_cs, P<const bf16_t>(wsplit), ws_cs, ws_plane);
   });
   m.def("conv_gl_wanted", &conv_gl_wanted);
   m.def("conv_gl_fwd", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int K, int rep,
@@ -139,10 +143,14 @@ PYBIND11_MODULE(_dls_hip, m) {
     relu_bwd(P<const void>(dy), P<const void>(y), P<void>(dx), n, f32, S(s));
   });
 
-  m.def("sgd_step", [](ptr theta, ptr grad, ptr mom, ptr shadow, ptr lr, ptr active, ptr first, int K, long Pn, long ld,
-                       float wd, float momentum, float dampening, int nesterov, ptr s) {
-    sgd_step(P<float>(theta), P<const float>(grad), P<float>(mom), P<bf16_t>(shadow), P<const float>(lr),
-             P<const uint8_t>(active), P<const uint8_t>(first), K, Pn, ld, wd, momentum, dampening, nesterov, S(s));
+  m.def("sgd_step", [](ptr theta, ptr grad, ptr mom, ptr shadow, ptr split, ptr lr, ptr active, ptr first, int K,
+                       long Pn, long ld, float wd, float momentum, float dampening, int nesterov, ptr s) {
+    sgd_step(P<float>(theta), P<const float>(grad), P<float>(mom), P<bf16_t>(shadow), P<bf16_t>(split),
+             P<const float>(lr), P<const uint8_t>(active), P<const uint8_t>(first), K, Pn, ld, wd, momentum, dampening,
+             nesterov, S(s));
+  });
+  m.def("split_rows", [](ptr theta, ptr split, int K, long Pn, long ld, ptr s) {
+    split_rows(P<const float>(theta), P<bf16_t>(split), K, Pn, ld, S(s));
   });
   m.def("adam_step", [](ptr theta, ptr grad, ptr mm, ptr v, ptr shadow, ptr lr, ptr active, ptr step, int K, long Pn,
                         long ld, float b1, float b2, float eps, float wd, ptr s) {

@@ -68,8 +68,11 @@ __device__ __forceinline__ int swz(int r, int e) {
 }
 
 // ------------------------------------------------------------------------- NT (fwd / dgrad)
-template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int NBUF, int MINW = 1>
+template <int BM, int BN, int BK, int WM, int WN, int VA, int VB, bool BKM, int NBUF, int MINW = 1, bool BSPL = false>
 __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTParams p) {
+  // BSPL: B comes pre-split (p.wsplit hi / lo bf16 planes, written by the SGD step): its loads
+  // are 16-B bf16 vectors stored to LDS as they are, no split VALU for B in the loop
+  static_assert(!BSPL || VB == 8, "pre-split B needs 8-element vectors");
   constexpr int T = WM * WN * 64;
   constexpr int TM = BM / (WM * 32);
   constexpr int TN = BN / (WN * 32);
@@ -111,7 +114,11 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
   // --- operand windows as buffer resources: an out-of-range lane offset reads zeros, so image
   // padding, M / N / R tails and idle loader threads cost a select instead of a branch
   const auto xr = make_rsrc(x, (uint32_t)((long)p.B * p.H * p.W * p.ldx * 4));
-  const auto wr = make_rsrc(w, (uint32_t)((BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R) * 4));
+  const long w_ext = BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R;  // elements
+  const auto wr = make_rsrc(w, (uint32_t)(w_ext * 4));
+  const auto wsr = make_rsrc(BSPL ? (const void*)(p.wsplit + (long)(client / p.rep) * p.ws_cs) : (const void*)w,
+                             BSPL ? (uint32_t)((p.ws_plane + w_ext) * 2) : 0u);
+  const uint32_t ws_lo = (uint32_t)(p.ws_plane * 2);  // byte distance hi → lo plane
 
   // --- A loader: PA rows per thread, one fixed K sub-chunk, incremental im2col state. A row's
   // element offset is a_off0[j] (its pixel window origin) + koff, the tap / channel part shared by
@@ -175,7 +182,16 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
   const int w_co_step = p.wKH * p.wKW * p.N;  // element offset of one input channel
 
   FV<VA> ra[PA];
-  FV<VB> rb[NB];
+  FV<BSPL ? 1 : VB> rb[NB];
+  u32x4_t rbh[BSPL ? NB : 1], rbl[BSPL ? NB : 1];
+  auto load_b = [&](int j, uint32_t e_off, bool ok) {  // B element offset e_off (w's layout)
+    if constexpr (BSPL) {
+      rbh[j] = __builtin_amdgcn_raw_buffer_load_b128(wsr, ok ? e_off * 2u : OOB_OFF, 0, 0);
+      rbl[j] = __builtin_amdgcn_raw_buffer_load_b128(wsr, ok ? e_off * 2u + ws_lo : OOB_OFF, 0, 0);
+    } else {
+      buf_load<VB>(rb[j].v, wr, ok ? e_off * 4u : OOB_OFF);
+    }
+  };
 
   auto load = [&]() {
     const int k0 = k_next;
@@ -190,13 +206,12 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
     if constexpr (!BKM) {
       const int rB = k0 + kcb * VB;
 #pragma unroll
-      for (int j = 0; j < PB; ++j)
-        buf_load<VB>(rb[j].v, wr, (b_row[j] >= 0 && rB < p.R) ? (uint32_t)(b_row[j] + rB) * 4u : OOB_OFF);
+      for (int j = 0; j < PB; ++j) load_b(j, (uint32_t)(b_row[j] + rB), b_row[j] >= 0 && rB < p.R);
     } else {
 #pragma unroll
       for (int j = 0; j < PK; ++j) {
         const int k = k0 + tid / CCB + j * RPK;
-        buf_load<VB>(rb[j].v, wr, (b_live && k < p.R) ? (uint32_t)bk_off[j] * 4u : OOB_OFF);
+        load_b(j, (uint32_t)bk_off[j], b_live && k < p.R);
         // advance this k-row by BK: channel, then tap column (kw_step apart in the weight), then
         // tap row (kh_step apart)
         bk_co[j] += BK;
@@ -237,14 +252,24 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
         const int r = tid / KCB + j * RPB;
         if (B_PART && r >= BN) continue;
         const int off = (buf * B_ROWS + r) * B_COLS + swz<BK>(r, kcb * VB);
-        st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+        if constexpr (BSPL) {
+          *reinterpret_cast<u32x4_t*>(Bs + off) = rbh[j];
+          *reinterpret_cast<u32x4_t*>(Bs + B_PLANE + off) = rbl[j];
+        } else {
+          st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+        }
       }
     } else {
 #pragma unroll
       for (int j = 0; j < PK; ++j) {
         if (K_PART && tid / CCB >= BK) continue;
         const int off = (buf * B_ROWS + tid / CCB + j * RPK) * B_COLS + kcb * VB;
-        st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+        if constexpr (BSPL) {
+          *reinterpret_cast<u32x4_t*>(Bs + off) = rbh[j];
+          *reinterpret_cast<u32x4_t*>(Bs + B_PLANE + off) = rbl[j];
+        } else {
+          st_split(Bs + off, Bs + B_PLANE + off, rb[j]);
+        }
       }
     }
   };
@@ -435,6 +460,15 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_f32_kernel(ConvNTPa
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, int VSET, int MINW = 1>
 bool launch_nt_f32_cfg(const ConvNTParams& p, int K, int va, int vb, bool bkm, hipStream_t s) {
   const int grid = K * cdiv(p.M, BM) * cdiv(p.N, BN);
+  if (p.wsplit && va == 8 && vb == 8) {  // pre-split weight planes (8-wide vectors only)
+    if (bkm)
+      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, 8, 8, true, NBUF, MINW, true>), dim3(grid),
+                         dim3(WM * WN * 64), 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_nt_f32_kernel<BM, BN, BK, WM, WN, 8, 8, false, NBUF, MINW, true>), dim3(grid),
+                         dim3(WM * WN * 64), 0, s, p);
+    return true;
+  }
 #define NTF_CASE(A, B)                                                                                       \
   if (va == A && vb == B) {                                                                                  \
     if (bkm)                                                                                                 \
@@ -541,25 +575,60 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_f32_kernel(ConvTNParams p
   const auto xr = make_rsrc(x, (uint32_t)((long)p.B * p.H * p.W * p.ldx * 4));
   const bool a_live = cok && !(A_PART && tid / CCA >= BKT);
   int k_next = mbeg;
+  // im2col rows of X̃ without divisions in the loop: each of the thread's PB GEMM rows m keeps
+  // its input coordinates (ih, iw) and element offset, advanced by BKT rows per step through the
+  // fixed decomposition BKT = q_b·OH·OW + q_oh·OW + r_ow (one carry per level: no muls)
+  const int q_b = BKT / (p.OH * p.OW), rem_b = BKT - q_b * p.OH * p.OW;
+  const int q_oh = rem_b / p.OW, r_ow = rem_b - q_oh * p.OW;
+  const int s_ldx = p.stride * p.ldx, s_row = p.stride * p.W * p.ldx, img = p.H * p.W * p.ldx;
+  const int d_iw = r_ow * p.stride, d_off = r_ow * s_ldx + q_oh * s_row + q_b * img;
+  const int w_wrap = p.OW * p.stride, off_c1 = s_row - p.OW * s_ldx;    // ow wraps: next output row
+  const int d_ih0 = q_oh * p.stride, d_ih1 = (q_oh + 1) * p.stride;
+  const int h_wrap = p.OH * p.stride, off_c2 = img - p.OH * s_row;       // oh wraps: next image
+  int bx_ow[PB], bx_oh[PB], bx_ih[PB], bx_iw[PB], bx_off[PB];
+#pragma unroll
+  for (int j = 0; j < PB; ++j) {
+    const uint32_t m = mbeg + tid / CCB + j * RPB;
+    const uint32_t b = fdiv(m, p.fd_ohw);
+    const uint32_t rem = m - b * p.OH * p.OW;
+    const uint32_t oh = fdiv(rem, p.fd_ow);
+    const uint32_t ow = rem - oh * p.OW;
+    bx_ow[j] = ow;
+    bx_oh[j] = oh;
+    bx_ih[j] = (int)oh * p.stride - p.pad + kh;
+    bx_iw[j] = (int)ow * p.stride - p.pad + kw;
+    bx_off[j] = (((int)b * p.H + bx_ih[j]) * p.W + bx_iw[j]) * p.ldx + c;
+  }
+  int a_off = (mbeg + tid / CCA) * p.ldy + cocol;  // + j·RPA·ldy for row j
+  const int a_jstep = RPA * p.ldy, a_kstep = BKT * p.ldy;
   auto load = [&]() {
     const int k0 = k_next;
     k_next += BKT;
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int m = k0 + tid / CCA + j * RPA;
-      buf_load<VA>(ra[j].v, dyr, (a_live && m < mend) ? (uint32_t)(m * p.ldy + cocol) * 4u : OOB_OFF);
+      buf_load<VA>(ra[j].v, dyr, (a_live && m < mend) ? (uint32_t)(a_off + j * a_jstep) * 4u : OOB_OFF);
     }
+    a_off += a_kstep;
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int m = k0 + tid / CCB + j * RPB;
-      const uint32_t mm = m < mend ? m : 0;
-      const uint32_t b = fdiv(mm, p.fd_ohw);
-      const uint32_t rem = mm - b * p.OH * p.OW;
-      const uint32_t oh = fdiv(rem, p.fd_ow);
-      const uint32_t ow = rem - oh * p.OW;
-      const int ih = (int)oh * p.stride - p.pad + kh, iw = (int)ow * p.stride - p.pad + kw;
-      const bool ok = rok && m < mend && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      buf_load<VB>(rb[j].v, xr, ok ? (uint32_t)((((int)b * p.H + ih) * p.W + iw) * p.ldx + c) * 4u : OOB_OFF);
+      const bool ok = rok && m < mend && (unsigned)bx_ih[j] < (unsigned)p.H && (unsigned)bx_iw[j] < (unsigned)p.W;
+      buf_load<VB>(rb[j].v, xr, ok ? (uint32_t)bx_off[j] * 4u : OOB_OFF);
+      // advance row m by BKT (wave-uniform step constants; the carries are selects)
+      bx_ow[j] += r_ow;
+      bx_iw[j] += d_iw;
+      bx_off[j] += d_off;
+      const bool c1 = bx_ow[j] >= p.OW;
+      bx_ow[j] -= c1 ? p.OW : 0;
+      bx_oh[j] += c1 ? q_oh + 1 : q_oh;
+      bx_iw[j] -= c1 ? w_wrap : 0;
+      bx_ih[j] += c1 ? d_ih1 : d_ih0;
+      bx_off[j] += c1 ? off_c1 : 0;
+      const bool c2 = bx_oh[j] >= p.OH;
+      bx_oh[j] -= c2 ? p.OH : 0;
+      bx_ih[j] -= c2 ? h_wrap : 0;
+      bx_off[j] += c2 ? off_c2 : 0;
     }
   };
   auto store = [&](int buf) {
@@ -709,9 +778,15 @@ int tn_f32_default_variant(int K, int Co, int R) {
   // K <= 8 (8 ranks x 3 streams): the 64x64 tile beats the split-K 128 tiles on every ResNet-18
   // layer (K = 4: l4a 143 vs 103, l2a 129 vs 94, l4 178 vs 157 TFLOP/s); at K = 13 it loses
   if (K <= 8 && (small_k_rules() & 2)) return 5;
+  // re-measured after the buffer-load loaders (kernel_bench --f32 --sweep, K = 33 / 100):
+  // 1x1 shortcut convs (R <= 256) the 64x64 tile (l4sc 165 vs 97 TFLOP/s at K = 33); Co <= 64 the
+  // 64x128 double-buffered tile; 3x3 layers with Co >= 256 and R >= 2048 the 256x128 tile (l3 / l4
+  // 277-304 vs 256-291); the rest the double-buffered 128x128 (l2 / l3a 258-270 vs 238-268)
+  (void)tiles;
+  if (R <= 256 && Co > 64) return 5;
   if (Co <= 64) return 1;
-  if (Co >= 512 && tiles(256, 128) >= 1024) return 3;
-  return 2;
+  if (Co >= 256 && R >= 2048) return 3;
+  return 0;
 }
 
 int resolve_tn_f32_variant(int variant, int K, int Co, int R, int va, int vb) {
@@ -749,7 +824,7 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     fprintf(stderr, "conv_nt_f32: input dilation is not supported\n");
     abort();
   }
-  if (xb >= (long)OOB_OFF || wb >= (long)OOB_OFF) {
+  if (xb >= (long)OOB_OFF || wb >= (long)OOB_OFF || (p.wsplit && (p.ws_plane + wb / 4) * 2 >= (long)OOB_OFF)) {
     fprintf(stderr, "conv_nt_f32: per-client operand window over 2 GiB (x %ld B, w %ld B)\n", xb, wb);
     abort();
   }
@@ -760,13 +835,16 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     // tiles win everywhere — 40-60 KB of LDS keeps 3 workgroups per CU, whose waves hide each
     // other's split (VALU) and global-load phases: 128x128 fwd/dgrad 275-299 TFLOP/s on l2-l4
     // (80 KB double-buffered v0: 262-276), 256x64 for N <= 64 (l1 fwd 211 vs 184, dgrad 209 vs 181)
-    variant = p.N <= 64 ? 6 : 1;
+    // (re-measured after the buffer-load loaders: for N <= 64 the 256x64 tile compiled for 3
+    // waves per SIMD, v9: l1 dgrad 233-236 vs 205-222, strided-dgrad classes onto 64 channels
+    // 157-179 vs 132-151, the 8-channel stem 118 vs 98-108; fwd equal)
+    variant = p.N <= 64 ? 9 : 1;
     // few clients per launch (8 ranks x 3 sub-cohort streams: K = 4-5) or short reductions:
     // the 20-KB 64x64 tile. Measured (kernel_bench --f32 --sweep, K = 4 / 13): l4 / l4a fwd
     // and dgrad at K = 4 (<= 128 big tiles) 142-154 vs 95-105 TFLOP/s; 1x1 shortcut convs
     // (R <= 128) 63-117 vs 41-107; stride-2 dgrad parity classes onto 64 channels 114-138 vs
     // 91-125. At K >= 13 the big tiles win the 3x3 layers (l4 269 vs 198).
-    const long big = (long)K * cdiv(p.M, variant == 6 ? 256 : 128) * cdiv(p.N, variant == 6 ? 64 : 128);
+    const long big = (long)K * cdiv(p.M, variant == 9 ? 256 : 128) * cdiv(p.N, variant == 9 ? 64 : 128);
     if ((small_k_rules() & 1) && (big <= 192 || p.R <= 128 || (p.out_s > 1 && p.N <= 64))) variant = 7;
     if (p.N <= 32) variant = 10;
   }

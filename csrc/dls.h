@@ -64,6 +64,11 @@ struct ConvNTParams {
   const uint32_t* drop_seeds;
   float drop_p;
   float out_scale;
+  // optional pre-split weight planes (fp32 kernels): the B operand's bf16 hi plane in w's layout,
+  // the lo plane ws_plane elements after it, client stride ws_cs (elements). Kept current by the
+  // SGD kernel (sgd_step's `split`), so the GEMM skips splitting B in every workgroup.
+  const bf16_t* wsplit;
+  long ws_cs, ws_plane;
 };
 
 struct ConvTNParams {
@@ -120,7 +125,7 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
-                int ld_dy = 0, long dy_cs = 0);
+                int ld_dy = 0, long dy_cs = 0, const bf16_t* wsplit = nullptr, long ws_cs = 0, long ws_plane = 0);
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
@@ -203,13 +208,16 @@ void neighbor_sample(const int* rowptr, const int* col, const int* owner, const 
                      const int64_t* clients, int n, int fanout, unsigned long long seed_h, int* out_nbr, int* out_cnt,
                      hipStream_t s);
 
-void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
+void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, bf16_t* split, const float* lr,
+              const uint8_t* active,
               const uint8_t* first, int K, long P, long ld, float wd, float momentum, float dampening, int nesterov,
               hipStream_t s);
 void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shadow, const float* lr,
                const uint8_t* active, const float* step, int K, long P, long ld, float b1, float b2, float eps,
                float wd, hipStream_t s);
 void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s);
+// split[k] = (bf16 hi plane, bf16 lo plane) of theta[k] rows ([K][2][ld] bf16)
+void split_rows(const float* theta, bf16_t* split, int K, long P, long ld, hipStream_t s);
 void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s);
 // out += Σ_k w_k x[k] / num += Σ w m x, den += Σ w m: fp64 accumulators (in place)
 void weighted_sum(const float* x, const double* w, double* out, int K, long P, long ld, hipStream_t s);

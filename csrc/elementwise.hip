@@ -211,8 +211,30 @@ __global__ void relu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ 
 
 // ------------------------------------------------------------- optimiser steps
 // grid: (chunks of P/4, K). float4 over the row; per-client lr / active / first-step flags.
+// split[k] row = [hi plane (ld)][lo plane (ld)] bf16 of theta[k] (the fp32 GEMMs' pre-split
+// weight operand, ConvNTParams::wsplit): 4 consecutive values → 8 B of hi + 8 B of lo
+__device__ __forceinline__ void store_split4(bf16_t* __restrict__ split, long k, long ld, long i, const float* v) {
+  uint32_t h0, l0, h1, l1;
+  split_pair(v[0], v[1], h0, l0);
+  split_pair(v[2], v[3], h1, l1);
+  bf16_t* sp = split + k * 2 * ld;
+  reinterpret_cast<uint2*>(sp)[i] = make_uint2(h0, h1);
+  reinterpret_cast<uint2*>(sp + ld)[i] = make_uint2(l0, l1);
+}
+
+__global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict__ theta, bf16_t* __restrict__ split,
+                                                         long P4, long ld) {
+  const int k = blockIdx.y;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
+    const float4 t = reinterpret_cast<const float4*>(theta + (long)k * ld)[i];
+    const float v[4] = {t.x, t.y, t.z, t.w};
+    store_split4(split, k, ld, i, v);
+  }
+}
+
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ theta, const float* __restrict__ grad,
                                                   float* __restrict__ mom, bf16_t* __restrict__ shadow,
+                                                  bf16_t* __restrict__ split,
                                                   const float* __restrict__ lr, const uint8_t* __restrict__ active,
                                                   const uint8_t* __restrict__ first, long P4, long ld, float wd,
                                                   float momentum, float dampening, int nesterov) {
@@ -250,6 +272,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ theta, con
       u.y = (uint32_t)f2bf(tv[2]) | ((uint32_t)f2bf(tv[3]) << 16);
       reinterpret_cast<uint2*>(shadow + base)[i] = u;
     }
+    if (split) store_split4(split, k, ld, i, tv);
   }
 }
 
@@ -687,13 +710,18 @@ void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStrea
                                      n));
 }
 
-void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, const float* lr, const uint8_t* active,
-              const uint8_t* first, int K, long P, long ld, float wd, float momentum, float dampening, int nesterov,
-              hipStream_t s) {
+void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, bf16_t* split, const float* lr,
+              const uint8_t* active, const uint8_t* first, int K, long P, long ld, float wd, float momentum,
+              float dampening, int nesterov, hipStream_t s) {
   const long P4 = P / 4;  // P is a multiple of 16 (layout alignment)
   dim3 grid(grid_for(P4, 256, 1024), K);
-  hipLaunchKernelGGL(sgd_kernel, grid, dim3(256), 0, s, theta, grad, mom, shadow, lr, active, first, P4, ld, wd,
+  hipLaunchKernelGGL(sgd_kernel, grid, dim3(256), 0, s, theta, grad, mom, shadow, split, lr, active, first, P4, ld, wd,
                      momentum, dampening, nesterov);
+}
+
+void split_rows(const float* theta, bf16_t* split, int K, long P, long ld, hipStream_t s) {
+  dim3 grid(grid_for(P / 4, 256, 1024), K);
+  hipLaunchKernelGGL(split_rows_kernel, grid, dim3(256), 0, s, theta, split, P / 4, ld);
 }
 
 void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shadow, const float* lr,

@@ -5,7 +5,8 @@ first executor in a process takes a cross-process lock, picks the GPU with enoug
 for its previous peak and releases the lock after the first batch. With all
 of a rank's clients advancing together, the equivalent decision is made once, up front:
 
-  per_client = optimizer/parameter state (θ, grad, momentum[, Adam v], bf16 shadow: P_pad each)
+  per_client = optimizer/parameter state (θ, grad, momentum[, Adam v], bf16 shadow or the fp32
+               GEMMs' pre-split weight planes: P_pad each)
              + activation peak of one client's training step (measured by a probe step)
   capacity   = min(clients this rank hosts, ⌊budget / per_client⌋),  budget = fraction × free HBM
 
@@ -30,6 +31,8 @@ def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
         n += 4 * P
     if compute_dtype != torch.float32:
         n += torch.tensor([], dtype=compute_dtype).element_size() * P
+    elif optimizer.lower() != "adam":
+        n += 4 * P  # pre-split (hi, lo) bf16 weight planes of the fp32 GEMMs (CohortBuffers.split)
     return n
 
 
@@ -61,7 +64,8 @@ def probe_activation_bytes(model, dc, hyper, device, compute_dtype) -> int:
     loss.sum().backward()
     # parameter / gradient rows are state (counted by state_bytes_per_client), not activations
     b = trainer.buffers
-    state = {t.untyped_storage().data_ptr() for t in (b.theta, b.grad, b.state1, b.state2, b.shadow) if t is not None}
+    state = {t.untyped_storage().data_ptr() for t in (b.theta, b.grad, b.state1, b.state2, b.shadow, b.split)
+             if t is not None}
     acts = [nb for ptr, nb in seen.items() if ptr not in state]
     saved = sum(acts)
     biggest = max(acts, default=0)

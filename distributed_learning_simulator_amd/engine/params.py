@@ -19,6 +19,7 @@ Parameter order/naming follows PyTorch `state_dict` naming of the equivalent nn.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -147,6 +148,14 @@ class CohortBuffers:
             torch.zeros((capacity, P), dtype=compute_dtype, device=device)
             if compute_dtype != torch.float32 else None
         )
+        # fp32 compute on the GPU: every row's weights also as (bf16 hi, bf16 lo) planes, written by
+        # the SGD kernel with θ, so the split-bf16 convolutions load the weight operand pre-split
+        # instead of splitting it in every workgroup (DLS_WSPLIT=0 disables; SGD only)
+        self.split = (
+            torch.zeros((capacity, 2, P), dtype=torch.bfloat16, device=device)
+            if (compute_dtype == torch.float32 and torch.device(device).type == "cuda"
+                and optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "1") != "0") else None
+        )
 
     @property
     def compute(self) -> torch.Tensor:
@@ -154,7 +163,7 @@ class CohortBuffers:
 
     def nbytes(self) -> int:
         n = 0
-        for t in (self.theta, self.grad, self.state1, self.state2, self.shadow):
+        for t in (self.theta, self.grad, self.state1, self.state2, self.shadow, self.split):
             if t is not None:
                 n += t.numel() * t.element_size()
         return n
@@ -167,18 +176,27 @@ class BoundParams:
     grad: [K, P] fp32 or None (inference)."""
 
     def __init__(self, layout: ParamLayout, compute: torch.Tensor, grad: torch.Tensor | None,
-                 K: int | None = None):
+                 K: int | None = None, split: torch.Tensor | None = None):
         self.layout = layout
         self.index = layout.index()
         self.compute = compute
         self.grad = grad
         self.K = K if K is not None else compute.shape[0]
         self.token = torch.empty(0, requires_grad=grad is not None)
+        self.split = split  # [K, 2, P] bf16 (hi, lo) planes of `compute`, or None
 
     def w(self, name: str) -> torch.Tensor:
         e = self.index[name]
         v = self.compute[:, e.offset : e.offset + e.numel]
         return v.unflatten(1, e.shape)
+
+    def ws(self, name: str) -> torch.Tensor | None:
+        """The weight's bf16 hi plane (same shape as w(name); the lo plane follows at +P in the
+        split buffer), or None when no pre-split planes are live."""
+        if self.split is None:
+            return None
+        e = self.index[name]
+        return self.split[:, 0, e.offset : e.offset + e.numel].unflatten(1, e.shape)
 
     def g(self, name: str) -> torch.Tensor | None:
         if self.grad is None:

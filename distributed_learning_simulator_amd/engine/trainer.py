@@ -135,6 +135,10 @@ class CohortTrainer:
         self.use_graphs = os.environ.get("DLS_GRAPHS", "1") != "0"
         self._graphs: dict = {}
         self.max_graphs = int(os.environ.get("DLS_MAX_GRAPHS", "2"))
+        # pre-split weight planes (buffers.split) are read by the convolutions only inside a
+        # graphed training run: refreshed from θ when it starts and after epoch hooks, kept
+        # current by the SGD kernel in between (no other θ writer runs there)
+        self._split_live = False
         self.hooks = HookRegistry()
         self.adam_step_count = torch.zeros(capacity, dtype=torch.float32, device=self.device)
         self.graph = dataset_collection.graph
@@ -229,7 +233,9 @@ class CohortTrainer:
         separate rows of `grad_rows` (default grad[row0:row0+K])."""
         b = self.buffers
         grad = grad_rows if grad_rows is not None else b.grad[row0 : row0 + K]
-        params = BoundParams(self.layout, b.compute[:1] if shared else b.compute[row0 : row0 + K], grad, K=K)
+        split = b.split[row0 : row0 + K] if (self._split_live and not shared) else None
+        params = BoundParams(self.layout, b.compute[:1] if shared else b.compute[row0 : row0 + K], grad, K=K,
+                             split=split)
         ctx = RunCtx(params, valid, training=True, client_ids=client_ids, seed=step_seed)
         logits = self.model.forward(x, ctx)
         loss, correct = Fn.cross_entropy(logits, labels, valid)
@@ -282,7 +288,8 @@ class CohortTrainer:
                          self.adam_step_count[r], weight_decay=h.weight_decay, shadow=shadow)
         else:
             fl.sgd_step(b.theta[r], b.grad[r], b.state1[r], lr, active, first, h.weight_decay,
-                        h.momentum, h.dampening, h.nesterov, shadow)
+                        h.momentum, h.dampening, h.nesterov, shadow,
+                        b.split[r] if self._split_live else None)
 
     # ------------------------------------------------------------------ streams
     def _sub_cohorts(self, K: int) -> list[tuple[int, int]]:
@@ -448,6 +455,10 @@ class CohortTrainer:
         sg.correct.zero_()
         sg.samples.zero_()
         self.hooks.exec(ExecutorHookPoint.BEFORE_EXECUTE, executor=executor)
+        split = self.buffers.split
+        if split is not None:
+            fl.split_rows(self.buffers.theta[:K], split[:K])
+            self._split_live = True
         e = 0
         try:
             for s in range(schedule.steps):
@@ -488,9 +499,13 @@ class CohortTrainer:
                     if self.hooks.has_hook(ExecutorHookPoint.AFTER_EPOCH):
                         self.hooks.exec(ExecutorHookPoint.AFTER_EPOCH, executor=executor, epoch=epoch_base + e + 1,
                                         stats=stats, local_epoch=e)
+                        if split is not None:  # (an epoch hook may rewrite θ rows: FedOBD stage 2)
+                            fl.split_rows(self.buffers.theta[:K], split[:K])
                     e += 1
         except StopExecutingException:
             pass
+        finally:
+            self._split_live = False
         self.hooks.exec(ExecutorHookPoint.AFTER_EXECUTE, executor=executor, stats=stats)
         return stats
 

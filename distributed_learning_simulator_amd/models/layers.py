@@ -135,7 +135,8 @@ class Conv2d(Module):
         P = ctx.P
         b = P.w(self.b) if self.b else None
         gb = P.g(self.b) if self.b else None
-        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb, link=link, stats=stats)
+        return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb, link=link, stats=stats,
+                         w_split=P.ws(self.w))
 
 
 class BatchNorm(Module):

@@ -26,10 +26,15 @@ from . import backend, ref
 
 
 def sgd_step(theta, grad, mom, lr, active, first_step, weight_decay=0.0, momentum=0.0,
-             dampening=0.0, nesterov=False, shadow=None):
+             dampening=0.0, nesterov=False, shadow=None, split=None):
     be = backend.get(theta)
     be.sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, nesterov,
-                first_step, shadow)
+                first_step, shadow, split)
+
+
+def split_rows(theta, split):
+    """Refresh the pre-split (hi, lo) bf16 weight planes of θ rows (fp32 GEMM operand)."""
+    backend.get(theta).split_rows(theta, split)
 
 
 def adam_step(theta, grad, m, v, lr, active, step, beta1=0.9, beta2=0.999, eps=1e-8,

@@ -57,20 +57,27 @@ class _Conv(torch.autograd.Function):
     real channels' gradient is written back."""
 
     @staticmethod
-    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None, stats=None):
+    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None, stats=None, w_split=None):
         be = _be(x)
         ci = w.shape[-1]
         if x.shape[-1] > ci:
             w = torch.nn.functional.pad(w, (0, x.shape[-1] - ci))
+            w_split = None  # (the padded copy has no planes)
+        if be is ref or x.dtype != torch.float32:
+            w_split = None
         if stats is not None and be is not ref and x.dtype == torch.float32 and EPILOGUE_BN_STATS:
             K, B, H, W = x.shape[:4]
             KH = w.shape[2]
             OH, OW = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - w.shape[3]) // stride + 1
             stats.part = torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
                                      device=x.device)
-            y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid)
+            y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid,
+                            **({"w_split": w_split} if w_split is not None else {}))
+        elif w_split is not None:
+            y = be.conv_fwd(x, w, stride, pad, bias=b, w_split=w_split)
         else:
             y = be.conv_fwd(x, w, stride, pad, bias=b)
+        ctx.w_split = w_split
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         ctx.link = link
@@ -87,7 +94,10 @@ class _Conv(torch.autograd.Function):
         if link is not None:
             link.grad = None
         if ctx.needs_input_grad[0]:
-            dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc)
+            if ctx.w_split is not None:
+                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split)
+            else:
+                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc)
             if dx.shape[-1] > ctx.ci:
                 dx = dx[..., : ctx.ci]
         elif acc is not None:
@@ -106,17 +116,17 @@ class _Conv(torch.autograd.Function):
                     be.bias_grad(dy, ctx.gb)
             if padded:
                 ctx.gw.copy_(gw[..., : ctx.ci])
-        return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None, link: ResidualLink | None = None,
-           stats: BNStats | None = None):
+           stats: BNStats | None = None, w_split: torch.Tensor | None = None):
     """`link`: this conv's input is also the identity shortcut of a residual BN fed the same
     link (its gradient then arrives through the dgrad epilogue). `stats`: the output feeds a
     BatchNorm given the same holder (its statistics come from this conv's epilogue)."""
     if link is not None:
         assert stride == 1 and w.shape[-1] == x.shape[-1], "residual link needs a stride-1, unpadded conv"
-    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link, stats)
+    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link, stats, w_split)
 
 
 # --------------------------------------------------------------------------- linear

@@ -147,7 +147,8 @@ def conv_stats_parts(M: int) -> int:
     return (M + 31) // 32
 
 
-def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats=None, stats_valid=None):
+def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats=None, stats_valid=None,
+             w_split=None):
     """`x` may be a channel slice of a wider buffer, `out` (optional) a channel slice to write
     into (DenseNet block buffer): both are read / written in place through channel strides.
     `stats` (fp32 only): a [K, conv_stats_parts(M), 2, Co] fp32 buffer the epilogue fills with the
@@ -183,13 +184,14 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
         _C.conv_gl_fwd(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, K, rep, B, H, W, C, OH, OW,
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
     _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), x.stride(0), y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
                pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32,
-               _s(), ldx, ldy, _p(stats), _p(stats_valid), NULL, 0.0, 0.0)
+               _s(), ldx, ldy, _p(stats), _p(stats_valid), NULL, 0.0, 0.0, ws_p, ws_cs, ws_plane)
     return y
 
 
-def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None):
     """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
     residual branch of a ResNet block, so autograd never materialises the sum separately).
     `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient)."""
@@ -214,8 +216,9 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None):
         return dx
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
     _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
-                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy.stride(0))
+                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy.stride(0), ws_p, ws_cs, ws_plane)
     return dx
 
 
@@ -264,7 +267,7 @@ def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_see
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
                int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL,
-               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0)
+               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, NULL, 0, 0)
     return y
 
 
@@ -284,7 +287,7 @@ def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0):
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
                1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0,
-               NULL, NULL, NULL, 0.0, float(gate_scale))
+               NULL, NULL, NULL, 0.0, float(gate_scale), NULL, 0, 0)
     return dx
 
 
@@ -699,12 +702,17 @@ def _row_args(theta):
     return K, P, theta.stride(0)
 
 
-def sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, nesterov, first_step, shadow=None):
+def sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, nesterov, first_step, shadow=None,
+             split=None):
+    """`split` [K, 2, P] bf16: the rows' (hi, lo) weight planes, rewritten with the new θ (the
+    fp32 convolutions read them instead of splitting the weights in every workgroup)."""
     K, P, ld = _row_args(theta)
     assert grad.stride(0) == ld and mom.stride(0) == ld
     if shadow is not None:
         assert shadow.stride(0) == ld and shadow.dtype == BF16
-    _C.sgd_step(_p(theta), _p(grad), _p(mom), _p(shadow), _p(lr.float().contiguous()),
+    if split is not None:
+        assert split.shape == (K, 2, P) and split.is_contiguous() and split.dtype == BF16 and ld == P
+    _C.sgd_step(_p(theta), _p(grad), _p(mom), _p(shadow), _p(split), _p(lr.float().contiguous()),
                 _p(active.to(torch.uint8).contiguous()), _p(first_step.to(torch.uint8).contiguous()), K, P, ld,
                 float(weight_decay), float(momentum), float(dampening), int(nesterov), _s())
 
@@ -714,6 +722,24 @@ def adam_step(theta, grad, m, v, lr, active, step, beta1, beta2, eps, weight_dec
     _C.adam_step(_p(theta), _p(grad), _p(m), _p(v), _p(shadow), _p(lr.float().contiguous()),
                  _p(active.to(torch.uint8).contiguous()), _p(step.float().contiguous()), K, P, ld, beta1, beta2, eps,
                  weight_decay, _s())
+
+
+def split_rows(theta, split):
+    """split[k] = (bf16 hi, bf16 lo) planes of theta[k] (x = hi + lo, RNE hi)."""
+    K, P, ld = _row_args(theta)
+    assert split.shape == (K, 2, P) and split.is_contiguous() and split.dtype == BF16 and ld == P
+    _C.split_rows(_p(theta), _p(split), K, P, ld, _s())
+
+
+def _wsplit_args(w_split, w):
+    """(pointer, client stride, hi→lo plane distance) of a weight's pre-split planes: `w_split`
+    is the hi-plane view of the weight inside a [K, 2, P] split buffer, same shape as `w`."""
+    if w_split is None:
+        return NULL, 0, 0
+    assert w_split.dtype == BF16 and w_split.shape == w.shape, (w_split.shape, w.shape)
+    base = w_split._base if w_split._base is not None else w_split
+    assert base.dim() == 3 and base.shape[1] == 2, "w_split must view a [K, 2, P] split buffer"
+    return _p(w_split), w_split.stride(0), base.stride(1)
 
 
 def broadcast_rows(theta_rows, src, shadow_rows=None):

@@ -357,7 +357,7 @@ def spmm(rowptr, col, val, x):
 
 # ---------------------------------------------------------------- optimiser / FL math
 def sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, nesterov,
-             first_step, shadow=None):
+             first_step, shadow=None, split=None):
     """Fused SGD over flat [K,P] buffers (torch.optim.SGD semantics, per-client lr[K]).
     `first_step[k]` (bool) makes buf = g (torch initialises the momentum buffer with the
     first gradient). Inactive clients are left untouched."""
@@ -374,6 +374,8 @@ def sgd_step(theta, grad, mom, lr, active, weight_decay, momentum, dampening, ne
     theta.copy_(torch.where(a[:, None], new, theta))
     if shadow is not None:
         shadow.copy_(theta.to(shadow.dtype))
+    if split is not None:
+        split_rows(theta, split)
 
 
 def adam_step(theta, grad, m, v, lr, active, step, beta1, beta2, eps, weight_decay, shadow=None):
@@ -425,3 +427,10 @@ def broadcast_rows(dst, src, rows=None):
 
 def delta(theta, base):
     return theta - base.unsqueeze(0)
+
+
+def split_rows(theta, split):
+    """split[k] = (bf16 hi, bf16 lo) planes of theta[k]: hi = RNE(x), lo = RNE(x - hi)."""
+    hi = theta.to(torch.bfloat16)
+    split[:, 0].copy_(hi)
+    split[:, 1].copy_((theta - hi.float()).to(torch.bfloat16))

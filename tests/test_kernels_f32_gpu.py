@@ -87,11 +87,12 @@ def test_conv_f32_every_variant(hip, case):
     for v in range(hip._C.conv_nt_f32_num_variants()):
         y = torch.empty_like(dy)
         hip._C.conv_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, B * H * W * Ci, M * Co, w.stride(0), 0, B, H, W,
-                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0, 0, 0, 0, 0.0, 0.0)
+                       Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0, 0, 0, 0, 0.0, 0.0,
+                       0, 0, 0)
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
-                          W, Ci, k, k, s, p, v, 1, stream, 0, 0)
+                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0)
         _close(dx, dx_ref)
     for v in range(hip._C.conv_tn_f32_num_variants()):
         gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
@@ -409,3 +410,40 @@ def test_synthetic_image_generator_matches_cpu(hip):
     b = cpu.gather(idx)
     assert a.shape == b.shape == (4, 224, 224, 8)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", [(3, 2, 8, 8, 64, 128, 3, 1, 1), (2, 2, 9, 9, 64, 128, 3, 2, 1),
+                                  (2, 3, 8, 8, 64, 64, 3, 1, 1), (2, 2, 8, 8, 128, 256, 1, 2, 0)])
+def test_conv_presplit_weight_planes(hip, case):
+    """Pre-split weight planes (the SGD kernel's `split` output, read by the fp32 conv fwd / dgrad
+    instead of splitting w per workgroup) give bit-identical results to the in-kernel split, and
+    sgd_step(split=) writes exactly split_rows(θ_new)."""
+    from distributed_learning_simulator_amd.ops import ref
+
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(5)
+    n = Co * k * k * Ci
+    P = ((n + 32 + 15) // 16) * 16
+    theta = _f(K, P, scale=0.2)
+    grad, mom = _f(K, P), torch.zeros(K, P, device=DEV)
+    split = torch.zeros((K, 2, P), dtype=torch.bfloat16, device=DEV)
+    lr = torch.full((K,), 0.05, device=DEV)
+    on = torch.ones(K, dtype=torch.bool, device=DEV)
+    hip.sgd_step(theta, grad, mom, lr, on, 0.0, 0.9, 0.0, False, on, None, split)
+    exp = torch.zeros_like(split)
+    hip.split_rows(theta, exp)
+    assert torch.equal(split, exp)
+    ref_split = torch.zeros_like(split)
+    ref.split_rows(theta, ref_split)
+    assert torch.equal(split, ref_split)  # CPU rule == GPU planes (RNE hi, RNE lo)
+    w = theta[:, 16 : 16 + n].unflatten(1, (Co, k, k, Ci))
+    ws = split[:, 0, 16 : 16 + n].unflatten(1, (Co, k, k, Ci))
+    x = _f(K, B, H, W, Ci)
+    y0 = hip.conv_fwd(x, w, s, p)
+    y1 = hip.conv_fwd(x, w, s, p, w_split=ws)
+    assert torch.equal(y0, y1)
+    dy = _f(*y0.shape)
+    dx0 = hip.conv_dgrad(dy, w, (H, W), s, p)
+    dx1 = hip.conv_dgrad(dy, w, (H, W), s, p, w_split=ws)
+    assert torch.equal(dx0, dx1)
+    _close(y1, ref.conv_fwd(_d(x), _d(w), s, p))
