@@ -18,6 +18,7 @@ wave; ResNet-50/ImageNet at batch 128 costs ≈20 GB of activations and runs in 
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -31,7 +32,7 @@ def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
         n += 4 * P
     if compute_dtype != torch.float32:
         n += torch.tensor([], dtype=compute_dtype).element_size() * P
-    elif optimizer.lower() != "adam":
+    elif optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "0") == "1":
         n += 4 * P  # pre-split (hi, lo) bf16 weight planes of the fp32 GEMMs (CohortBuffers.split)
     return n
 

@@ -341,6 +341,15 @@ class CohortTrainer:
                 main.wait_stream(st)
 
         self.hooks.exec(ExecutorHookPoint.BEFORE_EXECUTE, executor=executor)
+        # pre-split weight planes in eager runs too (Transformer / text models), when nothing but
+        # this loop's optimizer steps writes θ between two forwards
+        split = self.buffers.split
+        if (split is not None and not self.hooks.has_hook(ExecutorHookPoint.OPTIMIZER_STEP)
+                and not self.hooks.has_hook(ExecutorHookPoint.AFTER_BATCH) and self.model.input_kind != "graph"):
+            fl.split_rows(self.buffers.theta[:K], split[:K])
+            self._split_live = True
+        else:
+            split = None
         if multi:
             fork()
         try:
@@ -361,11 +370,15 @@ class CohortTrainer:
                             join()
                         self.hooks.exec(ExecutorHookPoint.AFTER_EPOCH, executor=executor, epoch=epoch_base + e + 1,
                                         stats=stats, local_epoch=e)
+                        if split is not None:  # (an epoch hook may rewrite θ rows)
+                            fl.split_rows(self.buffers.theta[:K], split[:K])
                         if multi:
                             fork()
                     e += 1
         except StopExecutingException:
             pass
+        finally:
+            self._split_live = False
         if multi:
             join()
         self.hooks.exec(ExecutorHookPoint.AFTER_EXECUTE, executor=executor, stats=stats)

@@ -190,7 +190,7 @@ class Linear(Module):
         """`fuse`: epilogue fusions of Fn.linear (relu, premasked, gate_input, residual)."""
         P = ctx.P
         return Fn.linear(x, ctx.token, P.w(self.w), P.w(self.b) if self.b else None,
-                         P.g(self.w), P.g(self.b) if self.b else None, **fuse)
+                         P.g(self.w), P.g(self.b) if self.b else None, w_split=P.ws(self.w), **fuse)
 
 
 class LayerNorm(Module):

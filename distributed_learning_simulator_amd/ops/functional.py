@@ -145,9 +145,13 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False,
-                drop_p=0.0, drop_seeds=None, gate_scale=1.0):
+                drop_p=0.0, drop_seeds=None, gate_scale=1.0, w_split=None):
         be = _be(x)
-        y = be.linear_fwd(x, w, b, relu=relu, acc=residual, drop_p=drop_p, drop_seeds=drop_seeds)
+        if be is ref or x.dtype != torch.float32:
+            w_split = None
+        ws = {"w_split": w_split} if w_split is not None else {}
+        y = be.linear_fwd(x, w, b, relu=relu, acc=residual, drop_p=drop_p, drop_seeds=drop_seeds, **ws)
+        ctx.ws = ws
         mask_dy = relu and not premasked
         ctx.save_for_backward(x, w, y if mask_dy else None, drop_seeds if drop_p else None)
         ctx.gw, ctx.gb = gw, gb
@@ -169,7 +173,7 @@ class _Linear(torch.autograd.Function):
         elif ctx.drop_p and not ctx.premasked:
             dy = be.dropout_apply(dy, seeds, ctx.drop_p)  # the GEMM branch's gradient
         gate = x.contiguous() if ctx.gate_input else None
-        dx = be.linear_dgrad(dy, w, gate=gate, gate_scale=ctx.gate_scale) if ctx.needs_input_grad[0] else None
+        dx = be.linear_dgrad(dy, w, gate=gate, gate_scale=ctx.gate_scale, **ctx.ws) if ctx.needs_input_grad[0] else None
         if ctx.gw is not None:
             if be is ref:
                 dw, db = ref.linear_wgrad(dy.float(), x.float(), ctx.gb is not None)
@@ -178,18 +182,20 @@ class _Linear(torch.autograd.Function):
                     ctx.gb.copy_(db)
             else:
                 be.linear_wgrad(dy, x, ctx.gw, ctx.gb)
-        return dx, None, None, None, None, None, dres, None, None, None, None, None, None
+        return dx, None, None, None, None, None, dres, None, None, None, None, None, None, None
 
 
 def linear(x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False,
-           drop_p: float = 0.0, drop_seeds=None, gate_scale: float = 1.0):
+           drop_p: float = 0.0, drop_seeds=None, gate_scale: float = 1.0, w_split=None):
     """x [K, N, Fi] -> [K, N, Fo]; any extra middle dims are flattened. Epilogue fusions: see
-    _Linear (relu / premasked / gate_input / residual / dropout)."""
+    _Linear (relu / premasked / gate_input / residual / dropout). `w_split`: the weight's
+    pre-split bf16 planes (BoundParams.ws) for the fp32 GEMMs."""
     assert not (relu and residual is not None), "ReLU and residual epilogues are not combined"
     shp = x.shape
     x3 = x.reshape(shp[0], -1, shp[-1])
     r3 = residual.reshape(shp[0], x3.shape[1], -1).contiguous() if residual is not None else None
-    y = _Linear.apply(x3, token, w, b, gw, gb, r3, relu, premasked, gate_input, drop_p, drop_seeds, gate_scale)
+    y = _Linear.apply(x3, token, w, b, gw, gb, r3, relu, premasked, gate_input, drop_p, drop_seeds, gate_scale,
+                      w_split)
     return y.reshape(*shp[:-1], y.shape[-1])
 
 

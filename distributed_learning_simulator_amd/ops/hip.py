@@ -251,7 +251,7 @@ def bias_grad(dy, gb):
 
 
 # --------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_seeds=None):
+def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_seeds=None, w_split=None):
     """y = x Wᵀ + b, optionally ReLU'd, dropped out (`drop_p`, per-client-row `drop_seeds`
     [K] int32: the epilogue mask of `dropout_apply`) and/or + `acc` (a residual branch), in the
     epilogue."""
@@ -265,13 +265,14 @@ def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_see
     y = torch.empty((K, N, Fo), dtype=x.dtype, device=x.device)
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
                int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL,
-               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, NULL, 0, 0)
+               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, ws_p, ws_cs, ws_plane)
     return y
 
 
-def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0):
+def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0, w_split=None):
     """dX = dY W, zeroed where `gate` <= 0 when given (gate = the ReLU output this layer read:
     the gradient then leaves already through the ReLU), times `gate_scale` (the 1/(1-p) of a
     dropout folded into that ReLU output)."""
@@ -285,9 +286,10 @@ def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0):
     if gate is not None:
         assert gate.shape == dx.shape and gate.dtype == dy.dtype and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
                1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0,
-               NULL, NULL, NULL, 0.0, float(gate_scale), NULL, 0, 0)
+               NULL, NULL, NULL, 0.0, float(gate_scale), ws_p, ws_cs, ws_plane)
     return dx
 
 

@@ -447,3 +447,19 @@ def test_conv_presplit_weight_planes(hip, case):
     dx1 = hip.conv_dgrad(dy, w, (H, W), s, p, w_split=ws)
     assert torch.equal(dx0, dx1)
     _close(y1, ref.conv_fwd(_d(x), _d(w), s, p))
+
+
+def test_linear_presplit_weight_planes(hip):
+    """Linear fwd / dgrad with pre-split weight planes == the in-kernel split, bit for bit."""
+    torch.manual_seed(6)
+    K, N, Fi, Fo = 3, 77, 256, 512
+    P = Fo * Fi + 16
+    theta = _f(K, P, scale=0.05)
+    split = torch.zeros((K, 2, P), dtype=torch.bfloat16, device=DEV)
+    hip.split_rows(theta, split)
+    w = theta[:, :Fo * Fi].unflatten(1, (Fo, Fi))
+    ws = split[:, 0, :Fo * Fi].unflatten(1, (Fo, Fi))
+    x, b = _f(K, N, Fi), _f(K, Fo)
+    assert torch.equal(hip.linear_fwd(x, w, b), hip.linear_fwd(x, w, b, w_split=ws))
+    dy = _f(K, N, Fo)
+    assert torch.equal(hip.linear_dgrad(dy, w), hip.linear_dgrad(dy, w, w_split=ws))
