@@ -131,12 +131,12 @@ class Conv2d(Module):
     def own_params(self):
         return [self.w] + ([self.b] if self.b else [])
 
-    def forward(self, x, ctx, link=None, stats=None):
+    def forward(self, x, ctx, link=None, stats=None, donor=None):
         P = ctx.P
         b = P.w(self.b) if self.b else None
         gb = P.g(self.b) if self.b else None
         return Fn.conv2d(x, ctx.token, P.w(self.w), P.g(self.w), self.stride, self.pad, b, gb, link=link, stats=stats,
-                         w_split=P.ws(self.w))
+                         w_split=P.ws(self.w), donor=donor)
 
 
 class BatchNorm(Module):
@@ -166,10 +166,10 @@ class BatchNorm(Module):
                              stats=stats)
 
 
-def conv_bn(conv: Conv2d, bn: BatchNorm, x, ctx, conv_link=None, **bn_kw):
+def conv_bn(conv: Conv2d, bn: BatchNorm, x, ctx, conv_link=None, conv_donor=None, **bn_kw):
     """conv → BatchNorm with the BN statistics taken from the conv's epilogue (Fn.BNStats)."""
     st = Fn.BNStats(ctx.valid)
-    return bn.forward(conv.forward(x, ctx, link=conv_link, stats=st), ctx, stats=st, **bn_kw)
+    return bn.forward(conv.forward(x, ctx, link=conv_link, stats=st, donor=conv_donor), ctx, stats=st, **bn_kw)
 
 
 class Linear(Module):

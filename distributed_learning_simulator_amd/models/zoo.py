@@ -87,17 +87,19 @@ class LeNet5Net(Module):
 
 # ------------------------------------------------------------------------- ResNets
 def _residual_link(block, x, ctx):
-    """Identity-shortcut blocks in training route the shortcut gradient through conv1's dgrad
-    epilogue (Fn.ResidualLink) instead of a separate autograd add over the block input."""
-    if block.down is None and ctx.training and x.requires_grad:
+    """Blocks in training route the shortcut's gradient of the block input through conv1's dgrad
+    epilogue (Fn.ResidualLink) instead of a separate autograd add over the block input: the
+    identity shortcut's from the last BN, a downsample shortcut's from its conv (the donor)."""
+    if ctx.training and x.requires_grad:
         return Fn.ResidualLink()
     return None
 
 
-def _down(seq: Seq, x, ctx):
-    """Downsample shortcut Seq(Conv2d 1x1, BatchNorm) with epilogue statistics."""
+def _down(seq: Seq, x, ctx, donor=None):
+    """Downsample shortcut Seq(Conv2d 1x1, BatchNorm) with epilogue statistics; `donor`: the
+    shortcut conv's input gradient goes to the block's first conv (Fn.ResidualLink)."""
     conv, bn = seq.children
-    return conv_bn(conv, bn, x, ctx)
+    return conv_bn(conv, bn, x, ctx, conv_donor=donor)
 
 
 class BasicBlock(Module):
@@ -117,8 +119,9 @@ class BasicBlock(Module):
     def forward(self, x, ctx):
         link = _residual_link(self, x, ctx)
         out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link)
-        sc = x if self.down is None else _down(self.down, x, ctx)
-        return conv_bn(self.conv2, self.bn2, out, ctx, residual=sc, relu=True, link=link)
+        sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
+        return conv_bn(self.conv2, self.bn2, out, ctx, residual=sc, relu=True,
+                       link=link if self.down is None else None)
 
 
 class Bottleneck(Module):
@@ -142,8 +145,9 @@ class Bottleneck(Module):
         link = _residual_link(self, x, ctx)
         out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link)
         out = conv_bn(self.conv2, self.bn2, out, ctx)
-        sc = x if self.down is None else _down(self.down, x, ctx)
-        return conv_bn(self.conv3, self.bn3, out, ctx, residual=sc, relu=True, link=link)
+        sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
+        return conv_bn(self.conv3, self.bn3, out, ctx, residual=sc, relu=True,
+                       link=link if self.down is None else None)
 
 
 class ResNetNet(Module):

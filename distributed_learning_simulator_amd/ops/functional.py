@@ -23,15 +23,19 @@ def _be(t):
 
 # --------------------------------------------------------------------------- conv2d
 class ResidualLink:
-    """Hands the identity-shortcut gradient of a residual block from the block's last BN
-    (whose backward runs first) to the block's first conv, whose dgrad adds it in its epilogue:
-    autograd then never materialises `dX_conv + dX_shortcut` with a separate add pass over the
-    block input (ResNet BasicBlock / Bottleneck without downsample)."""
+    """Hands a second gradient of a residual block's input to the block's first conv, whose
+    dgrad adds it in its epilogue: autograd then never materialises `dX_conv + dX_other` with a
+    separate add pass over the block input.
+    - identity shortcut: the block's last BN (whose backward runs first) deposits dX_shortcut;
+    - downsample shortcut: the shortcut conv (`donor`) deposits its dX. Autograd normally runs
+      it before the main branch reaches the first conv; if not, the first conv marks
+      `receiver_done` and the donor returns its dX to autograd as usual (same result)."""
 
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "receiver_done")
 
     def __init__(self):
         self.grad = None
+        self.receiver_done = False
 
 
 # DLS_BN_EPILOGUE_STATS=0: BatchNorm computes its statistics in its own pass (A/B switch)
@@ -57,7 +61,7 @@ class _Conv(torch.autograd.Function):
     real channels' gradient is written back."""
 
     @staticmethod
-    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None, stats=None, w_split=None):
+    def forward(ctx, x, token, w, gw, stride, pad, b, gb, link=None, stats=None, w_split=None, donor=None):
         be = _be(x)
         ci = w.shape[-1]
         if x.shape[-1] > ci:
@@ -81,6 +85,7 @@ class _Conv(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         ctx.link = link
+        ctx.donor = donor
         return y
 
     @staticmethod
@@ -93,6 +98,8 @@ class _Conv(torch.autograd.Function):
         acc = link.grad if link is not None else None
         if link is not None:
             link.grad = None
+            if acc is None:
+                link.receiver_done = True  # (a late donor hands its dX to autograd instead)
         if ctx.needs_input_grad[0]:
             if ctx.w_split is not None:
                 dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split)
@@ -116,17 +123,22 @@ class _Conv(torch.autograd.Function):
                     be.bias_grad(dy, ctx.gb)
             if padded:
                 ctx.gw.copy_(gw[..., : ctx.ci])
-        return dx, None, None, None, None, None, None, None, None, None, None
+        donor = ctx.donor
+        if donor is not None and dx is not None and not donor.receiver_done:
+            donor.grad = dx  # added by the block's first conv in its dgrad epilogue
+            dx = None
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, token, w, gw, stride=1, pad=0, b=None, gb=None, link: ResidualLink | None = None,
-           stats: BNStats | None = None, w_split: torch.Tensor | None = None):
-    """`link`: this conv's input is also the identity shortcut of a residual BN fed the same
-    link (its gradient then arrives through the dgrad epilogue). `stats`: the output feeds a
+           stats: BNStats | None = None, w_split: torch.Tensor | None = None, donor: ResidualLink | None = None):
+    """`link`: this conv's input gets a second gradient through the link (identity shortcut of a
+    residual BN, or a downsample conv given the same link as `donor`), added in the dgrad epilogue.
+    `donor`: this conv's input gradient is deposited in the link instead of returned. `stats`: the output feeds a
     BatchNorm given the same holder (its statistics come from this conv's epilogue)."""
     if link is not None:
-        assert stride == 1 and w.shape[-1] == x.shape[-1], "residual link needs a stride-1, unpadded conv"
-    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link, stats, w_split)
+        assert w.shape[-1] == x.shape[-1], "a residual link needs an unpadded conv"
+    return _Conv.apply(x, token, w, gw, stride, pad, b, gb, link, stats, w_split, donor)
 
 
 # --------------------------------------------------------------------------- linear

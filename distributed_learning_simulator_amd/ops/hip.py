@@ -205,8 +205,10 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None):
     H, W = int(in_hw[0]), int(in_hw[1])
     dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
     if acc is not None:
-        assert stride == 1 and acc.shape == dx.shape and acc.dtype == dy.dtype and acc.is_contiguous(), acc.shape
-    if not f32 and ld_dy == Co and (stride == 1 or gl_mode == 1) and _gl(K, B * H * W, Ci, Co, KH * KW):
+        # (stride > 1: every parity-class launch adds acc at the pixels it writes)
+        assert acc.shape == dx.shape and acc.dtype == dy.dtype and acc.is_contiguous(), acc.shape
+    if (not f32 and ld_dy == Co and (stride == 1 or (gl_mode == 1 and acc is None))
+            and _gl(K, B * H * W, Ci, Co, KH * KW)):
         # (strided dgrad splits into stride² short-K parity classes: conv_nt's smaller tiles win
         # there, l3a dgrad 447 vs 396 TFLOP/s). Large tiles want a k-contiguous B: one flip+transpose pass over the weight rows
         # (weights are small next to the activations), then stride² parity-class launches

@@ -111,8 +111,9 @@ def test_zero_padded_input_channels_are_exact():
 
 @pytest.mark.parametrize("name,ds", [("ResNet18", "CIFAR10"), ("Resnet50", "ImageNet")])
 def test_residual_link_gradients_equal_autograd_sum(name, ds, monkeypatch):
-    """Identity-shortcut gradients routed through conv1's dgrad epilogue (Fn.ResidualLink)
-    equal autograd's own accumulation of the two branches."""
+    """Shortcut gradients routed through conv1's dgrad epilogue (Fn.ResidualLink: identity
+    shortcuts from the last BN, downsample shortcuts from their conv) equal autograd's own
+    accumulation of the two branches; every downsample donor ran before its receiver (fused)."""
     from distributed_learning_simulator_amd.models import zoo
 
     torch.manual_seed(0)
@@ -134,6 +135,7 @@ def test_residual_link_gradients_equal_autograd_sum(name, ds, monkeypatch):
     monkeypatch.setattr(zoo, "_residual_link", counting)
     loss_l, grad_l = _run(model, x, y, 1, theta.clone())
     assert sum(link is not None for link in made) > 0 and all(link is None or link.grad is None for link in made)
+    assert all(link is None or not link.receiver_done for link in made)
     monkeypatch.setattr(zoo, "_residual_link", lambda *a: None)
     loss_a, grad_a = _run(model, x, y, 1, theta.clone())
     torch.testing.assert_close(loss_l, loss_a)
