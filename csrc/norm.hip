@@ -213,7 +213,18 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
 //        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
 // grid (cdiv(C, 32), K), 1024 threads = 32 channels × 32 part-groups: the per-workgroup partial
 // sums of a client are reduced in a fixed order (deterministic) by 8 lanes per channel.
-constexpr int COEF_GROUPS = 32;  // partial-sum rows reduced in parallel per channel
+// partial-sum rows reduced in parallel per channel: G = 8 (256-thread workgroups) by default,
+// DLS_BN_COEF_GROUPS=32 for the 1024-thread form. The coefficient kernel is tiny and sits on the
+// stream's critical path; a 1024-thread workgroup has to wait for a whole CU's wave slots while
+// the other sub-cohort stream's GEMM workgroups occupy them
+constexpr int COEF_GROUPS = 32;  // (upper bound: shared-memory sizing)
+static int coef_groups() {
+  static const int g = [] {
+    const char* e = getenv("DLS_BN_COEF_GROUPS");
+    return (e && atoi(e) == 32) ? 32 : 8;
+  }();
+  return g;
+}
 
 // First stage for the conv-epilogue statistics, which arrive as one partial per 32 GEMM rows
 // (2,048 per client on a 32x32x64 layer): a single (32-channel, client) workgroup reading them
@@ -249,8 +260,8 @@ __global__ void __launch_bounds__(256) part_fold_kernel(const float* __restrict_
   }
 }
 
-template <typename T, typename PT>
-__global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const PT* __restrict__ ws, int nparts,
+template <typename T, typename PT, int G>
+__global__ void __launch_bounds__(32 * G) bn_coef_kernel(const PT* __restrict__ ws, int nparts,
                                                       const T* __restrict__ gamma,
                                                       const T* __restrict__ beta, const int* __restrict__ valid_rows,
                                                       const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -260,14 +271,14 @@ __global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const PT* __r
                                                       float eps, int rep, int bwd) {
   // partials are summed in fp64 (the conv-epilogue statistics arrive as thousands of 32-row
   // partials per channel; Σx² − n·μ² then keeps its precision), in a fixed order
-  __shared__ double red[2][COEF_GROUPS][33];
+  __shared__ double red[2][G][33];
   const int k = blockIdx.y;
   const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   double d0 = 0.0, d1 = 0.0;
   if (c < C) {
     const PT* part = ws + (long)k * nparts * 2 * C;
-    for (int b = grp; b < nparts; b += COEF_GROUPS) {
+    for (int b = grp; b < nparts; b += G) {
       d0 += part[(long)b * 2 * C + c];
       d1 += part[(long)b * 2 * C + C + c];
     }
@@ -277,7 +288,7 @@ __global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const PT* __r
   __syncthreads();
   if (grp != 0 || c >= C) return;
 #pragma unroll
-  for (int g2 = 1; g2 < COEF_GROUPS; ++g2) {
+  for (int g2 = 1; g2 < G; ++g2) {
     d0 += red[0][g2][cl];
     d1 += red[1][g2][cl];
   }
@@ -309,6 +320,14 @@ __global__ void __launch_bounds__(32 * COEF_GROUPS) bn_coef_kernel(const PT* __r
       dgamma[(long)k * dg_cs + c] = s1;
     }
   }
+}
+
+template <typename TT, typename PT, typename... A>
+void launch_coef(dim3 grid, hipStream_t s, A... args) {
+  if (coef_groups() == 32)
+    hipLaunchKernelGGL((bn_coef_kernel<TT, PT, 32>), grid, dim3(32 * 32), 0, s, args...);
+  else
+    hipLaunchKernelGGL((bn_coef_kernel<TT, PT, 8>), grid, dim3(32 * 8), 0, s, args...);
 }
 
 // thread owns one V-channel chunk and strides over rows; grid (row-blocks, K)
@@ -589,13 +608,13 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
       const int nfold = cdiv(nparts, FOLD);
       double* folds = reinterpret_cast<double*>(ws + bn_fold_offset(K, R, C));
       hipLaunchKernelGGL(part_fold_kernel, dim3(nfold, K), dim3(256), 0, s, pre_part, nparts, 2 * C, folds, nfold);
-      hipLaunchKernelGGL((bn_coef_kernel<TT, double>), dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s,
-                         (const double*)folds, nfold, CP(gamma), CP(beta), valid_rows, nullptr, nullptr, mean, rstd,
-                         coef, nullptr, nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+      launch_coef<TT, double>(dim3(cdiv(C, 32), K), s, (const double*)folds, nfold, CP(gamma), CP(beta), valid_rows,
+                              (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
+                              (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
     } else if (!counters || pre_part) {
-      hipLaunchKernelGGL((bn_coef_kernel<TT, float>), dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, nparts,
-                         CP(gamma), CP(beta), valid_rows, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs,
-                         K, R, C, eps, rep, 0);
+      launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, part, nparts, CP(gamma), CP(beta), valid_rows,
+                             (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
+                             (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
     }
     DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
                                      valid_rows, coef, R, C, relu, rpb, rmask, ldx));
@@ -618,9 +637,9 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
     DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                      mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
     if (!counters)
-      hipLaunchKernelGGL((bn_coef_kernel<TT, float>), dim3(cdiv(C, 32), K), dim3(32 * COEF_GROUPS), 0, s, part, (int)grid.x, CP(gamma),
-                         (const TT*)nullptr, valid_rows, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs,
-                         g_cs, K, R, C, 0.f, 1, 1);
+      launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, (const float*)part, (int)grid.x, CP(gamma), (const TT*)nullptr,
+                             valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K,
+                             R, C, 0.f, 1, 1);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                      valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx));
   });
