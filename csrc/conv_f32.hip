@@ -751,7 +751,8 @@ bool launch_tn_f32_cfg(const ConvTNParams& p, int va, int vb, int grid, hipStrea
 struct TnTile {
   int bm, bn;
 };
-constexpr TnTile kTnF32Tiles[] = {{128, 128}, {64, 128}, {128, 128}, {256, 128}, {128, 256}, {64, 64}, {32, 128}};
+constexpr TnTile kTnF32Tiles[] = {{128, 128}, {64, 128}, {128, 128}, {256, 128}, {128, 256}, {64, 64}, {32, 128},
+                                   {64, 256}};
 constexpr int kTnF32Variants = sizeof(kTnF32Tiles) / sizeof(kTnF32Tiles[0]);
 constexpr int TN_BKT_MAX = 32;
 
@@ -764,6 +765,10 @@ bool launch_tn_f32_variant(int v, const ConvTNParams& p, int va, int vb, int gri
     case 4: return launch_tn_f32_cfg<128, 256, 32, 2, 4, 1, false>(p, va, vb, grid, s);  // 60 KB
     case 5: return launch_tn_f32_cfg<64, 64, 32, 2, 2, 2, true>(p, va, vb, grid, s);    // 40 KB
     case 6: return launch_tn_f32_cfg<32, 128, 32, 1, 4, 2, true>(p, va, vb, grid, s);   // 56 KB, Co <= 32
+    // 64x256, 49 KB single-buffered: 4 column fragments per wave, twice the MFMAs per k-step of
+    // the 64x128 tile. Measured slower on Co = 64 (l1 wgrad 172 vs 197 TFLOP/s at K = 100,
+    // profiles/r2_kernel_bench_f32_tn64x256_sweep.jsonl): sweep-only
+    case 7: return launch_tn_f32_cfg<64, 256, 32, 2, 2, 1, false>(p, va, vb, grid, s);
     default: return false;
   }
 }
