@@ -40,10 +40,12 @@ sys.path.insert(0, ROOT)
 # The reference publishes no numbers. Its execution model — clients trained one
 # after another per GPU in eager PyTorch fp32, fp64 server average — re-created with stock
 # PyTorch-ROCm (bench/torch_reference_baseline.py) and measured on one MI355X, in rounds/s for
-# the default (headline) config and the reference's own DenseNet-40 config;
-# profiles/r2_torch_eager_reference_baseline_{resnet18,densenet40}.json.
+# the default (headline) config, the reference's own DenseNet-40 config and the FedOBD
+# Transformer-base config; profiles/r2_torch_eager_reference_baseline_*.json.
 # With N GPUs the reference would deal the clients over N processes: N x this rate at best.
-REFERENCE_STYLE_ROUNDS_PER_S = {"fedavg_resnet18": 0.05827, "fedavg_densenet40": 0.03161}
+REFERENCE_STYLE_ROUNDS_PER_S = {"fedavg_resnet18": 0.05827, "fedavg_densenet40": 0.03161,
+                                # training only (no block dropout / NNADQ): a lower bound on its time
+                                "fedobd_transformer": 0.01587}
 
 
 def vs_baseline(args, value: float, n_gpus: int, fp32: bool):
@@ -236,8 +238,14 @@ def workload_config(args, rounds: int) -> dict:
               "save_dir": os.path.join("/tmp", f"dls_bench_{os.getpid()}")}
 
     def shard_samples(sess):
+        # samples trained per round: every client's shard × local epochs, scaled by the share of
+        # clients a round selects (FedOBD stage 1: random_client_number of worker_number)
         name = sess.dc.spec.name
-        return sum(p.dataset_size(name) for p in sess.practitioners.values()) * sess.config.epoch
+        total = sum(p.dataset_size(name) for p in sess.practitioners.values()) * sess.config.epoch
+        n = sess.config.algorithm_kwargs.get("random_client_number")
+        if n is not None and int(n) < sess.config.worker_number:
+            total = total * int(n) / sess.config.worker_number
+        return total
 
     if args.workload == "fedavg_mlp_mnist":
         # BASELINE.json config 1: the plumbing check (runs on the CPU executor as well)

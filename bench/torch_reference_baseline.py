@@ -99,9 +99,37 @@ class DenseNet40(nn.Module):
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
+class TransformerClassifier(nn.Module):
+    """Transformer-base text classifier as models/zoo.py TransformerClassificationModel: token
+    embedding x sqrt(d) + sinusoidal PE, 6 post-norm nn.TransformerEncoderLayer (d 512, 8 heads,
+    FFN 2048, ReLU, dropout 0.1), masked mean over the sequence, linear head (AG-News: 4 classes)."""
+
+    def __init__(self, vocab=30000, d=512, heads=8, layers=6, ffn=2048, classes=4, max_len=128) -> None:
+        super().__init__()
+        self.d = d
+        self.emb = nn.Embedding(vocab, d, padding_idx=0)
+        pos = torch.arange(max_len).unsqueeze(1)
+        div = torch.exp(torch.arange(0, d, 2) * (-torch.log(torch.tensor(10000.0)) / d))
+        pe = torch.zeros(max_len, d)
+        pe[:, 0::2] = torch.sin(pos * div)
+        pe[:, 1::2] = torch.cos(pos * div)
+        self.register_buffer("pe", pe)
+        layer = nn.TransformerEncoderLayer(d, heads, ffn, dropout=0.1, batch_first=True)
+        self.encoder = nn.TransformerEncoder(layer, layers, enable_nested_tensor=False)
+        self.fc = nn.Linear(d, classes)
+
+    def forward(self, tokens):
+        pad = tokens == 0
+        x = self.emb(tokens) * self.d ** 0.5 + self.pe[: tokens.shape[1]]
+        x = self.encoder(x, src_key_padding_mask=pad)
+        keep = (~pad).unsqueeze(-1).float()
+        return self.fc((x * keep).sum(1) / keep.sum(1).clamp(min=1))
+
+
 def train_client(model, global_state, images, labels, args):
     model.load_state_dict(global_state)
-    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr if args.lr else (0.01 if args.model == "transformer" else 0.1),
+                          momentum=0.9)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=args.epoch)
     n = images.shape[0]
     for _ in range(args.epoch):
@@ -123,10 +151,10 @@ def main() -> None:
     ap.add_argument("--warmup-clients", type=int, default=1)
     ap.add_argument("--epoch", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=0.0, help="0: the config's (0.1 CNNs, 0.01 FedOBD Transformer)")
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--channels-last", action="store_true")
-    ap.add_argument("--model", default="ResNet18", choices=["ResNet18", "densenet40"])
+    ap.add_argument("--model", default="ResNet18", choices=["ResNet18", "densenet40", "transformer"])
     ap.add_argument("--no-benchmark", action="store_true", help="torch.backends.cudnn.benchmark off")
     args = ap.parse_args()
 
@@ -143,13 +171,24 @@ def main() -> None:
 
     threading.Thread(target=beat, daemon=True).start()
     dev = torch.device("cuda:0")
-    per_client = args.train_size // args.clients
     g = torch.Generator(device="cpu").manual_seed(0)
-    images = torch.randn(per_client, 3, 32, 32, generator=g).to(dev)
-    labels = torch.randint(0, 10, (per_client,), generator=g).to(dev)
-    fmt = torch.channels_last if args.channels_last else torch.contiguous_format
-    images = images.contiguous(memory_format=fmt)
-    model = (ResNet18() if args.model == "ResNet18" else DenseNet40()).to(dev).to(memory_format=fmt)
+    if args.model == "transformer":
+        # BASELINE config 3: AG-News-shaped (120k samples over 100 clients, L 128, lengths in
+        # [L/4, L], token 0 = padding), 50 clients trained per FedOBD round
+        per_client = 120000 // 100
+        lengths = torch.randint(32, 129, (per_client,), generator=g)
+        images = torch.randint(1, 30000, (per_client, 128), generator=g)
+        images[torch.arange(128).view(1, -1) >= lengths.view(-1, 1)] = 0
+        images = images.to(dev)
+        labels = torch.randint(0, 4, (per_client,), generator=g).to(dev)
+        model = TransformerClassifier().to(dev)
+    else:
+        per_client = args.train_size // args.clients
+        images = torch.randn(per_client, 3, 32, 32, generator=g).to(dev)
+        labels = torch.randint(0, 10, (per_client,), generator=g).to(dev)
+        fmt = torch.channels_last if args.channels_last else torch.contiguous_format
+        images = images.contiguous(memory_format=fmt)
+        model = (ResNet18() if args.model == "ResNet18" else DenseNet40()).to(dev).to(memory_format=fmt)
     global_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
     n_params = sum(p.numel() for p in model.parameters())
 
@@ -172,10 +211,14 @@ def main() -> None:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     s_per_client = dt / args.clients_timed
-    s_round = s_per_client * args.clients
+    round_clients = 50 if args.model == "transformer" else args.clients  # FedOBD: 50 of 100 per round
+    s_round = s_per_client * round_clients
     print(json.dumps({
-        "metric": f"FL rounds/sec (FedAvg, {args.clients} clients, {'ResNet-18' if args.model == 'ResNet18' else 'DenseNet-40'}, "
-                  "CIFAR-10-shaped) — reference-style PyTorch eager",
+        "metric": ("FL rounds/sec (FedOBD stage 1 training, 100 clients / 50 per round, Transformer-base, "
+                   "AG-News-shaped) — reference-style PyTorch eager" if args.model == "transformer" else
+                   f"FL rounds/sec (FedAvg, {args.clients} clients, "
+                   f"{'ResNet-18' if args.model == 'ResNet18' else 'DenseNet-40'}, CIFAR-10-shaped) — "
+                   "reference-style PyTorch eager"),
         "value": 1.0 / s_round, "unit": "rounds/s", "s_per_round": s_round, "s_per_client": s_per_client,
         "samples_per_s": per_client * args.epoch / s_per_client, "clients_timed": args.clients_timed,
         "dtype": "fp32", "params": n_params, "channels_last": args.channels_last,
