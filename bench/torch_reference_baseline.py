@@ -99,6 +99,82 @@ class DenseNet40(nn.Module):
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
+class Bottleneck(nn.Module):
+    def __init__(self, cin: int, width: int, stride: int) -> None:
+        super().__init__()
+        cout = width * 4
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return F.relu(out + (x if self.down is None else self.down(x)))
+
+
+class ResNet50(nn.Module):
+    """ImageNet ResNet-50 (25,557,032 parameters, as models/zoo.py pins)."""
+
+    def __init__(self, classes: int = 1000) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        blocks, cin = [], 64
+        for width, n, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+            for i in range(n):
+                blocks.append(Bottleneck(cin, width, stride if i == 0 else 1))
+                cin = width * 4
+        self.layers = nn.Sequential(*blocks)
+        self.fc = nn.Linear(2048, classes)
+
+    def forward(self, x):
+        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x))), 3, 2, 1)
+        x = self.layers(x)
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def signsgd_step_time(args, dev):
+    """sign-SGD (BASELINE config 4) in the reference's style: every step each of the 128 clients
+    computes its gradient on its next batch of 128 images in turn (sequential eager fp32), the
+    signs are summed into a majority vote and the shared model takes one step. Times
+    `--clients-timed` client gradients of one step, scaled to 128 clients x 8 steps per round."""
+    model = ResNet50().to(dev)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    images = torch.randn(args.batch, 3, 224, 224, generator=g).to(dev)
+    labels = torch.randint(0, 1000, (args.batch,), generator=g).to(dev)
+    params = [p for p in model.parameters()]
+    vote = [torch.zeros_like(p) for p in params]
+
+    def client_grad():
+        model.zero_grad(set_to_none=True)
+        F.cross_entropy(model(images), labels).backward()
+        for v, p in zip(vote, params):
+            v.add_(torch.sign(p.grad))
+
+    for _ in range(args.warmup_clients):
+        client_grad()
+        print("[baseline] warmup client done", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for c in range(args.clients_timed):
+        client_grad()
+        print(f"[baseline] client {c + 1}/{args.clients_timed} {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.clients_timed
+    with torch.no_grad():
+        for v, p in zip(vote, params):
+            p.add_(torch.sign(v), alpha=-0.001)
+    return dt, sum(p.numel() for p in params)
+
+
 class TransformerClassifier(nn.Module):
     """Transformer-base text classifier as models/zoo.py TransformerClassificationModel: token
     embedding x sqrt(d) + sinusoidal PE, 6 post-norm nn.TransformerEncoderLayer (d 512, 8 heads,
@@ -154,14 +230,14 @@ def main() -> None:
     ap.add_argument("--lr", type=float, default=0.0, help="0: the config's (0.1 CNNs, 0.01 FedOBD Transformer)")
     ap.add_argument("--train-size", type=int, default=50000)
     ap.add_argument("--channels-last", action="store_true")
-    ap.add_argument("--model", default="ResNet18", choices=["ResNet18", "densenet40", "transformer"])
+    ap.add_argument("--model", default="ResNet18", choices=["ResNet18", "densenet40", "transformer", "resnet50"])
     ap.add_argument("--no-benchmark", action="store_true", help="torch.backends.cudnn.benchmark off")
     args = ap.parse_args()
 
     # MIOpen auto-tuning per shape: on for ResNet-18 (11 conv shapes); DenseNet-40 has ~80 distinct
     # conv shapes (every layer a new input width, plus the ragged last batch) and its exhaustive
     # search alone ran > 8 minutes, so it runs with PyTorch's default (off)
-    torch.backends.cudnn.benchmark = args.model == "ResNet18" and not args.no_benchmark
+    torch.backends.cudnn.benchmark = args.model in ("ResNet18", "resnet50") and not args.no_benchmark
     t_start = time.perf_counter()
 
     def beat():  # keeps a long MIOpen kernel search visibly alive
@@ -171,6 +247,19 @@ def main() -> None:
 
     threading.Thread(target=beat, daemon=True).start()
     dev = torch.device("cuda:0")
+    if args.model == "resnet50":
+        args.batch = 128
+        per_client_step, n_params = signsgd_step_time(args, dev)
+        s_round = per_client_step * 128 * 8  # 128 clients, 8 vote steps per round (10 % shards)
+        print(json.dumps({
+            "metric": "FL rounds/sec (sign-SGD, 128 clients, ResNet-50, ImageNet-shaped) — reference-style PyTorch eager",
+            "value": 1.0 / s_round, "unit": "rounds/s", "s_per_round": s_round, "s_per_client_step": per_client_step,
+            "samples_per_s": args.batch / per_client_step, "clients_timed": args.clients_timed, "dtype": "fp32",
+            "params": n_params, "miopen_benchmark": torch.backends.cudnn.benchmark,
+            "config": {"model": "resnet50", "clients": 128, "steps_per_round": 8, "per_client_batch": 128},
+            "torch": torch.__version__, "device": torch.cuda.get_device_name(0),
+        }), flush=True)
+        return
     g = torch.Generator(device="cpu").manual_seed(0)
     if args.model == "transformer":
         # BASELINE config 3: AG-News-shaped (120k samples over 100 clients, L 128, lengths in
