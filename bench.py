@@ -40,12 +40,14 @@ sys.path.insert(0, ROOT)
 # The reference publishes no numbers. Its execution model — clients trained one
 # after another per GPU in eager PyTorch fp32, fp64 server average — re-created with stock
 # PyTorch-ROCm (bench/torch_reference_baseline.py) and measured on one MI355X, in rounds/s for
-# the default (headline) config, the reference's own DenseNet-40 config and the FedOBD
-# Transformer-base config; profiles/r2_torch_eager_reference_baseline_*.json.
+# the default (headline) config, the reference's own DenseNet-40 config, the FedOBD
+# Transformer-base config and sign-SGD ResNet-50; profiles/r2_torch_eager_reference_baseline_*.json.
 # With N GPUs the reference would deal the clients over N processes: N x this rate at best.
 REFERENCE_STYLE_ROUNDS_PER_S = {"fedavg_resnet18": 0.05827, "fedavg_densenet40": 0.03161,
                                 # training only (no block dropout / NNADQ): a lower bound on its time
-                                "fedobd_transformer": 0.01587}
+                                "fedobd_transformer": 0.01587,
+                                # 128 sequential client gradients per step, 8 vote steps per round
+                                "signsgd_resnet50": 0.01621}
 
 
 def vs_baseline(args, value: float, n_gpus: int, fp32: bool):
