@@ -844,8 +844,8 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     // waves per SIMD, v9: l1 dgrad 233-236 vs 205-222, strided-dgrad classes onto 64 channels
     // 157-179 vs 132-151, the 8-channel stem 118 vs 98-108; fwd equal)
     variant = p.N <= 64 ? 9 : 1;
-    // few clients per launch (8 ranks x 3 sub-cohort streams: K = 4-5) or short reductions:
-    // the 20-KB 64x64 tile. Measured (kernel_bench --f32 --sweep, K = 4 / 13): l4 / l4a fwd
+    // opt-in (DLS_F32_SMALLK bit 0, see small_k_rules): few clients per launch (K = 4-5) or short
+    // reductions → the 20-KB 64x64 tile. In isolation (kernel_bench --f32 --sweep, K = 4 / 13): l4 / l4a fwd
     // and dgrad at K = 4 (<= 128 big tiles) 142-154 vs 95-105 TFLOP/s; 1x1 shortcut convs
     // (R <= 128) 63-117 vs 41-107; stride-2 dgrad parity classes onto 64 channels 114-138 vs
     // 91-125. At K >= 13 the big tiles win the 3x3 layers (l4 269 vs 198).
