@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--skip-misc", action="store_true", help="conv layers only (no BN/SGD)")
     ap.add_argument("--gl", action="store_true", help="A/B the LDS-DMA large-tile kernel (conv_gl) vs conv_nt")
     ap.add_argument("--f32", action="store_true", help="fp32 tensors: the split-bf16 kernels (csrc/conv_f32.hip)")
+    ap.add_argument("--planes", action="store_true",
+                    help="fp32: A/B the pre-split-operand LDS-DMA kernels (csrc/conv_pl.hip, every variant) "
+                         "against the register-staged split kernels with pre-split weights")
     args = ap.parse_args()
     from distributed_learning_simulator_amd.ops import build
 
@@ -115,6 +118,31 @@ def main():
             for key in ab:
                 row[f"{key}_fwd_tflops"] = round(max(a for a, _ in ab[key]), 1)
                 row[f"{key}_dgrad_tflops"] = round(max(b for _, b in ab[key]), 1)
+        if args.planes and Ci % 32 == 0:
+            n = Co * k * k * Ci
+            wpl = torch.empty((K, 2, n), dtype=torch.bfloat16, device=dev)
+            hip.split_rows(w.reshape(K, n).contiguous(), wpl)
+            ws = wpl[:, 0].unflatten(1, (Co, k, k, Ci))
+            xp, dyp = hip.split_planes(x), hip.split_planes(dy)
+            base_f = flops / timeit(lambda: hip.conv_fwd(x, w, s, pad, w_split=ws), args.iters) / 1e12
+            base_d = flops / timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad, w_split=ws), args.iters) / 1e12
+            pv = {}
+            for v in [-1] + list(range(hip._C.conv_nt_pl_num_variants())):
+                hip._C.conv_nt_pl_set_variant(v)
+                tf_v = timeit(lambda: hip.conv_fwd(x, w, s, pad, w_split=ws, x_planes=xp), args.iters)
+                td_v = timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad, w_split=ws, dy_planes=dyp), args.iters)
+                pv[v] = (round(flops / tf_v / 1e12, 1), round(flops / td_v / 1e12, 1))
+            hip._C.conv_nt_pl_set_variant(-1)
+            row["split_w_fwd_dgrad"] = (round(base_f, 1), round(base_d, 1))
+            row["planes_fwd_dgrad"] = pv
+            pw = {}
+            for v in [-1] + list(range(hip._C.conv_tn_pl_num_variants())):
+                hip._C.conv_tn_pl_set_variant(v)
+                tw_v = timeit(lambda: hip.conv_wgrad(dy, x, gw, s, pad, dy_planes=dyp, x_planes=xp), args.iters)
+                pw[v] = round(flops / tw_v / 1e12, 1)
+            hip._C.conv_tn_pl_set_variant(-1)
+            row["planes_wgrad"] = pw
+            del xp, dyp, wpl
         if args.sweep:
             # every NT tile configuration on this shape (fwd / dgrad TFLOP/s per variant id)
             sw = {}

@@ -21,8 +21,9 @@ PYBIND11_MODULE(_dls_hip, m) {
                       int C, int OH, int OW, int KH, int KW, int stride, int pad, int dil, int M, int N, int R, int rep,
                       int relu, int K, int b_kmajor, int variant, ptr acc, ptr gate, int f32, ptr s, int ldx, int ldy,
                       ptr stats, ptr stats_valid, ptr drop_seeds, float drop_p, float out_scale, ptr wsplit,
-                      long ws_cs, long ws_plane) {
+                      long ws_cs, long ws_plane, long x_lo) {
     ConvNTParams p{};
+    p.x_lo = x_lo;
     p.wsplit = P<const bf16_t>(wsplit);
     p.ws_cs = ws_cs;
     p.ws_plane = ws_plane;
@@ -48,9 +49,9 @@ PYBIND11_MODULE(_dls_hip, m) {
   });
   m.def("conv_dgrad", [](ptr dy, ptr w, ptr dx, ptr acc, long w_cs, int K, int rep, int B, int OH, int OW, int Co, int H,
                          int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, ptr s, int ld_dy,
-                         long dy_cs, ptr wsplit, long ws_cs, long ws_plane) {
+                         long dy_cs, ptr wsplit, long ws_cs, long ws_plane, long x_lo) {
     conv_dgrad(P<const bf16_t>(dy), P<const bf16_t>(w), P<bf16_t>(dx), P<const bf16_t>(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW,
-               stride, pad, variant, f32, S(s), ld_dy, dy_cs, P<const bf16_t>(wsplit), ws_cs, ws_plane);
+               stride, pad, variant, f32, S(s), ld_dy, dy_cs, P<const bf16_t>(wsplit), ws_cs, ws_plane, x_lo);
   });
   m.def("conv_gl_wanted", &conv_gl_wanted);
   m.def("conv_gl_fwd", [](ptr x, ptr w, ptr y, ptr bias, long x_cs, long y_cs, long w_cs, long b_cs, int K, int rep,
@@ -71,8 +72,11 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt_default_variant", &conv_nt_default_variant);
   m.def("conv_tn", [](ptr dy, ptr x, ptr dw, long dy_cs, long x_cs, long dw_cs, int B, int H, int W, int C, int OH,
                       int OW, int KH, int KW, int stride, int pad, int M, int Co, int R, int K, int variant, int f32,
-                      ptr s, int ldy, int ldx) {
+                      ptr s, int ldy, int ldx, ptr part, long dy_lo, long x_lo) {
     ConvTNParams p{};
+    p.part = P<float>(part);
+    p.dy_lo = dy_lo;
+    p.x_lo = x_lo;
     p.f32 = f32;
     p.ldy = ldy;
     p.ldx = ldx;
@@ -85,9 +89,14 @@ PYBIND11_MODULE(_dls_hip, m) {
     conv_tn(p, K, variant, S(s));
   });
   m.def("conv_tn_splitk", &conv_tn_splitk, py::arg("K"), py::arg("Co"), py::arg("R"), py::arg("M"), py::arg("C"),
-        py::arg("variant"), py::arg("f32"), py::arg("ldy") = 0, py::arg("ldx") = 0);
+        py::arg("variant"), py::arg("f32"), py::arg("ldy") = 0, py::arg("ldx") = 0, py::arg("planes") = 0);
+  m.def("conv_tn_pl_num_variants", &conv_tn_pl_num_variants);
+  m.def("conv_tn_pl_set_variant", &conv_tn_pl_set_variant);
+  m.def("conv_tn_pl_variant", &conv_tn_pl_variant);
   m.def("conv_tn_num_variants", &conv_tn_num_variants);
   m.def("conv_nt_f32_num_variants", &conv_nt_f32_num_variants);
+  m.def("conv_nt_pl_num_variants", &conv_nt_pl_num_variants);
+  m.def("conv_nt_pl_set_variant", &conv_nt_pl_set_variant);
   m.def("conv_tn_f32_num_variants", &conv_tn_f32_num_variants);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);

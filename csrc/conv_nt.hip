@@ -418,8 +418,9 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
 
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
-                int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane) {
+                int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane, long x_lo) {
   ConvNTParams p{};
+  p.x_lo = x_lo;
   p.wsplit = wsplit;  // (fp32 kernels: pre-split weight planes, read k-major in place like w)
   p.ws_cs = ws_cs;
   p.ws_plane = ws_plane;

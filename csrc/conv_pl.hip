@@ -1,0 +1,646 @@
+// fp32-accurate implicit-GEMM convolution / linear on PRE-SPLIT operands for gfx950 (MI355X).
+//
+// Same arithmetic as conv_f32.hip (split bf16 "bf16x3": a·b ≈ ah·bh + al·bh + ah·bl on
+// v_mfma_f32_32x32x16_bf16, fp32 accumulate; products in the same order, so the result is
+// bit-identical for the same hi / lo values), but both operands arrive already split into two
+// bf16 planes (hi = bf16(x), lo = bf16(x − hi), RNE):
+//   A  — the activation (or dY) planes written by the producing BatchNorm (bn_fwd / bn_bwd
+//        `planes` outputs): one extra 4-B/element write there replaces the per-workgroup split
+//        of every tile that reads the element (3x3 im2col reads each element up to 9× per N tile);
+//   B  — the weight planes the SGD step keeps current (sgd_step `split`).
+// The loaders are then pure data movement: every 16-B piece goes HBM/L2 → LDS by LDS-DMA
+// (`buffer_load_dwordx4 … lds`, per-lane source address, lane-linear LDS destination), so the
+// main loop issues no split VALU, no ds_write and holds no staging registers; the DMA of
+// stage k+1 (k+2) is in flight under the MFMAs of stage k (guide §5 "Pipelining across
+// barriers": counted vmcnt + raw s_barrier, all LDS in ONE __shared__ array).
+//
+// Buffer resources bound each client's operand window: an out-of-window lane offset (image
+// padding taps, M / N tails) makes the DMA write zeros, so no lane is ever masked (a masked
+// lane would leave a hole in the lane-linear image).
+//
+// LDS images (per stage): A hi / lo [BM][32] and B hi / lo [BN][32] (row-major: 64-B rows,
+// 16-B chunk c stored at c ^ ((row >> 2) & 3) → conflict-free ds_read_b128 fragment reads) or,
+// for a k-major B (dgrad reading the forward weight in place), B hi / lo [32][BN] read by
+// ds_read_b64_tr_b16 with the 32-element segment XOR-swizzled by k-row.
+//
+// Restrictions (the host dispatcher falls back to conv_f32.hip otherwise): C % 32 == 0 (one K
+// tile never straddles a tap), pixel stride % 8 == 0, N % 8 == 0, per-client windows < 2 GiB.
+#include "dls.h"
+#include "epilogue_f32.h"
+#include "gemm_common.h"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int PK = 32;  // K tile: 32 bf16 per plane row (64 B)
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
+}
+
+// s_waitcnt with only vmcnt = N (expcnt / lgkmcnt left at their maxima), gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BM, int BN, int WM, int WN, bool BKM, int NST, int MINW, bool ILV, int PKT>
+__global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  static_assert(PKT == 16 || PKT == 32, "K tile");
+  constexpr int A_PL = BM * PKT * 2, B_PL = BN * PKT * 2;  // bytes per plane image
+  constexpr int STAGE = 2 * (A_PL + B_PL);
+  // row-major images: PKT·2-byte rows, CR 16-B chunks per row, RI rows per 1-KiB DMA
+  // instruction, RB rows per 256-B bank row; chunk c of row r stored at c ^ ((r / RB) % CR)
+  constexpr int CR = PKT / 8, RI = 64 / CR, RB = 256 / (PKT * 2);
+  constexpr int AI = BM / RI / NW;  // DMA instructions per wave per plane (1 KiB each)
+  constexpr int BI = BN * PKT / 512 / NW;
+  static_assert(AI * RI * NW == BM && BI * 512 * NW == BN * PKT, "DMA split");
+  constexpr int G = 2 * (AI + BI);  // DMA instructions per wave per stage
+  constexpr int SW = TN * 32 + 4;
+  constexpr int EPI = NW * 32 * SW * 4;
+  constexpr int SMEM = NST * STAGE > EPI ? NST * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tilesM = (p.M + BM - 1) / BM, tilesN = (p.N + BN - 1) / BN;
+  const int per_client = tilesM * tilesN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int client = bid / per_client;
+  const int t = bid - client * per_client;
+  const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BN;
+
+  // ---- operand windows (hi plane .. end of lo plane) as buffer resources
+  const long a_img = (long)p.B * p.H * p.W * p.ldx;  // elements of one plane of a client's image
+  const auto ar = make_rsrc(p.x + (long)client * p.x_cs, (uint32_t)((p.x_lo + a_img) * 2));
+  const uint32_t a_lo = (uint32_t)(p.x_lo * 2);
+  const long w_ext = BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R;
+  const auto br = make_rsrc(p.wsplit + (long)client * p.ws_cs, (uint32_t)((p.ws_plane + w_ext) * 2));
+  const uint32_t b_lo = (uint32_t)(p.ws_plane * 2);
+
+  // ---- A loader: instruction i of wave w fills tile rows (i·NW + w)·RI + lane / CR, physical
+  // chunk lane % CR, fetching logical chunk lc = (lane % CR) ^ ((row / RB) % CR) = … ^ ((lane >> 4) % CR)
+  const int lc = (lane % CR) ^ ((lane >> 4) % CR);
+  int a_off[AI], a_ih[AI], a_iw[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + (i * NW + wid) * RI + lane / CR;
+    if (m < p.M) {
+      const uint32_t b = fdiv((uint32_t)m, p.fd_ohw);
+      const uint32_t rem = (uint32_t)m - b * (uint32_t)(p.OH * p.OW);
+      const uint32_t oh = fdiv(rem, p.fd_ow);
+      const uint32_t ow = rem - oh * (uint32_t)p.OW;
+      a_ih[i] = (int)oh * p.stride - p.pad;
+      a_iw[i] = (int)ow * p.stride - p.pad_w;
+      a_off[i] = (((int)b * p.H + a_ih[i]) * p.W + a_iw[i]) * p.ldx + lc * 8;
+    } else {
+      a_ih[i] = -(1 << 28);  // never inside the image
+      a_iw[i] = 0;
+      a_off[i] = 0;
+    }
+  }
+  // ---- B loader
+  // row-major [N][R]: rows (i·NW + w)·16 + (lane >> 2), same chunk swizzle as A
+  // k-major [k][N] (dgrad, the forward weight W[co][kh][kw][ci] read in place): instruction i
+  // covers k-rows (i·NW + w)·RPI + lane / CPR, physical chunk lane % CPR
+  constexpr int CPR = BN / 8, RPI = BKM ? 64 / CPR : RI;
+  constexpr int SD = (128 / BN) > 1 ? 128 / BN : 1, SS = (BN / 32) < 4 ? BN / 32 : 4;  // k-major swizzle
+  int b_off[BI];
+  const long wkhwn = (long)p.wKH * p.wKW * p.N;  // element distance of one input channel (k-major)
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    if constexpr (!BKM) {
+      const int n = n0 + (i * NW + wid) * RI + lane / CR;
+      b_off[i] = n < p.N ? n * p.R + lc * 8 : -1;
+    } else {
+      const int kr = (i * NW + wid) * RPI + lane / CPR;
+      const int f = SS > 1 ? (kr / SD) & (SS - 1) : 0;
+      const int n = n0 + ((lane % CPR) ^ (f << 2)) * 8;
+      b_off[i] = n < p.N ? (int)(kr * wkhwn) + n : -1;
+    }
+  }
+
+  // K-tile walk: taps (kh, kw) × 32-channel chunks kc of the GEMM's A image (C % 32 == 0).
+  // prep() fixes the scalar part of the next stage's source offsets and advances the walk;
+  // piece(n, buf) issues that stage's n-th DMA (n < G: A hi / lo per A instruction, then B hi /
+  // lo per B instruction). A stage past the last K tile is issued with every lane out of window
+  // (zeros into a buffer nobody reads again), so the loop needs no branch around its DMAs.
+  int kc = 0, kh = 0, kw = 0, k_next = 0;
+  int s_toff = 0, s_boff = 0, s_kh = 0, s_kw = 0;
+  bool s_live = false;
+  auto prep = [&](bool live) {
+    s_live = live;
+    s_kh = kh;
+    s_kw = kw;
+    s_toff = (kh * p.W + kw) * p.ldx + kc;
+    if constexpr (!BKM) {
+      s_boff = k_next;
+    } else {
+      const int khh = p.kh_off - p.kh_step * kh, kww = p.kw_off - p.kw_step * kw;
+      s_boff = (int)(kc * wkhwn) + (khh * p.wKW + kww) * p.N;
+    }
+    k_next += PKT;
+    kc += PKT;
+    if (kc == p.C) {
+      kc = 0;
+      if (++kw == p.KW) {
+        kw = 0;
+        ++kh;
+      }
+    }
+  };
+  auto piece = [&](int n, int buf) {
+    unsigned char* As = smem + buf * STAGE;
+    unsigned char* Bs = As + 2 * A_PL;
+    if (n < 2 * AI) {
+      const int i = n >> 1;
+      const bool ok = s_live && (unsigned)(a_ih[i] + s_kh) < (unsigned)p.H && (unsigned)(a_iw[i] + s_kw) < (unsigned)p.W;
+      const uint32_t off = (uint32_t)(a_off[i] + s_toff) * 2u + ((n & 1) ? a_lo : 0u);
+      dma16(ar, As + (n & 1) * A_PL + (i * NW + wid) * 1024, ok ? off : OOB_OFF);
+    } else {
+      const int i = (n - 2 * AI) >> 1;
+      const bool ok = s_live && b_off[i] >= 0;
+      const uint32_t off = (uint32_t)(b_off[i] + s_boff) * 2u + ((n & 1) ? b_lo : 0u);
+      dma16(br, Bs + (n & 1) * B_PL + (i * NW + wid) * 1024, ok ? off : OOB_OFF);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const int wm0 = (wid / WN) * (TM * 32), wn0 = (wid % WN) * (TN * 32);
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
+  const int rsw = ((lane & 31) / RB) % CR;  // row-major image key of fragment row (lane & 31)
+  constexpr int KS = PKT / 16, NTRI = KS * TM * TN;  // MFMA triples per K tile
+  // compute(buf, nb): the MFMAs of stage buf; with ILV the next stage's G DMAs (into buffer nb)
+  // are spread over the MFMA triples (piece n after triple n·NTRI/G) instead of issued as one
+  // burst after the barrier, so the DMA issue overlaps the matrix pipe
+  auto compute = [&](int buf, int nb) {
+    const unsigned char* As = smem + buf * STAGE;
+    const unsigned char* Bs = As + 2 * A_PL;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int ch = ((ks * 2 + h) ^ rsw) * 16;
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const unsigned char* a = As + (wm0 + i * 32 + (lane & 31)) * (PKT * 2) + ch;
+        ah[i] = *reinterpret_cast<const bf16x8*>(a);
+        al[i] = *reinterpret_cast<const bf16x8*>(a + A_PL);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (!BKM) {
+          const unsigned char* b = Bs + (wn0 + j * 32 + (lane & 31)) * (PKT * 2) + ch;
+          bh[j] = *reinterpret_cast<const bf16x8*>(b);
+          bl[j] = *reinterpret_cast<const bf16x8*>(b + B_PL);
+        } else {
+          const int kr = ks * 16 + 8 * h + q;  // (kr + 4 has the same swizzle key)
+          const int f = SS > 1 ? (kr / SD) & (SS - 1) : 0;
+          const int col = (wn0 + j * 32 + 16 * (g & 1) + 4 * pp) ^ (f << 5);
+          const bf16_t* b0 = reinterpret_cast<const bf16_t*>(Bs) + kr * BN + col;
+          bh[j] = tr_frag(b0, b0 + 4 * BN);
+          bl[j] = tr_frag(b0 + B_PL / 2, b0 + B_PL / 2 + 4 * BN);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          if constexpr (ILV) {
+            const int tri = (ks * TM + i) * TN + j;
+#pragma unroll
+            for (int n = 0; n < G; ++n)
+              if ((n * NTRI) / G == tri) {
+                piece(n, nb);
+                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // the triple's MFMAs ...
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // ... then this DMA
+              }
+          }
+        }
+    }
+  };
+
+  // ---- main loop: NST-stage LDS ring. Stage kt+NST-1 is issued after the barrier that retires
+  // every wave's reads of its buffer (compute(kt-1)); stage kt is waited for by a counted vmcnt
+  // that leaves the younger stage in flight (NST = 3)
+  const int nk = p.R / PKT;
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st) {
+    prep(st < nk);
+#pragma unroll
+    for (int n = 0; n < G; ++n) piece(n, st);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vm<G*(NST - 2)>();
+    __builtin_amdgcn_s_barrier();
+    const int nb = (kt + NST - 1) % NST;
+    prep(kt + NST - 1 < nk);
+    if constexpr (!ILV) {
+#pragma unroll
+      for (int n = 0; n < G; ++n) piece(n, nb);
+    }
+    compute(kt % NST, nb);
+  }
+  wait_vm<0>();
+
+  nt_f32_epilogue<TM, TN, NW>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
+}
+
+template <int BM, int BN, int WM, int WN, int NST, bool ILV = false, int PKT = 32, int MINW = 1>
+void launch_pl(const ConvNTParams& p, int K, bool bkm, hipStream_t s) {
+  const int grid = K * cdiv(p.M, BM) * cdiv(p.N, BN);
+  if (bkm)
+    hipLaunchKernelGGL((conv_nt_pl_kernel<BM, BN, WM, WN, true, NST, MINW, ILV, PKT>), dim3(grid),
+                       dim3(WM * WN * 64), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_nt_pl_kernel<BM, BN, WM, WN, false, NST, MINW, ILV, PKT>), dim3(grid),
+                       dim3(WM * WN * 64), 0, s, p);
+}
+
+}  // namespace
+
+static int g_pl_variant = -1;
+int conv_nt_pl_variant() { return g_pl_variant; }
+void conv_nt_pl_set_variant(int v) { g_pl_variant = v; }
+
+// variant ids are stable (bench/kernel_bench.py --planes sweeps them)
+int conv_nt_pl_num_variants() { return 8; }
+
+bool conv_nt_pl_supported(const ConvNTParams& p) {
+  return p.x_lo != 0 && p.wsplit != nullptr && p.rep == 1 && p.dil == 1 && p.C % PK == 0 && p.ldx % 8 == 0 &&
+         p.N % 8 == 0 && (p.R == p.KH * p.KW * p.C || p.R == 0);
+}
+
+int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
+  (void)K;
+  if (p.N <= 64) return 2;  // 256x64
+  return 0;                 // 256x128
+}
+
+bool conv_nt_pl(const ConvNTParams& p, int K, int variant, hipStream_t s) {
+  if (!conv_nt_pl_supported(p)) return false;
+  const long ab = (p.x_lo + (long)p.B * p.H * p.W * p.ldx) * 2;
+  const long wb = (p.ws_plane + (p.b_kmajor ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R)) * 2;
+  if (ab >= (long)OOB_OFF || wb >= (long)OOB_OFF) return false;
+  if (variant < 0) variant = conv_nt_pl_default_variant(p, K);
+  const bool bkm = p.b_kmajor != 0;
+  switch (variant) {
+    case 0: launch_pl<256, 128, 4, 2, 2>(p, K, bkm, s); break;  // 96 KB, 8 waves
+    case 1: launch_pl<128, 128, 2, 2, 2>(p, K, bkm, s); break;  // 64 KB, 2 blocks/CU
+    case 2: launch_pl<256, 64, 4, 1, 2>(p, K, bkm, s); break;   // 80 KB, 2 blocks/CU
+    case 3: launch_pl<256, 256, 2, 4, 2>(p, K, bkm, s); break;  // 128 KB, 8 waves, 128x64 wave tiles
+    // 3 stages, the next-but-one stage's DMAs interleaved with the MFMAs (ILV)
+    case 4: launch_pl<256, 128, 4, 2, 3, true>(p, K, bkm, s); break;  // 144 KB
+    case 5: launch_pl<256, 256, 2, 4, 4, false, 16>(p, K, bkm, s); break;  // 128 KB: BK 16, 4 stages
+    case 6: launch_pl<256, 256, 2, 4, 3, false, 16>(p, K, bkm, s); break;  // 96 KB: BK 16, 3 stages
+    case 7: launch_pl<256, 128, 4, 2, 3>(p, K, bkm, s); break;  // 144 KB, 3 stages, DMA burst
+    default: return false;
+  }
+  return true;
+}
+
+// ============================================================================ TN (weight gradient)
+//   dW[co][r] = Σ_m dY[m][co] · X̃[m][r]   (X̃ = im2col of the layer input, r = (kh, kw, c))
+// Both operands are k-major (k = m, the pixel reduction): LDS images A hi / lo [32][BMc] and
+// B hi / lo [32][BNr], 32-element segments XOR-swizzled by k-row, fragments by
+// ds_read_b64_tr_b16. Each DMA lane keeps one fixed 8-column chunk for the whole kernel (its
+// (kh, kw, c) for B), so only the pixel walk m → (b, oh, ow) advances, 32 rows per K tile,
+// with carries instead of divisions. Split-K over pixels writes per-split slabs (ConvTNParams::part)
+// folded in order by tn_fold: no atomics, bitwise-reproducible.
+namespace {
+
+template <int W>
+struct KmSwz {  // k-major image of W-element rows: segment key of k-row kr
+  static constexpr int SD = (128 / W) > 1 ? 128 / W : 1, SS = (W / 32) < 4 ? W / 32 : 4;
+  static __device__ __forceinline__ int f(int kr) { return SS > 1 ? (kr / SD) & (SS - 1) : 0; }
+};
+
+template <int BMc, int BNr, int WM, int WN, int NST, bool ILV>
+__global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BMc / (WM * 32), TN = BNr / (WN * 32);
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  constexpr int A_PL = PK * BMc * 2, B_PL = PK * BNr * 2;
+  constexpr int STAGE = 2 * (A_PL + B_PL);
+  constexpr int AI = BMc / 16 / NW, BI = BNr / 16 / NW;
+  static_assert(AI * 16 * NW == BMc && BI * 16 * NW == BNr, "DMA split");
+  constexpr int G = 2 * (AI + BI);
+  constexpr int CPA = BMc / 8, RPA = 64 / CPA, CPB = BNr / 8, RPB = 64 / CPB;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NST * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tilesM = (p.Co + BMc - 1) / BMc, tilesN = (p.R + BNr - 1) / BNr;
+  const int per_client = tilesM * tilesN * p.splitk;
+  const int nclients = gridDim.x / per_client;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int client = bid / per_client;
+  int t = bid - client * per_client;
+  const int split = t % p.splitk;
+  t /= p.splitk;
+  const int co0 = (t / tilesN) * BMc, r0 = (t % tilesN) * BNr;
+  const int mbeg = split * p.m_per_split;
+  const int mend = min(p.M, mbeg + p.m_per_split);
+
+  const auto ar = make_rsrc(p.dy + (long)client * p.dy_cs, (uint32_t)((p.dy_lo + (long)p.M * p.ldy) * 2));
+  const uint32_t a_lo = (uint32_t)(p.dy_lo * 2);
+  const auto br = make_rsrc(p.x + (long)client * p.x_cs, (uint32_t)((p.x_lo + (long)p.B * p.H * p.W * p.ldx) * 2));
+  const uint32_t b_lo = (uint32_t)(p.x_lo * 2);
+
+  // ---- A (dY) loader: k-row ka_i, columns co0 + chunk·8
+  int a_kr[AI], a_off[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int kr = (i * NW + wid) * RPA + lane / CPA;
+    const int co = co0 + ((lane % CPA) ^ (KmSwz<BMc>::f(kr) << 2)) * 8;
+    a_kr[i] = co < p.Co ? kr : (1 << 29);  // a column past Co never loads
+    a_off[i] = (mbeg + kr) * p.ldy + co;
+  }
+  // ---- B (im2col X) loader: fixed column chunk → fixed (kh, kw, c); pixel walk per k-row
+  constexpr int S = PK;  // pixels per K tile
+  const int q_b = S / (p.OH * p.OW), rem_b = S - q_b * p.OH * p.OW;
+  const int q_oh = rem_b / p.OW, r_ow = rem_b - q_oh * p.OW;
+  const int s_ldx = p.stride * p.ldx, s_row = p.stride * p.W * p.ldx, img = p.H * p.W * p.ldx;
+  const int d_iw = r_ow * p.stride, d_off = r_ow * s_ldx + q_oh * s_row + q_b * img;
+  const int w_wrap = p.OW * p.stride, off_c1 = s_row - p.OW * s_ldx;
+  const int d_ih0 = q_oh * p.stride, d_ih1 = (q_oh + 1) * p.stride;
+  const int h_wrap = p.OH * p.stride, off_c2 = img - p.OH * s_row;
+  int b_kr[BI], b_ow[BI], b_oh[BI], b_ih[BI], b_iw[BI], b_off[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int kr = (i * NW + wid) * RPB + lane / CPB;
+    const int r = r0 + ((lane % CPB) ^ (KmSwz<BNr>::f(kr) << 2)) * 8;
+    int kh = 0, kw = 0, c = 0;
+    if (r < p.R) {
+      kh = r / (p.KW * p.C);
+      const int rr = r - kh * p.KW * p.C;
+      kw = rr / p.C;
+      c = rr - kw * p.C;
+    }
+    b_kr[i] = r < p.R ? kr : (1 << 29);
+    const uint32_t m = mbeg + kr;
+    const uint32_t b = fdiv(m, p.fd_ohw);
+    const uint32_t rem = m - b * p.OH * p.OW;
+    const uint32_t oh = fdiv(rem, p.fd_ow);
+    const uint32_t ow = rem - oh * p.OW;
+    b_ow[i] = ow;
+    b_oh[i] = oh;
+    b_ih[i] = (int)oh * p.stride - p.pad + kh;
+    b_iw[i] = (int)ow * p.stride - p.pad + kw;
+    b_off[i] = (((int)b * p.H + b_ih[i]) * p.W + b_iw[i]) * p.ldx + c;
+  }
+
+  int k_rows = mbeg;  // first pixel of the stage being prepared
+  bool s_live = false;
+  int s_m0 = 0;
+  int sa_off[AI], sb_off[BI];
+  bool sb_ok[BI];
+  auto prep = [&](bool live) {
+    s_live = live;
+    s_m0 = k_rows;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      sa_off[i] = a_off[i];
+      a_off[i] += S * p.ldy;
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      sb_ok[i] = (unsigned)b_ih[i] < (unsigned)p.H && (unsigned)b_iw[i] < (unsigned)p.W;
+      sb_off[i] = b_off[i];
+      // advance this k-row's pixel by S (wave-uniform step constants, carries as selects)
+      b_ow[i] += r_ow;
+      b_iw[i] += d_iw;
+      b_off[i] += d_off;
+      const bool c1 = b_ow[i] >= p.OW;
+      b_ow[i] -= c1 ? p.OW : 0;
+      b_oh[i] += c1 ? q_oh + 1 : q_oh;
+      b_iw[i] -= c1 ? w_wrap : 0;
+      b_ih[i] += c1 ? d_ih1 : d_ih0;
+      b_off[i] += c1 ? off_c1 : 0;
+      const bool c2 = b_oh[i] >= p.OH;
+      b_oh[i] -= c2 ? p.OH : 0;
+      b_ih[i] -= c2 ? h_wrap : 0;
+      b_off[i] += c2 ? off_c2 : 0;
+    }
+    k_rows += S;
+  };
+  auto piece = [&](int n, int buf) {
+    unsigned char* As = smem + buf * STAGE;
+    unsigned char* Bs = As + 2 * A_PL;
+    if (n < 2 * AI) {
+      const int i = n >> 1;
+      const bool ok = s_live && s_m0 + a_kr[i] < mend;
+      const uint32_t off = (uint32_t)sa_off[i] * 2u + ((n & 1) ? a_lo : 0u);
+      dma16(ar, As + (n & 1) * A_PL + (i * NW + wid) * 1024, ok ? off : OOB_OFF);
+    } else {
+      const int i = (n - 2 * AI) >> 1;
+      const bool ok = s_live && s_m0 + b_kr[i] < mend && sb_ok[i];
+      const uint32_t off = (uint32_t)sb_off[i] * 2u + ((n & 1) ? b_lo : 0u);
+      dma16(br, Bs + (n & 1) * B_PL + (i * NW + wid) * 1024, ok ? off : OOB_OFF);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const int wm0 = (wid / WN) * (TM * 32), wn0 = (wid % WN) * (TN * 32);
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
+  constexpr int KS = PK / 16, NTRI = KS * TM * TN;
+  auto compute = [&](int buf, int nb) {
+    const bf16_t* As = reinterpret_cast<const bf16_t*>(smem + buf * STAGE);
+    const bf16_t* Bs = As + A_PL;  // (element offset 2·A_PL bytes)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kr = ks * 16 + 8 * h + q;  // (kr + 4 has the same swizzle key)
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+      const int fa = KmSwz<BMc>::f(kr), fb = KmSwz<BNr>::f(kr);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bf16_t* a0 = As + kr * BMc + ((wm0 + i * 32 + 16 * (g & 1) + 4 * pp) ^ (fa << 5));
+        ah[i] = tr_frag(a0, a0 + 4 * BMc);
+        al[i] = tr_frag(a0 + A_PL / 2, a0 + A_PL / 2 + 4 * BMc);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16_t* b0 = Bs + kr * BNr + ((wn0 + j * 32 + 16 * (g & 1) + 4 * pp) ^ (fb << 5));
+        bh[j] = tr_frag(b0, b0 + 4 * BNr);
+        bl[j] = tr_frag(b0 + B_PL / 2, b0 + B_PL / 2 + 4 * BNr);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          if constexpr (ILV) {
+            const int tri = (ks * TM + i) * TN + j;
+#pragma unroll
+            for (int n = 0; n < G; ++n)
+              if ((n * NTRI) / G == tri) {
+                piece(n, nb);
+                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+              }
+          }
+        }
+    }
+  };
+
+  const int nk = (mend - mbeg + PK - 1) / PK;
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st) {
+    prep(st < nk);
+#pragma unroll
+    for (int n = 0; n < G; ++n) piece(n, st);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vm<G*(NST - 2)>();
+    __builtin_amdgcn_s_barrier();
+    const int nb = (kt + NST - 1) % NST;
+    prep(kt + NST - 1 < nk);
+    if constexpr (!ILV) {
+#pragma unroll
+      for (int n = 0; n < G; ++n) piece(n, nb);
+    }
+    compute(kt % NST, nb);
+  }
+  wait_vm<0>();
+
+  // ---- epilogue: direct stores (splitk == 1) or this split's slab (deterministic fold)
+  const bool slab = p.splitk > 1;
+  float* __restrict__ dst = slab ? p.part + ((long)split * nclients + client) * p.Co * p.R
+                                 : p.dw + (long)client * p.dw_cs;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = r0 + wn0 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wm0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (co < p.Co && r < p.R) dst[(long)co * p.R + r] = acc[i][j][e];
+      }
+    }
+}
+
+// deterministic split-K fold: dw[k][i] = Σ_s part[(s·K + k)·CoR + i], s ascending
+__global__ void __launch_bounds__(256) tn_fold_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                      long dw_cs, int K, int splitk, long CoR) {
+  const long n4 = CoR / 4;
+  const int k = blockIdx.y;
+  const bool vec = (CoR % 4 == 0) && (dw_cs % 4 == 0) && (((uintptr_t)dw & 15) == 0);
+  if (vec) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      float4 a = reinterpret_cast<const float4*>(part + (long)k * CoR)[i];
+      for (int sp = 1; sp < splitk; ++sp) {
+        const float4 b = reinterpret_cast<const float4*>(part + ((long)sp * K + k) * CoR)[i];
+        a.x += b.x;
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+      }
+      reinterpret_cast<float4*>(dw + (long)k * dw_cs)[i] = a;
+    }
+  } else {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < CoR; i += (long)gridDim.x * 256) {
+      float a = part[(long)k * CoR + i];
+      for (int sp = 1; sp < splitk; ++sp) a += part[((long)sp * K + k) * CoR + i];
+      dw[(long)k * dw_cs + i] = a;
+    }
+  }
+}
+
+struct TnPlTile {
+  int bm, bn;
+};
+constexpr TnPlTile kTnPlTiles[] = {{128, 128}, {64, 128}, {128, 128}, {64, 128}, {256, 128}, {128, 256}};
+constexpr int kTnPlVariants = sizeof(kTnPlTiles) / sizeof(kTnPlTiles[0]);
+
+int tn_pl_default_variant(int K, int Co, int R) {
+  (void)K;
+  (void)R;
+  return Co <= 64 ? 1 : 0;
+}
+
+void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
+  const TnPlTile t = kTnPlTiles[variant];
+  const long tiles = (long)K * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  splitk = 1;
+  const int target = 512;  // ≥ 2 blocks per CU
+  if (tiles < target) {
+    splitk = (int)((target + tiles - 1) / tiles);
+    splitk = min(splitk, max(1, M / (8 * PK)));  // ≥ 8 K tiles per split
+  }
+  mps = cdiv(M, splitk);
+  mps = ((mps + PK - 1) / PK) * PK;
+  splitk = cdiv(M, mps);
+}
+
+static int g_tn_pl_variant = -1;
+
+}  // namespace
+
+int conv_tn_pl_num_variants() { return kTnPlVariants; }
+int conv_tn_pl_variant() { return g_tn_pl_variant; }
+void conv_tn_pl_set_variant(int v) { g_tn_pl_variant = v; }
+
+bool conv_tn_pl_supported(const ConvTNParams& p) {
+  return p.dy_lo != 0 && p.x_lo != 0 && p.C % 8 == 0 && p.Co % 8 == 0 && p.ldy == p.Co && p.ldx == p.C;
+}
+
+static int resolve_tn_pl(int variant, int K, int Co, int R) {
+  if (variant < 0 || variant >= kTnPlVariants) variant = tn_pl_default_variant(K, Co, R);
+  return variant;
+}
+
+int conv_tn_pl_splitk(int K, int Co, int R, int M, int variant) {
+  int splitk, mps;
+  tn_pl_split(K, Co, R, M, resolve_tn_pl(variant, K, Co, R), splitk, mps);
+  return splitk;
+}
+
+void tn_fold(const float* part, float* dw, long dw_cs, int K, int splitk, long CoR, hipStream_t s) {
+  const long n = (CoR + 3) / 4;
+  const int gx = (int)std::min<long>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(tn_fold_kernel, dim3(gx, K), dim3(256), 0, s, part, dw, dw_cs, K, splitk, CoR);
+}
+
+bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s) {
+  if (!conv_tn_pl_supported(p)) return false;
+  const long ab = (p.dy_lo + (long)p.M * p.ldy) * 2, bb = (p.x_lo + (long)p.B * p.H * p.W * p.ldx) * 2;
+  if (ab >= (long)OOB_OFF || bb >= (long)OOB_OFF) return false;
+  variant = resolve_tn_pl(variant < 0 ? g_tn_pl_variant : variant, K, p.Co, p.R);
+  tn_pl_split(K, p.Co, p.R, p.M, variant, p.splitk, p.m_per_split);
+  if (p.splitk > 1 && p.part == nullptr) return false;  // (the caller sizes the slabs)
+  const TnPlTile t = kTnPlTiles[variant];
+  const int grid = (int)((long)K * cdiv(p.Co, t.bm) * cdiv(p.R, t.bn) * p.splitk);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 128, 2, 2, 2, false>), dim3(grid), dim3(256), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((conv_tn_pl_kernel<64, 128, 2, 2, 2, false>), dim3(grid), dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 128, 2, 2, 3, true>), dim3(grid), dim3(256), 0, s, p); break;
+    case 3: hipLaunchKernelGGL((conv_tn_pl_kernel<64, 128, 2, 2, 3, true>), dim3(grid), dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL((conv_tn_pl_kernel<256, 128, 4, 2, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
+    case 5: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 256, 2, 4, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
+    default: return false;
+  }
+  if (p.splitk > 1) tn_fold(p.part, p.dw, p.dw_cs, K, p.splitk, (long)p.Co * p.R, s);
+  return true;
+}

@@ -291,7 +291,8 @@ void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s) {
   if (!launch_tn_variant(variant, p, va, vb, grid, s)) fprintf(stderr, "conv_tn: bad variant %d\n", variant);
 }
 
-int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32, int ldy, int ldx) {
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32, int ldy, int ldx, int planes) {
+  if (planes) return conv_tn_pl_splitk(K, Co, R, M, variant);
   if (ldy == 0) ldy = Co;
   if (ldx == 0) ldx = C;
   if (f32) return conv_tn_f32_splitk(K, Co, R, M, std::gcd(Co, ldy), std::gcd(C, ldx), variant);

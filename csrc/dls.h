@@ -69,6 +69,12 @@ struct ConvNTParams {
   // SGD kernel (sgd_step's `split`), so the GEMM skips splitting B in every workgroup.
   const bf16_t* wsplit;
   long ws_cs, ws_plane;
+  // optional pre-split A operand (fp32 kernels, conv_pl.hip): x is then the bf16 hi plane of the
+  // activation (same element layout as the fp32 tensor, client stride x_cs in bf16 elements)
+  // and its lo plane starts x_lo elements after it (0 = A is an fp32 tensor). Written by the
+  // producing BatchNorm (bn_fwd / bn_bwd planes outputs): with wsplit the GEMM moves both
+  // operands HBM → LDS by LDS-DMA and spends no VALU on the split.
+  long x_lo;
 };
 
 struct ConvTNParams {
@@ -82,6 +88,14 @@ struct ConvTNParams {
   FastDiv fd_ohw, fd_ow;  // filled by conv_tn()
   int f32;                // 1: dy / x are fp32 (split-bf16 GEMM, conv_f32.hip)
   int ldy, ldx;           // dy row stride (0 = Co), x pixel stride (0 = C): channel-sliced views
+  // deterministic split-K: with splitk > 1 and part != nullptr every split writes its own fp32
+  // slab part[(split·K + client)·Co·R + co·R + r] (plain stores, no atomics, no pre-zeroed dw)
+  // and a fold pass sums the slabs in split order into dw — bitwise-reproducible weight
+  // gradients (the launchers run the fold; part holds splitk·K·Co·R floats)
+  float* part;
+  // pre-split operands (conv_pl.hip): dy / x are bf16 hi planes, lo planes dy_lo / x_lo
+  // elements after them (0 = fp32 tensors); client strides dy_cs / x_cs in bf16 elements
+  long dy_lo, x_lo;
 };
 
 // Large-tile conv GEMM fed by the LDS-DMA (conv_gl.hip): K loop over a tap table × 64-channel
@@ -125,15 +139,32 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 // classes, each a dense stride-1 GEMM over only the taps that reach it (no dilation zeros).
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
-                int ld_dy = 0, long dy_cs = 0, const bf16_t* wsplit = nullptr, long ws_cs = 0, long ws_plane = 0);
+                int ld_dy = 0, long dy_cs = 0, const bf16_t* wsplit = nullptr, long ws_cs = 0, long ws_plane = 0,
+                long x_lo = 0);  // x_lo: dy is the hi plane of pre-split planes (ConvNTParams::x_lo)
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
-int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32, int ldy = 0, int ldx = 0);
+int conv_tn_splitk(int K, int Co, int R, int M, int C, int variant, int f32, int ldy = 0, int ldx = 0,
+                   int planes = 0);  // planes: the pre-split launch (conv_tn_pl_splitk, its own variant ids)
 // fp32 (split-bf16 MFMA) GEMMs, conv_f32.hip; reached through conv_nt / conv_tn with p.f32 = 1
 void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s);
 int conv_nt_f32_num_variants();
 void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s);
+// pre-split operand planes (conv_pl.hip): false when the shape is outside the kernels' contract
+bool conv_nt_pl_supported(const ConvNTParams& p);
+bool conv_nt_pl(const ConvNTParams& p, int K, int variant, hipStream_t s);
+int conv_nt_pl_num_variants();
+int conv_nt_pl_variant();           // -1: shape heuristic (set by benchmarks)
+void conv_nt_pl_set_variant(int v);
+bool conv_tn_pl_supported(const ConvTNParams& p);
+bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s);
+int conv_tn_pl_num_variants();
+int conv_tn_pl_variant();
+void conv_tn_pl_set_variant(int v);
+// split-K factor of the pre-split wgrad launch (callers size ConvTNParams::part with it)
+int conv_tn_pl_splitk(int K, int Co, int R, int M, int variant);
+// dw[k][i] = Σ_s part[(s·K + k)·CoR + i] in split order (deterministic split-K fold)
+void tn_fold(const float* part, float* dw, long dw_cs, int K, int splitk, long CoR, hipStream_t s);
 int conv_tn_f32_num_variants();
 int conv_tn_f32_splitk(int K, int Co, int R, int M, int gco, int gc, int variant);
 

@@ -1,0 +1,120 @@
+// fp32 epilogue of the NT GEMMs (conv_f32.hip register-staged tiles, conv_pl.hip pre-split
+// planes): bias (+ReLU) → optional BN statistics partials straight from the accumulators →
+// per-wave 32-row fp32 LDS slab → 16-B coalesced stores with the optional gate (ReLU' of the
+// next layer's input), dropout mask and accumulate (second gradient branch).
+#pragma once
+#include "dls.h"
+#include "gemm_common.h"
+
+// acc[TM][TN]: the wave's 32x32 accumulator tiles (v_mfma_f32_32x32x16 C layout); smem: ≥
+// NW·32·SW floats, free (the caller has retired every read of the main-loop images)
+template <int TM, int TN, int NW>
+__device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&acc)[TM][TN], unsigned char* smem,
+                                                int client, int m0, int n0, int wm0, int wn0, int wid, int lane) {
+  constexpr int SW = TN * 32 + 4;  // slab row (fp32), 16-B aligned
+  float* __restrict__ y = reinterpret_cast<float*>(p.y) + (long)client * p.y_cs;
+  const float* accp = p.acc ? reinterpret_cast<const float*>(p.acc) + (long)client * p.y_cs : nullptr;
+  const float* gatep = p.gate ? reinterpret_cast<const float*>(p.gate) + (long)client * p.y_cs : nullptr;
+  const float* bias = p.bias ? reinterpret_cast<const float*>(p.bias) + (long)(client / p.rep) * p.b_cs : nullptr;
+  // epilogue scale (dropout's 1/(1-p), or the dgrad gate's) and dropout mask of this client row
+  const bool drop = p.drop_p > 0.f && p.drop_seeds != nullptr;
+  const uint32_t dseed = drop ? p.drop_seeds[client] : 0u;
+  const float oscale = (p.out_scale != 0.f ? p.out_scale : 1.f) * (drop ? 1.f / (1.f - p.drop_p) : 1.f);
+  float bvals[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + j * 32 + (lane & 31);
+    bvals[j] = (bias && n < p.N) ? bias[n] : 0.f;
+  }
+  float* slab = reinterpret_cast<float*>(smem) + wid * 32 * SW;
+  const bool vec_ok = (p.N % 4) == 0 && (p.ldy % 4) == 0 && ((uintptr_t)y & 15) == 0;
+  // BN statistics rows: GEMM rows of this client's valid samples
+  const int stat_rows = p.stats ? (p.stats_valid ? min(p.M, p.stats_valid[client] * p.OH * p.OW) : p.M) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int g0 = m0 + wm0 + i * 32;  // this wave's 32-row group (a multiple of 32)
+    if (p.stats && g0 < p.M) {
+      // per-column Σy, Σy² of the group straight from the accumulators: lane (c, h) holds rows
+      // (e&3) + 8(e>>2) + 4h of column c; the two half-waves combine with one xor-shuffle
+      float* part = p.stats + ((long)client * ((p.M + 31) / 32) + g0 / 32) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = g0 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          float v = acc[i][j][e] + bvals[j];
+          if (p.relu) v = fmaxf(v, 0.f);
+          if (m < stat_rows) {
+            s0 += v;
+            s1 = fmaf(v, v, s1);
+          }
+        }
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        const int n = n0 + wn0 + j * 32 + (lane & 31);
+        if (lane < 32 && n < p.N) {
+          part[n] = s0;
+          part[p.N + n] = s1;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float v = acc[i][j][e] + bvals[j];
+        if (p.relu) v = fmaxf(v, 0.f);
+        v *= oscale;
+        if (drop) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          if (!drop_keep(dseed, m0 + wm0 + i * 32 + rr, p.N, n0 + wn0 + j * 32 + (lane & 31), p.drop_p)) v = 0.f;
+        }
+        slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = v;
+      }
+    }
+    __syncthreads();
+    for (int qd = lane; qd < 32 * TN * 8; qd += 64) {
+      const int r = qd / (TN * 8), cc = (qd % (TN * 8)) * 4;
+      const int m = m0 + wm0 + i * 32 + r, n = n0 + wn0 + cc;
+      if (m >= p.M || n >= p.N) continue;
+      long row = m;
+      if (p.out_s > 1) {
+        const uint32_t b = fdiv(m, p.fd_ohw);
+        const uint32_t rem = m - b * p.OH * p.OW;
+        const uint32_t oh = fdiv(rem, p.fd_ow);
+        const uint32_t ow = rem - oh * p.OW;
+        row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
+      }
+      float* dst = y + row * p.ldy + n;
+      const float* src = slab + r * SW + cc;
+      if (vec_ok && n + 4 <= p.N) {
+        float4 v = *reinterpret_cast<const float4*>(src);
+        if (gatep) {
+          const float4 gv = *reinterpret_cast<const float4*>(gatep + row * p.ldy + n);
+          v.x = gv.x > 0.f ? v.x : 0.f;
+          v.y = gv.y > 0.f ? v.y : 0.f;
+          v.z = gv.z > 0.f ? v.z : 0.f;
+          v.w = gv.w > 0.f ? v.w : 0.f;
+        }
+        if (accp) {
+          const float4 av = *reinterpret_cast<const float4*>(accp + row * p.ldy + n);
+          v.x += av.x;
+          v.y += av.y;
+          v.z += av.z;
+          v.w += av.w;
+        }
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        for (int t2 = 0; t2 < 4 && n + t2 < p.N; ++t2) {
+          float o = src[t2];
+          if (gatep && !(gatep[row * p.ldy + n + t2] > 0.f)) o = 0.f;
+          if (accp) o += accp[row * p.ldy + n + t2];
+          dst[t2] = o;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}

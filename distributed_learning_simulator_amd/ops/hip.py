@@ -147,8 +147,34 @@ def conv_stats_parts(M: int) -> int:
     return (M + 31) // 32
 
 
+def planes_ok(C: int, N: int, ld: int | None = None) -> bool:
+    """Shape contract of the pre-split-operand GEMMs (csrc/conv_pl.hip): a K tile of 32 never
+    straddles a tap (C % 32), contiguous planes, 16-B output columns (N % 8)."""
+    return C % 32 == 0 and N % 8 == 0 and (ld is None or ld == C)
+
+
+def split_planes(x, out=None):
+    """[K, 2, *x.shape[1:]] bf16 (hi, lo) planes of a contiguous fp32 activation x:
+    hi = bf16(x), lo = bf16(x − hi) (RNE), the operand form of the conv_pl.hip GEMMs."""
+    assert x.dtype == F32 and x.is_contiguous()
+    K = x.shape[0]
+    if out is None:
+        out = torch.empty((K, 2) + tuple(x.shape[1:]), dtype=BF16, device=x.device)
+    assert out.shape == (K, 2) + tuple(x.shape[1:]) and out.dtype == BF16 and out.is_contiguous()
+    split_rows(x.view(K, -1), out.view(K, 2, -1))
+    return out
+
+
+def _planes_args(planes, t):
+    """(hi-plane pointer, client stride, hi→lo distance) of [K, 2, ...] planes of tensor t."""
+    assert planes.dtype == BF16 and planes.is_contiguous(), "planes must be contiguous bf16"
+    assert planes.shape == (t.shape[0], 2) + tuple(t.shape[1:]), (planes.shape, t.shape)
+    assert planes.stride(1) * 4 < 2 ** 31, "per-client plane window over 2 GiB"
+    return _p(planes), planes.stride(0), planes.stride(1)
+
+
 def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats=None, stats_valid=None,
-             w_split=None):
+             w_split=None, x_planes=None):
     """`x` may be a channel slice of a wider buffer, `out` (optional) a channel slice to write
     into (DenseNet block buffer): both are read / written in place through channel strides.
     `stats` (fp32 only): a [K, conv_stats_parts(M), 2, Co] fp32 buffer the epilogue fills with the
@@ -185,13 +211,16 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
     ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
-    _C.conv_nt(_p(x), _p(w), _p(y), _p(bias), x.stride(0), y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
+    xp, x_cs, x_lo = _p(x), x.stride(0), 0
+    if x_planes is not None and ws_p and planes_ok(C, Co, ldx):
+        xp, x_cs, x_lo = _planes_args(x_planes, x)  # LDS-DMA GEMM on pre-split operands
+    _C.conv_nt(xp, _p(w), _p(y), _p(bias), x_cs, y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
                pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32,
-               _s(), ldx, ldy, _p(stats), _p(stats_valid), NULL, 0.0, 0.0, ws_p, ws_cs, ws_plane)
+               _s(), ldx, ldy, _p(stats), _p(stats_valid), NULL, 0.0, 0.0, ws_p, ws_cs, ws_plane, x_lo)
     return y
 
 
-def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None):
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None):
     """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
     residual branch of a ResNet block, so autograd never materialises the sum separately).
     `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient)."""
@@ -219,12 +248,55 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None):
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
     ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
-    _C.conv_dgrad(_p(dy), _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
-                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy.stride(0), ws_p, ws_cs, ws_plane)
+    dyp, dy_cs, dy_lo = _p(dy), dy.stride(0), 0
+    if dy_planes is not None and ws_p and planes_ok(Co, Ci, ld_dy):
+        dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
+    _C.conv_dgrad(dyp, _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
+                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy_cs, ws_p, ws_cs, ws_plane, dy_lo)
     return dx
 
 
-def conv_wgrad(dy, x, gw, stride: int, pad: int):
+# fp32 weight gradients: split-K partial slabs folded in split order (bitwise-reproducible, no
+# atomics) — DLS_DETERMINISTIC=0 restores fp32 atomics into pre-zeroed rows (A/B)
+deterministic = os.environ.get("DLS_DETERMINISTIC", "1") != "0"
+_part_cache: dict = {}
+
+
+def _tn_part(numel: int, device) -> torch.Tensor:
+    """Split-K slab buffer of the deterministic wgrad fold, per (device, stream); grown, never
+    shrunk, so a captured graph keeps a stable pointer after the warm-up step sized it."""
+    key = (device, torch.cuda.current_stream().cuda_stream)
+    t = _part_cache.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1 << 16), dtype=torch.float32, device=device)
+        _part_cache[key] = t
+    return t
+
+
+def _tn_launch(dy, x, gw, dy_cs, x_cs, B, H, W, C, OH, OW, KH, KW, stride, pad, M, Co, R, K, f32, ldy, ldx,
+               dy_planes=None, x_planes=None):
+    """conv_tn with the split-K policy: slabs + ordered fold (fp32, deterministic) or atomics."""
+    planes = f32 and dy_planes is not None and x_planes is not None
+    tv = (_C.conv_tn_pl_variant() if planes else tn_f32_variant) if f32 else tn_variant
+    dyp, xp, dy_lo, x_lo = _p(dy), _p(x), 0, 0
+    if planes:
+        dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
+        xp, x_cs, x_lo = _planes_args(x_planes, x)
+    splitk = _C.conv_tn_splitk(K, Co, R, M, C, tv, f32, ldy, ldx, int(planes))
+    part = NULL
+    if splitk > 1:
+        if f32 and (deterministic or planes):
+            part = _p(_tn_part(splitk * K * Co * R, gw.device))
+        else:
+            gw.zero_()
+    _C.conv_tn(dyp, xp, _p(gw), dy_cs, x_cs, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M, Co, R, K, tv,
+               f32, _s(), ldy, ldx, part, dy_lo, x_lo)
+
+
+def conv_wgrad(dy, x, gw, stride: int, pad: int, dy_planes=None, x_planes=None):
+    """dW of a conv into the fp32 gradient rows gw [K, Co, KH, KW, Ci]. `dy_planes` /
+    `x_planes` (fp32 only, both or neither): pre-split operands (split_planes), read by the
+    LDS-DMA GEMM of csrc/conv_pl.hip when the shape allows (planes_ok)."""
     K, B, OH, OW, Co = dy.shape
     _, _, H, W, C = x.shape
     dy, ldy = _pix_stride(dy)
@@ -236,11 +308,10 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int):
     assert Co2 == Co and Ci == C
     M = B * OH * OW
     R = KH * KW * C
-    tv = tn_f32_variant if f32 else tn_variant
-    if _C.conv_tn_splitk(K, Co, R, M, C, tv, f32, ldy, ldx) > 1:
-        gw.zero_()
-    _C.conv_tn(_p(dy), _p(x), _p(gw), dy.stride(0), x.stride(0), gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad,
-               M, Co, R, K, tv, f32, _s(), ldy, ldx)
+    use_pl = (dy_planes is not None and x_planes is not None and f32 and C % 8 == 0 and Co % 8 == 0
+              and ldy == Co and ldx == C)
+    _tn_launch(dy, x, gw, dy.stride(0), x.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M, Co, R, K, f32,
+               ldy, ldx, dy_planes if use_pl else None, x_planes if use_pl else None)
 
 
 def bias_grad(dy, gb):
@@ -270,7 +341,7 @@ def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_see
     ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
                int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL,
-               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, ws_p, ws_cs, ws_plane)
+               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, ws_p, ws_cs, ws_plane, 0)
     return y
 
 
@@ -291,7 +362,7 @@ def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0, w_split=None):
     ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
                1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0,
-               NULL, NULL, NULL, 0.0, float(gate_scale), ws_p, ws_cs, ws_plane)
+               NULL, NULL, NULL, 0.0, float(gate_scale), ws_p, ws_cs, ws_plane, 0)
     return dx
 
 
@@ -323,11 +394,7 @@ def linear_wgrad(dy, x, gw, gb=None):
     f32 = _f32(dy)
     assert x.dtype == dy.dtype
     assert gw.shape == (K, Fo, Fi) and gw[0].is_contiguous()
-    tv = tn_f32_variant if f32 else tn_variant
-    if _C.conv_tn_splitk(K, Fo, Fi, N, Fi, tv, f32) > 1:
-        gw.zero_()
-    _C.conv_tn(_p(dy), _p(x), _p(gw), N * Fo, N * Fi, gw.stride(0), 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K,
-               tv, f32, _s(), 0, 0)
+    _tn_launch(dy, x, gw, N * Fo, N * Fi, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K, f32, 0, 0)
     if gb is not None:
         gb.zero_()
         _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, f32, _s())

@@ -88,16 +88,16 @@ def test_conv_f32_every_variant(hip, case):
         y = torch.empty_like(dy)
         hip._C.conv_nt(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, B * H * W * Ci, M * Co, w.stride(0), 0, B, H, W,
                        Ci, OH, y.shape[3], k, k, s, p, 1, M, Co, k * k * Ci, 1, 0, K, 0, v, 0, 0, 1, stream, 0, 0, 0, 0, 0, 0.0, 0.0,
-                       0, 0, 0)
+                       0, 0, 0, 0)
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
-                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0)
+                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0)
         _close(dx, dx_ref)
     for v in range(hip._C.conv_tn_f32_num_variants()):
         gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
         hip._C.conv_tn(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M * Co, B * H * W * Ci, gw.stride(0), B, H, W, Ci,
-                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream, 0, 0)
+                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream, 0, 0, 0, 0, 0)
         _close(gw, dw_ref)
 
 
@@ -463,3 +463,82 @@ def test_linear_presplit_weight_planes(hip):
     assert torch.equal(hip.linear_fwd(x, w, b), hip.linear_fwd(x, w, b, w_split=ws))
     dy = _f(K, N, Fo)
     assert torch.equal(hip.linear_dgrad(dy, w), hip.linear_dgrad(dy, w, w_split=ws))
+
+
+def _wsplit(hip, w):
+    """Pre-split weight planes as the SGD step keeps them: hi-plane view into a [K, 2, P] buffer."""
+    K = w.shape[0]
+    ws = torch.empty((K, 2, w[0].numel()), dtype=torch.bfloat16, device=DEV)
+    hip.split_rows(w.reshape(K, -1).contiguous(), ws)
+    return ws[:, 0].view(w.shape)
+
+
+PLANES_CASES = [
+    # K, B, H, W, Ci, Co, k, stride, pad
+    (2, 2, 8, 8, 64, 64, 3, 1, 1),
+    (2, 3, 9, 9, 64, 128, 3, 2, 1),    # stride 2: four dgrad parity classes
+    (2, 2, 8, 8, 64, 128, 1, 2, 0),    # 1x1 downsample shortcut (a class with no tap)
+    (3, 2, 7, 7, 128, 256, 3, 1, 1),
+    (2, 2, 5, 5, 32, 40, 3, 1, 1),     # N tail (40 of a 64 / 128 tile)
+    (2, 4, 4, 4, 256, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", PLANES_CASES)
+def test_conv_planes_every_variant(hip, case):
+    """LDS-DMA GEMMs on pre-split operands (csrc/conv_pl.hip): every tile variant is bit-identical
+    to the register-staged split-bf16 kernel (same hi / lo values, same product order) and within
+    1e-5 of the fp64 oracle, forward and dgrad (k-major weight read in place, parity classes)."""
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(5)
+    x = _f(K, B, H, W, Ci)
+    w = _f(K, Co, k, k, Ci, scale=0.2)
+    ws = _wsplit(hip, w)
+    y_base = hip.conv_fwd(x, w, s, p, w_split=ws)
+    _close(y_base, ref.conv_fwd(_d(x), _d(w), s, p))
+    dy = _f(*y_base.shape)
+    acc = _f(K, B, H, W, Ci)
+    dx_base = hip.conv_dgrad(dy, w, (H, W), s, p, acc=acc, w_split=ws)
+    _close(dx_base, ref.conv_dgrad(_d(dy), _d(w), (H, W), s, p) + _d(acc))
+    xp, dyp = hip.split_planes(x), hip.split_planes(dy)
+    try:
+        for v in range(hip._C.conv_nt_pl_num_variants()):
+            hip._C.conv_nt_pl_set_variant(v)
+            y = hip.conv_fwd(x, w, s, p, w_split=ws, x_planes=xp)
+            assert torch.equal(y, y_base), f"variant {v} fwd differs"
+            dx = hip.conv_dgrad(dy, w, (H, W), s, p, acc=acc, w_split=ws, dy_planes=dyp)
+            assert torch.equal(dx, dx_base), f"variant {v} dgrad differs"
+    finally:
+        hip._C.conv_nt_pl_set_variant(-1)
+
+
+@pytest.mark.parametrize("case", PLANES_CASES + [(2, 8, 16, 16, 64, 64, 3, 1, 1), (3, 2, 8, 8, 8, 64, 3, 1, 1)])
+def test_wgrad_planes_every_variant(hip, case):
+    """Pre-split wgrad (csrc/conv_pl.hip TN, split-K slabs + ordered fold): every tile variant
+    within 1e-5 of the fp64 oracle and bitwise-reproducible run to run; the register-staged
+    fp32 wgrad with the deterministic fold likewise reproducible."""
+    K, B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(7)
+    x = _f(K, B, H, W, Ci)
+    OH = (H + 2 * p - k) // s + 1
+    OW = (W + 2 * p - k) // s + 1
+    dy = _f(K, B, OH, OW, Co)
+    exp = ref.conv_wgrad(_d(dy), _d(x), (K, Co, k, k, Ci), s, p)
+    gw0 = torch.empty((K, Co, k, k, Ci), device=DEV)
+    hip.conv_wgrad(dy, x, gw0, s, p)
+    _close(gw0, exp)
+    gw1 = torch.full_like(gw0, 3.0)
+    hip.conv_wgrad(dy, x, gw1, s, p)
+    assert torch.equal(gw0, gw1), "fp32 wgrad not reproducible"
+    xp, dyp = hip.split_planes(x), hip.split_planes(dy)
+    try:
+        for v in range(hip._C.conv_tn_pl_num_variants()):
+            hip._C.conv_tn_pl_set_variant(v)
+            ga = torch.full_like(gw0, 5.0)
+            hip.conv_wgrad(dy, x, ga, s, p, dy_planes=dyp, x_planes=xp)
+            _close(ga, exp)
+            gb = torch.full_like(gw0, -5.0)
+            hip.conv_wgrad(dy, x, gb, s, p, dy_planes=dyp, x_planes=xp)
+            assert torch.equal(ga, gb), f"variant {v} not reproducible"
+    finally:
+        hip._C.conv_tn_pl_set_variant(-1)
