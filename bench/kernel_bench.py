@@ -126,6 +126,18 @@ def main():
             xp, dyp = hip.split_planes(x), hip.split_planes(dy)
             base_f = flops / timeit(lambda: hip.conv_fwd(x, w, s, pad, w_split=ws), args.iters) / 1e12
             base_d = flops / timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad, w_split=ws), args.iters) / 1e12
+            if k == 3 and s == 1:  # 3x3 stride 1: the LDS-halo kernel (csrc/conv_halo.hip)
+                hip._C.conv_halo_set_mode(1)
+                hv = {}
+                for v in range(3):
+                    hip._C.conv_halo_set_variant(v)
+                    tf_h = timeit(lambda: hip.conv_fwd(x, w, s, pad, w_split=ws, x_planes=xp), args.iters)
+                    td_h = timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad, w_split=ws, dy_planes=dyp),
+                                  args.iters)
+                    hv[v] = (round(flops / tf_h / 1e12, 1), round(flops / td_h / 1e12, 1))
+                hip._C.conv_halo_set_variant(-1)
+                hip._C.conv_halo_set_mode(0)
+                row["halo_fwd_dgrad"] = hv
             pv = {}
             for v in [-1] + list(range(hip._C.conv_nt_pl_num_variants())):
                 hip._C.conv_nt_pl_set_variant(v)
@@ -133,6 +145,7 @@ def main():
                 td_v = timeit(lambda: hip.conv_dgrad(dy, w, (H, H), s, pad, w_split=ws, dy_planes=dyp), args.iters)
                 pv[v] = (round(flops / tf_v / 1e12, 1), round(flops / td_v / 1e12, 1))
             hip._C.conv_nt_pl_set_variant(-1)
+            hip._C.conv_halo_set_mode(-1)
             row["split_w_fwd_dgrad"] = (round(base_f, 1), round(base_d, 1))
             row["planes_fwd_dgrad"] = pv
             pw = {}

@@ -97,23 +97,25 @@ PYBIND11_MODULE(_dls_hip, m) {
   m.def("conv_nt_f32_num_variants", &conv_nt_f32_num_variants);
   m.def("conv_nt_pl_num_variants", &conv_nt_pl_num_variants);
   m.def("conv_nt_pl_set_variant", &conv_nt_pl_set_variant);
+  m.def("conv_halo_set_mode", &conv_halo_set_mode);
+  m.def("conv_halo_set_variant", &conv_halo_set_variant);
   m.def("conv_tn_f32_num_variants", &conv_tn_f32_num_variants);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_fwd", [](ptr x, ptr gamma, ptr beta, ptr res, ptr y, ptr mean, ptr rstd, ptr valid, long g_cs, int K,
                      int R, int C, int relu, float eps, int rep, ptr ws, ptr mask, ptr counters, int f32, ptr s,
-                     int ldx, ptr pre_part, int pre_nparts) {
+                     int ldx, ptr pre_part, int pre_nparts, ptr yp, int y_f32) {
     bn_fwd(P<const void>(x), P<const void>(gamma), P<const void>(beta), P<const void>(res), P<void>(y), P<float>(mean),
            P<float>(rstd), P<const int>(valid), g_cs, K, R, C, relu, eps, rep, P<float>(ws), P<uint8_t>(mask),
-           P<unsigned>(counters), f32, S(s), ldx, P<const float>(pre_part), pre_nparts);
+           P<unsigned>(counters), f32, S(s), ldx, P<const float>(pre_part), pre_nparts, P<bf16_t>(yp), y_f32);
   });
   m.def("bn_bwd", [](ptr dy, ptr x, ptr y, ptr mean, ptr rstd, ptr gamma, ptr valid, long g_cs, int K, int R, int C,
                      int relu, ptr dx, ptr dpre, ptr dgamma, ptr dbeta, long dg_cs, ptr ws, ptr mask, ptr counters,
-                     int f32, ptr s, int ldx, int acc_dx) {
+                     int f32, ptr s, int ldx, int acc_dx, ptr dxp, int dx_f32) {
     bn_bwd(P<const void>(dy), P<const void>(x), P<const void>(y), P<const float>(mean), P<const float>(rstd),
            P<const void>(gamma), P<const int>(valid), g_cs, K, R, C, relu, P<void>(dx), P<void>(dpre), P<float>(dgamma),
            P<float>(dbeta), dg_cs, P<float>(ws), P<const uint8_t>(mask), P<unsigned>(counters), f32, S(s), ldx,
-           acc_dx);
+           acc_dx, P<bf16_t>(dxp), dx_f32);
   });
   m.def("ln_fwd", [](ptr x, ptr gamma, ptr beta, ptr y, ptr mean, ptr rstd, long g_cs, int K, long rpc, int C,
                      float eps, int rep, int f32, ptr s) {

@@ -721,7 +721,8 @@ void tn_f32_split(int K, int Co, int R, int M, int variant, int& splitk, int& mp
 int conv_nt_f32_num_variants() { return 11; }
 
 void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
-  if (p.x_lo != 0) {  // pre-split A (and B) planes: the LDS-DMA kernels of conv_pl.hip
+  if (p.x_lo != 0) {  // pre-split A (and B) planes: the LDS-DMA kernels of conv_halo / conv_pl.hip
+    if (conv_nt_pl_variant() < 0 && conv_halo(p, K, s)) return;
     if (!conv_nt_pl(p, K, conv_nt_pl_variant(), s)) {
       fprintf(stderr, "conv_nt_f32: pre-split operands in an unsupported shape (C %d, ldx %d, N %d, R %d)\n", p.C,
               p.ldx, p.N, p.R);

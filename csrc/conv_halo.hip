@@ -1,0 +1,315 @@
+// 3x3 / stride-1 / pad-1 fp32-accurate convolution on pre-split operands with LDS halo reuse
+// (gfx950, MI355X).
+//
+// The implicit-GEMM kernels (conv_pl.hip) stage a fresh A tile for every (tap, channel chunk):
+// each input pixel crosses the L2 → LDS path up to 9 times per output-channel tile, and that
+// path (≈60 GB/s per CU for LDS-DMA gathers) is what bounds them. Here a workgroup owns a block
+// of whole output rows — IMG images × TH rows × the full width TW, BM = IMG·TH·TW GEMM rows —
+// and per 32-channel chunk DMAs the block's input HALO once ((TH+2)·(TW+2) pixels per image,
+// zeros outside the image) into LDS; the nine taps then read their A fragments from that halo
+// at a uniform row shift (dh·(TW+2) + dw). Only the weight tile is staged per tap. A-side bytes
+// per chunk drop from 9·BM rows to IMG·(TH+2)·(TW+2) rows: 2.6–8.5× fewer for ResNet-18's
+// 32², 16², 8², 4² layers.
+//
+// Arithmetic, split planes and product order are those of conv_pl.hip (bf16x3 on
+// v_mfma_f32_32x32x16_bf16), so outputs are bit-identical to it, and it serves
+//   forward : B = W[n][kh][kw][c] row-major;
+//   dgrad   : stride-1 full correlation of dY with the flipped kernel, B read k-major in place
+//             (ConvNTParams kh_off / kh_step mapping).
+// Pipeline (per wave, all in one __shared__ array): halo double-buffered — chunk c+1's halo is
+// issued at chunk c's first tap step; weight tiles in a 3-slot ring, tile s+2 issued at step s.
+// Counted vmcnt before each step's barrier: the step's weight tile and its chunk's halo are
+// older than everything left in flight (see the wait comments in the loop).
+#include "dls.h"
+#include "epilogue_f32.h"
+#include "gemm_common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void hdma16(__amdgpu_buffer_rsrc_t r, unsigned char* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void hwait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// HB: halo buffers (2: chunk c+1's halo in flight during chunk c; 1: loaded at the chunk start
+// behind a barrier — half the LDS, so two workgroups share a CU); NBS: weight-tile slots (3 or 2)
+template <int IMG, int TH, int TW, int BN, int WM, int WN, bool BKM, int MINW, int HB, int NBS>
+__global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTParams p) {
+  static_assert((HB == 2 && NBS == 3) || (HB == 1 && (NBS == 2 || NBS == 3)), "pipeline shape");
+  constexpr int BM = IMG * TH * TW;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM, "wave tile");
+  constexpr int HW2 = TW + 2, HH2 = TH + 2;
+  constexpr int HP = IMG * HH2 * HW2;              // halo pixels (rows of the A image)
+  constexpr int HI = (HP + 16 * NW - 1) / (16 * NW);  // halo DMA instructions per wave per plane
+  constexpr int H_PL = HI * 16 * NW * 64;          // bytes per halo plane (64-B rows)
+  constexpr int B_PL = BN * 64;                    // bytes per weight plane ([BN][32] or [32][BN])
+  constexpr int NBI = BN / 16;                     // 1-KiB weight DMA instructions per plane
+  constexpr int BI = (NBI + NW - 1) / NW;          // per wave (the surplus ones go to a scratch KiB)
+  constexpr int GH = 2 * HI, GB = 2 * BI;          // DMA instructions per wave: halo / weight tile
+  constexpr int H_OFF = 0, B_OFF = HB * 2 * H_PL;  // halo buffers (hi, lo each), then the weight slots
+  constexpr int SCR = B_OFF + NBS * 2 * B_PL;      // scratch KiB of the surplus weight DMAs
+  constexpr int LOOP = SCR + (BI * NW > NBI ? 1024 : 0);
+  constexpr int SW = TN * 32 + 4;
+  constexpr int EPI = NW * 32 * SW * 4;
+  constexpr int SMEM = LOOP > EPI ? LOOP : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tpi = p.OH / TH;  // row blocks per image (IMG == 1), 1 otherwise
+  const int tilesM = IMG == 1 ? p.B * tpi : p.B / IMG, tilesN = (p.N + BN - 1) / BN;
+  const int per_client = tilesM * tilesN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int client = bid / per_client;
+  const int t = bid - client * per_client;
+  const int tm = t / tilesN, n0 = (t % tilesN) * BN;
+  const int b0 = IMG == 1 ? tm / tpi : tm * IMG;
+  const int h0 = IMG == 1 ? (tm % tpi) * TH : 0;
+  const int m0 = tm * BM;
+
+  const long a_img = (long)p.B * p.H * p.W * p.ldx;
+  const auto ar = make_rsrc(p.x + (long)client * p.x_cs, (uint32_t)((p.x_lo + a_img) * 2));
+  const uint32_t a_lo = (uint32_t)(p.x_lo * 2);
+  const long w_ext = BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R;
+  const auto br = make_rsrc(p.wsplit + (long)client * p.ws_cs, (uint32_t)((p.ws_plane + w_ext) * 2));
+  const uint32_t b_lo = (uint32_t)(p.ws_plane * 2);
+
+  // ---- halo loader: instruction i of wave w fills halo rows (i·NW + w)·16 + lane/4, physical
+  // chunk lane & 3 ← logical chunk lc (row swizzle key (row >> 2) & 3 = (lane >> 4) & 3)
+  const int lc = (lane & 3) ^ ((lane >> 4) & 3);
+  int h_off[HI];
+#pragma unroll
+  for (int i = 0; i < HI; ++i) {
+    const int hr = (i * NW + wid) * 16 + (lane >> 2);
+    const int img = hr / (HH2 * HW2), rem = hr - img * (HH2 * HW2);
+    const int hh = rem / HW2, ww = rem - hh * HW2;
+    const int ih = h0 - p.pad + hh, iw = ww - p.pad_w;
+    const bool ok = hr < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    h_off[i] = ok ? (((b0 + img) * p.H + ih) * p.W + iw) * p.ldx + lc * 8 : -1;
+  }
+  // ---- weight loader (as conv_pl.hip): row-major rows (i·NW + w)·16 + lane/4; k-major k-rows
+  // (i·NW + w)·RPI + lane/CPR with the 32-element segment swizzle of the k-major image
+  constexpr int CPR = BN / 8, RPI = 64 / CPR;
+  constexpr int SD = (128 / BN) > 1 ? 128 / BN : 1, SS = (BN / 32) < 4 ? BN / 32 : 4;
+  const long wkhwn = (long)p.wKH * p.wKW * p.N;
+  int b_off[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    if constexpr (!BKM) {
+      const int n = n0 + (i * NW + wid) * 16 + (lane >> 2);
+      b_off[i] = n < p.N ? n * p.R + lc * 8 : -1;
+    } else {
+      const int kr = (i * NW + wid) * RPI + lane / CPR;
+      const int f = SS > 1 ? (kr / SD) & (SS - 1) : 0;
+      const int n = n0 + ((lane % CPR) ^ (f << 2)) * 8;
+      b_off[i] = n < p.N ? (int)(kr * wkhwn) + n : -1;
+    }
+    if (i * NW + wid >= NBI) b_off[i] = -1;
+  }
+
+  const int nchunks = p.C / 32, nsteps = nchunks * 9;
+  auto issue_halo = [&](int c, int buf) {
+    const bool live = c < nchunks;
+    unsigned char* Hs = smem + H_OFF + buf * 2 * H_PL;
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const bool ok = live && h_off[i] >= 0;
+      const uint32_t off = (uint32_t)(h_off[i] + c * 32) * 2u;
+      unsigned char* d = Hs + (i * NW + wid) * 1024;
+      hdma16(ar, d, ok ? off : OOB_OFF);
+      hdma16(ar, d + H_PL, ok ? off + a_lo : OOB_OFF);
+    }
+  };
+  auto issue_w = [&](int s, int slot) {
+    const bool live = s < nsteps;
+    const int c = s / 9, tap = s - c * 9;
+    int boff;
+    if constexpr (!BKM) {
+      boff = tap * p.C + c * 32;
+    } else {
+      const int kh2 = tap / 3, kw2 = tap - kh2 * 3;
+      const int khh = p.kh_off - p.kh_step * kh2, kww = p.kw_off - p.kw_step * kw2;
+      boff = (int)(c * 32 * wkhwn) + (khh * p.wKW + kww) * p.N;
+    }
+    unsigned char* Bs = smem + B_OFF + slot * 2 * B_PL;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const bool ok = live && b_off[i] >= 0;
+      const uint32_t off = (uint32_t)(b_off[i] + boff) * 2u;
+      const bool real = BI * NW == NBI || i * NW + wid < NBI;  // (wave-uniform)
+      unsigned char* d = real ? Bs + (i * NW + wid) * 1024 : smem + SCR;
+      hdma16(br, d, ok ? off : OOB_OFF);
+      hdma16(br, real ? d + B_PL : d, ok ? off + b_lo : OOB_OFF);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  const int wm0 = (wid / WN) * (TM * 32), wn0 = (wid % WN) * (TN * 32);
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
+  // halo row of each A fragment row at tap (0, 0); tap (dh, dw) adds dh·HW2 + dw
+  int hbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int pix = wm0 + i * 32 + (lane & 31);
+    const int img = pix / (TH * TW), rr = pix - img * (TH * TW);
+    const int th = rr / TW, tw = rr - th * TW;
+    hbase[i] = img * HH2 * HW2 + th * HW2 + tw;
+  }
+  const int rsw = (lane >> 2) & 3;  // row-major weight image key of fragment row (lane & 31)
+  auto compute = [&](int hb, int slot, int shift) {
+    const unsigned char* Hs = smem + H_OFF + hb * 2 * H_PL;
+    const unsigned char* Bs = smem + B_OFF + slot * 2 * B_PL;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int hr = hbase[i] + shift;
+        const unsigned char* a = Hs + hr * 64 + (((ks * 2 + h) ^ ((hr >> 2) & 3)) << 4);
+        ah[i] = *reinterpret_cast<const bf16x8*>(a);
+        al[i] = *reinterpret_cast<const bf16x8*>(a + H_PL);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (!BKM) {
+          const unsigned char* b = Bs + (wn0 + j * 32 + (lane & 31)) * 64 + (((ks * 2 + h) ^ rsw) << 4);
+          bh[j] = *reinterpret_cast<const bf16x8*>(b);
+          bl[j] = *reinterpret_cast<const bf16x8*>(b + B_PL);
+        } else {
+          const int kr = ks * 16 + 8 * h + q;
+          const int f = SS > 1 ? (kr / SD) & (SS - 1) : 0;
+          const int col = (wn0 + j * 32 + 16 * (g & 1) + 4 * pp) ^ (f << 5);
+          const bf16_t* b0p = reinterpret_cast<const bf16_t*>(Bs) + kr * BN + col;
+          bh[j] = tr_frag(b0p, b0p + 4 * BN);
+          bl[j] = tr_frag(b0p + B_PL / 2, b0p + B_PL / 2 + 4 * BN);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+
+  // issue order: halo(0), w(0) [, w(1)] | step s: [wait, barrier] w(s+NBS-1), (HB 2, tap 0)
+  // halo(c+1), MFMAs; HB 1: a chunk start first retires the old halo's reads (barrier), loads
+  // the new one and waits for everything
+  issue_halo(0, 0);
+  issue_w(0, 0);
+  if constexpr (NBS == 3) issue_w(1, 1);
+  int c = 0, tap = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    if constexpr (HB == 2) {
+      // w(s) and halo(c) are older than every DMA still allowed in flight: w(s+1) always, and
+      // halo(c+1) at taps 1 and 2 (issued at tap 0 right after w(s+2))
+      if (tap == 1 || tap == 2)
+        hwait_vm<GB + GH>();
+      else
+        hwait_vm<GB>();
+    } else {
+      if (tap == 0 && c > 0) {
+        __builtin_amdgcn_s_barrier();
+        issue_halo(c, 0);
+        hwait_vm<0>();
+      } else {
+        hwait_vm<GB*(NBS - 2)>();
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    issue_w(s + NBS - 1, (s + NBS - 1) % NBS);
+    if constexpr (HB == 2)
+      if (tap == 0) issue_halo(c + 1, (c + 1) & 1);
+    const int dh = tap / 3;
+    compute(HB == 2 ? (c & 1) : 0, s % NBS, dh * HW2 + (tap - dh * 3));
+    if (++tap == 9) {
+      tap = 0;
+      ++c;
+    }
+  }
+  hwait_vm<0>();
+
+  nt_f32_epilogue<TM, TN, NW>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
+}
+
+template <int IMG, int TH, int TW, int BN, int WM, int WN, int HB, int NBS>
+void launch_halo(const ConvNTParams& p, int K, hipStream_t s) {
+  const int tilesM = IMG == 1 ? p.B * (p.OH / TH) : p.B / IMG;
+  const int grid = K * tilesM * cdiv(p.N, BN);
+  if (p.b_kmajor)
+    hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, true, 1, HB, NBS>), dim3(grid), dim3(WM * WN * 64),
+                       0, s, p);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, false, 1, HB, NBS>), dim3(grid),
+                       dim3(WM * WN * 64), 0, s, p);
+}
+
+int g_halo_mode = -1;  // -1 shape rule, 0 never, 1 whenever supported (tests / A-B)
+int g_halo_variant = -1;
+
+}  // namespace
+
+void conv_halo_set_mode(int m) { g_halo_mode = m; }
+void conv_halo_set_variant(int v) { g_halo_variant = v; }
+
+// one of the compiled tile shapes fits this launch: full-width row blocks of 256 GEMM rows
+static int halo_config(const ConvNTParams& p) {
+  if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.pad_w != 1 || p.dil != 1) return -1;
+  if (p.OH != p.H || p.OW != p.W || p.out_s > 1 || p.C % 32 || p.N % 8 || p.ldx % 8 || p.R != 9 * p.C) return -1;
+  if (p.x_lo == 0 || p.wsplit == nullptr || p.rep != 1) return -1;
+  if (p.OW == 32 && p.OH % 8 == 0 && p.N <= 64) return 0;  // 1 × 8 × 32, BN 64
+  if (p.OW == 16 && p.OH == 16) return 1;                   // 1 × 16 × 16, BN 128
+  if (p.OW == 8 && p.OH == 8 && p.B % 2 == 0) return 2;     // 2 × 8 × 8, BN 128
+  // (4 × 4 images: the 256 x 256 implicit-GEMM tile of conv_pl.hip is as fast forward and faster
+  // in dgrad — l4 387 / 310 vs 385 / 331 TFLOP/s — so the halo shape serves it only on request)
+  if (p.OW == 4 && p.OH == 4 && p.B % 8 == 0 && g_halo_mode == 1) return 3;  // 8 × 4 × 4, BN 128
+  return -1;
+}
+
+bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
+  if (g_halo_mode == 0) return false;
+  const int cfg = halo_config(p);
+  if (cfg < 0) return false;
+  const long ab = (p.x_lo + (long)p.B * p.H * p.W * p.ldx) * 2;
+  const long wb = (p.ws_plane + (p.b_kmajor ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R)) * 2;
+  if (ab >= (long)OOB_OFF || wb >= (long)OOB_OFF) return false;
+  // variants (bench/kernel_bench.py --planes sweeps them): 0 = two halo buffers + 3 weight slots;
+  // 1 / 2 = one halo buffer (two workgroups per CU where the LDS allows), 8 waves
+  // measured (kernel_bench --f32 --planes, 50 clients; fwd / dgrad TFLOP/s vs the implicit-GEMM
+  // plane kernels): l1 v1 302 / 275 (259 / 247), l2 v1 441 / 396 (338 / 310), l3 v2 409 / 344
+  // (361 / 321)
+  const int v = g_halo_variant >= 0 ? g_halo_variant : (cfg == 2 ? 2 : 1);
+  switch (cfg * 3 + v) {
+    case 0: launch_halo<1, 8, 32, 64, 4, 1, 2, 3>(p, K, s); break;    // 120 KB, 4 waves
+    case 1: launch_halo<1, 8, 32, 64, 4, 2, 1, 3>(p, K, s); break;    // 73 KB, 8 waves
+    case 2: launch_halo<1, 8, 32, 64, 4, 2, 2, 3>(p, K, s); break;    // 121 KB
+    case 3: launch_halo<1, 16, 16, 128, 4, 2, 2, 3>(p, K, s); break;  // 144 KB
+    case 4: launch_halo<1, 16, 16, 128, 4, 2, 1, 2>(p, K, s); break;  // 80 KB
+    case 5: launch_halo<1, 16, 16, 128, 4, 2, 1, 3>(p, K, s); break;  // 96 KB
+    case 6: launch_halo<2, 8, 8, 128, 2, 2, 2, 3>(p, K, s); break;    // 112 KB, 4 waves
+    case 7: launch_halo<2, 8, 8, 128, 4, 2, 1, 3>(p, K, s); break;    // 80 KB, 8 waves
+    case 8: launch_halo<2, 8, 8, 128, 4, 2, 1, 2>(p, K, s); break;    // 64 KB
+    case 9: launch_halo<8, 4, 4, 128, 2, 2, 2, 3>(p, K, s); break;    // 144 KB, 4 waves
+    case 10: launch_halo<8, 4, 4, 128, 4, 2, 1, 3>(p, K, s); break;   // 96 KB, 8 waves
+    case 11: launch_halo<8, 4, 4, 128, 4, 2, 1, 2>(p, K, s); break;   // 80 KB
+    default: return false;
+  }
+  return true;
+}

@@ -285,10 +285,15 @@ bool conv_nt_pl_supported(const ConvNTParams& p) {
          p.N % 8 == 0 && (p.R == p.KH * p.KW * p.C || p.R == 0);
 }
 
+// measured (bench/kernel_bench.py --f32 --planes, ResNet-18 layers at 50 clients): N <= 64 the
+// 256x64 tile (l1 fwd / dgrad 253 / 238 TFLOP/s vs 168 / 165 for 128x128); N >= 512 the 256x256
+// tile (l4 354 / 297 vs 333 / 278); otherwise 128x128 at 2 blocks per CU (l3 331 / 291 vs 309 /
+// 249 for 256x128)
 int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
   (void)K;
-  if (p.N <= 64) return 2;  // 256x64
-  return 0;                 // 256x128
+  if (p.N <= 64) return 2;
+  if (p.N >= 512) return 3;
+  return 1;
 }
 
 bool conv_nt_pl(const ConvNTParams& p, int K, int variant, hipStream_t s) {

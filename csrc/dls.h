@@ -156,6 +156,10 @@ bool conv_nt_pl(const ConvNTParams& p, int K, int variant, hipStream_t s);
 int conv_nt_pl_num_variants();
 int conv_nt_pl_variant();           // -1: shape heuristic (set by benchmarks)
 void conv_nt_pl_set_variant(int v);
+// 3x3 stride-1 split-plane conv with LDS halo reuse (conv_halo.hip): false = shape not covered
+bool conv_halo(const ConvNTParams& p, int K, hipStream_t s);
+void conv_halo_set_mode(int m);  // -1 shape rule, 0 never, 1 whenever supported
+void conv_halo_set_variant(int v);  // -1 default, 0..2 pipeline / tile variant (benchmarks)
 bool conv_tn_pl_supported(const ConvTNParams& p);
 bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_pl_num_variants();
@@ -176,7 +180,8 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
             uint8_t* relu_mask, unsigned* counters, int f32, hipStream_t s,
             int ldx = 0, const float* pre_part = nullptr,
-            int pre_nparts = 0);  // relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused
+            int pre_nparts = 0, bf16_t* yp = nullptr,
+            int y_f32 = 1);  // yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused
                                   // coefs); ldx: row stride of x / res (channel slice of a wider buffer), y
                                   // contiguous; pre_part: [K][pre_nparts][2C] Σx / Σx² partials from the
                                   // producing conv's epilogue (ConvNTParams::stats) — no statistics pass
@@ -184,7 +189,8 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
             float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, unsigned* counters, int f32,
             hipStream_t s, int ldx = 0,
-            int acc_dx = 0);  // relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
+            int acc_dx = 0, bf16_t* dxp = nullptr,
+            int dx_f32 = 1);  // dxp / dx_f32: split planes of dX (fp32, contiguous) with or without dX; relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
                               // stride ldx, acc_dx: dx += (DenseNet block-buffer gradient)
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
             long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s);

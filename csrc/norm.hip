@@ -330,12 +330,42 @@ void launch_coef(dim3 grid, hipStream_t s, A... args) {
     hipLaunchKernelGGL((bn_coef_kernel<TT, PT, 8>), grid, dim3(32 * 8), 0, s, args...);
 }
 
+// V fp32 values → their split-bf16 planes (hi = bf16(v), lo = bf16(v − hi), RNE): the operand form
+// of the pre-split GEMMs (conv_pl.hip), bit-identical to the split those GEMMs would do themselves
+template <int V>
+__device__ __forceinline__ void store_planes(bf16_t* hi, bf16_t* lo, const float* f) {
+  if constexpr (V % 2 == 0) {
+    uint32_t h[V / 2], l[V / 2];
+#pragma unroll
+    for (int i = 0; i < V / 2; ++i) split_pair(f[2 * i], f[2 * i + 1], h[i], l[i]);
+    if constexpr (V == 8) {
+      *reinterpret_cast<uint4*>(hi) = make_uint4(h[0], h[1], h[2], h[3]);
+      *reinterpret_cast<uint4*>(lo) = make_uint4(l[0], l[1], l[2], l[3]);
+    } else if constexpr (V == 4) {
+      *reinterpret_cast<uint2*>(hi) = make_uint2(h[0], h[1]);
+      *reinterpret_cast<uint2*>(lo) = make_uint2(l[0], l[1]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        reinterpret_cast<uint32_t*>(hi)[i] = h[i];
+        reinterpret_cast<uint32_t*>(lo)[i] = l[i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) split2(f[i], hi[i], lo[i]);
+  }
+}
+
 // thread owns one V-channel chunk and strides over rows; grid (row-blocks, K)
+// yp (fp32 only): also / instead (y_f32 = 0) write the output's split planes, client k's hi plane
+// at yp + 2·k·R·C, its lo plane R·C elements later (the [K][2][R][C] layout of ops split_planes)
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                        T* __restrict__ y, const int* __restrict__ valid_rows,
                                                        const float* __restrict__ coef, int R, int C, int relu,
-                                                       int rpb, uint8_t* __restrict__ rmask, int ldx) {
+                                                       int rpb, uint8_t* __restrict__ rmask, int ldx,
+                                                       bf16_t* __restrict__ yp, int y_f32) {
   // x / res rows at stride ldx (channel slice of a wider buffer), y contiguous
   const int k = blockIdx.y;
   const int CT = C / V;
@@ -383,7 +413,11 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
         for (int j = 0; j < V; ++j) m |= (rt<T>(out[j]) > 0.f ? 1u : 0u) << j;
         rmask[((long)k * R + r) * (C / 8) + c0 / 8] = (uint8_t)m;
       }
-      store_vec<V>(y + off, out);
+      if (y_f32) store_vec<V>(y + off, out);
+      if (yp) {
+        bf16_t* hp = yp + (long)k * R * C + off;  // (off includes k·R·C: hi at 2·k·R·C + r·C + c)
+        store_planes<V>(hp, hp + (long)R * C, out);
+      }
     }
   }
 }
@@ -395,7 +429,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ coef, int R, int C, int relu,
                                                            T* __restrict__ dx, T* __restrict__ dpre,
                                                            int rpb, const uint8_t* __restrict__ rmask, int ldx,
-                                                           int acc_dx) {
+                                                           int acc_dx, bf16_t* __restrict__ dxp, int dx_f32) {
+  // dxp (fp32, contiguous dx, no acc_dx): dX's split planes ([K][2][R][C]), with or without
+  // (dx_f32 = 0) the fp32 dX
   // x and dx rows at stride ldx (channel slice of a wider buffer); acc_dx: dx += (DenseNet: the
   // block buffer's gradient collects every later layer's contribution); dy / y / dpre contiguous
   const int k = blockIdx.y;
@@ -450,7 +486,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
         for (int j = 0; j < V; ++j) o[j] += prev[j];
       }
-      store_vec<V>(dx + offx, o);
+      if (dx_f32) store_vec<V>(dx + offx, o);
+      if (dxp) {
+        bf16_t* hp = dxp + (long)k * R * C + off;
+        store_planes<V>(hp, hp + (long)R * C, o);
+      }
       if (dpre) store_vec<V>(dpre + off, gp);
     }
   }
@@ -586,7 +626,7 @@ long bn_workspace_floats(int K, long R, int C) {
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
             uint8_t* rmask, unsigned* counters, int f32, hipStream_t s, int ldx, const float* pre_part,
-            int pre_nparts) {
+            int pre_nparts, bf16_t* yp, int y_f32) {
   if (ldx == 0) ldx = C;
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
   float* coef = ws;
@@ -617,14 +657,19 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
                              (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
     }
     DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
-                                     valid_rows, coef, R, C, relu, rpb, rmask, ldx));
+                                     valid_rows, coef, R, C, relu, rpb, rmask, ldx, f32 ? yp : nullptr,
+                                     f32 ? y_f32 : 1));
   });
 }
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
             float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s,
-            int ldx, int acc_dx) {
+            int ldx, int acc_dx, bf16_t* dxp, int dx_f32) {
+  if (!f32 || acc_dx || (ldx != 0 && ldx != C)) {  // planes: fp32, contiguous dX only
+    dxp = nullptr;
+    dx_f32 = 1;
+  }
   if (ldx == 0) ldx = C;
   float* coef = ws;
   float* part = ws + (long)3 * C * K;
@@ -641,7 +686,8 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
                              valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K,
                              R, C, 0.f, 1, 1);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
-                                     valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx));
+                                     valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx, dxp,
+                                     dx_f32));
   });
 }
 

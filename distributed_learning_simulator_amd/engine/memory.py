@@ -32,7 +32,7 @@ def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
         n += 4 * P
     if compute_dtype != torch.float32:
         n += torch.tensor([], dtype=compute_dtype).element_size() * P
-    elif optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "0") == "1":
+    elif optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "1") == "1":
         n += 4 * P  # pre-split (hi, lo) bf16 weight planes of the fp32 GEMMs (CohortBuffers.split)
     return n
 

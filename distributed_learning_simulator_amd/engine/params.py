@@ -148,16 +148,15 @@ class CohortBuffers:
             torch.zeros((capacity, P), dtype=compute_dtype, device=device)
             if compute_dtype != torch.float32 else None
         )
-        # DLS_WSPLIT=1, fp32 compute on the GPU: every row's weights also as (bf16 hi, bf16 lo)
-        # planes, written by the SGD kernel with θ, so the split-bf16 convolutions load the weight
-        # operand pre-split instead of splitting it in every workgroup (SGD only). Off by default:
-        # measured on the 100-client ResNet-18 round (scripts/ab_wsplit.sh) the GEMMs gain 0-5 %
-        # (dgrad l3 336 vs 319 TFLOP/s, fwd within noise) but the extra plane writes cost more:
-        # 4.86 s/round with the planes vs 4.82 s without
+        # fp32 compute on the GPU: every row's weights also as (bf16 hi, bf16 lo) planes, written
+        # by the SGD kernel with θ. They are the B operand of the split-plane GEMMs
+        # (csrc/conv_pl.hip: LDS-DMA loads, no split VALU), whose A operand — activation / dY
+        # planes — the BatchNorms write (ops.functional planes). DLS_WSPLIT=0 disables both
+        # (SGD only: the Adam kernel does not write planes)
         self.split = (
             torch.zeros((capacity, 2, P), dtype=torch.bfloat16, device=device)
             if (compute_dtype == torch.float32 and torch.device(device).type == "cuda"
-                and optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "0") == "1") else None
+                and optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "1") == "1") else None
         )
 
     @property

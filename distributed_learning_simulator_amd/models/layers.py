@@ -156,18 +156,24 @@ class BatchNorm(Module):
     def own_params(self):
         return [self.gamma, self.beta]
 
-    def forward(self, x, ctx, residual=None, relu=None, link=None, stats=None):
+    def forward(self, x, ctx, residual=None, relu=None, link=None, stats=None, planes: int = 0):
+        """`planes`: the output's consumers are split-plane convs (Fn.batch_norm): 1 = they and
+        fp32 readers, 2 = split-plane convs only. Effective while the weights' planes are live
+        (training steps with BoundParams.split); otherwise the output is plain fp32."""
         P = ctx.P
         rps = 1
         for d in x.shape[2:-1]:
             rps *= d
+        if getattr(P, "split", None) is None or self.c % 32:
+            planes = 0
         return Fn.batch_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta),
                              ctx.valid_rows(rps), self.relu if relu is None else relu, residual, link=link,
-                             stats=stats)
+                             stats=stats, planes=planes)
 
 
 def conv_bn(conv: Conv2d, bn: BatchNorm, x, ctx, conv_link=None, conv_donor=None, **bn_kw):
-    """conv → BatchNorm with the BN statistics taken from the conv's epilogue (Fn.BNStats)."""
+    """conv → BatchNorm with the BN statistics taken from the conv's epilogue (Fn.BNStats) and,
+    for fp32 split-plane GEMMs, the BN backward handing the conv only dX's planes."""
     st = Fn.BNStats(ctx.valid)
     return bn.forward(conv.forward(x, ctx, link=conv_link, stats=st, donor=conv_donor), ctx, stats=st, **bn_kw)
 

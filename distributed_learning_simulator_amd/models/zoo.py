@@ -118,10 +118,12 @@ class BasicBlock(Module):
 
     def forward(self, x, ctx):
         link = _residual_link(self, x, ctx)
-        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link)
+        # split planes (fp32 GEMMs, Fn.batch_norm): bn1's output feeds conv2 only; the block
+        # output feeds the next block's convs and its shortcut
+        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link, planes=2)
         sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
         return conv_bn(self.conv2, self.bn2, out, ctx, residual=sc, relu=True,
-                       link=link if self.down is None else None)
+                       link=link if self.down is None else None, planes=1)
 
 
 class Bottleneck(Module):
@@ -143,11 +145,11 @@ class Bottleneck(Module):
 
     def forward(self, x, ctx):
         link = _residual_link(self, x, ctx)
-        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link)
-        out = conv_bn(self.conv2, self.bn2, out, ctx)
+        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link, planes=2)
+        out = conv_bn(self.conv2, self.bn2, out, ctx, planes=2)
         sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
         return conv_bn(self.conv3, self.bn3, out, ctx, residual=sc, relu=True,
-                       link=link if self.down is None else None)
+                       link=link if self.down is None else None, planes=1)
 
 
 class ResNetNet(Module):
@@ -176,7 +178,7 @@ class ResNetNet(Module):
         self.child("fc", Linear(c, classes))
 
     def forward(self, x, ctx):
-        x = conv_bn(self.conv1, self.bn1, x, ctx)
+        x = conv_bn(self.conv1, self.bn1, x, ctx, planes=0 if not self.cifar_stem else 1)
         if not self.cifar_stem:
             x = self.maxpool.forward(x, ctx)
         for s in self.stages:

@@ -46,16 +46,42 @@ DENSE_STATS_CACHE = os.environ.get("DLS_DENSE_STATS_CACHE", "0") == "1"
 
 
 class BNStats:
-    """Hands a BatchNorm's batch statistics from the conv that produces its input: the fp32 conv
-    epilogue writes per-32-row Σy / Σy² partials (of the first `valid[k]` samples' rows) and the
-    BN consumes them instead of re-reading y in a statistics pass. `part` stays None when the
-    producing conv could not provide them (CPU oracle, bf16 kernels, LDS-DMA path)."""
+    """Links a conv to the BatchNorm that consumes its output:
+    - statistics: the fp32 conv epilogue writes per-32-row Σy / Σy² partials (of the first
+      `valid[k]` samples' rows) and the BN consumes them instead of re-reading y in a statistics
+      pass. `part` stays None when the producing conv could not provide them (CPU oracle, bf16
+      kernels, LDS-DMA path);
+    - `dy_planes_ok`: the conv runs its dgrad and wgrad on split planes (csrc/conv_pl.hip), so
+      the BN backward writes only dX's planes (ops.hip.bn_bwd dx_planes=2), never the fp32 dX."""
 
-    __slots__ = ("valid", "part")
+    __slots__ = ("valid", "part", "dy_planes_ok")
 
     def __init__(self, valid=None):
         self.valid = valid
         self.part = None
+        self.dy_planes_ok = False
+
+
+# Split-plane operands (csrc/conv_pl.hip). A tensor produced together with its bf16 (hi, lo)
+# planes carries them as attribute `_dls_planes` ([K, 2, *shape[1:]], ops.hip.planes_buffer
+# layout); `_dls_planes_only` marks a tensor whose fp32 bytes ARE those planes (the producer
+# wrote nothing else) — only a planes-reading GEMM may consume it. DLS_PLANES=0 disables.
+PLANES = os.environ.get("DLS_PLANES", "1") != "0"
+
+
+def _planes_of(t):
+    return getattr(t, "_dls_planes", None)
+
+
+def _tag_planes(t, planes, only: bool):
+    t._dls_planes = planes
+    t._dls_planes_only = only
+    return t
+
+
+def _require_fp32(t, who: str):
+    if getattr(t, "_dls_planes_only", False):
+        raise RuntimeError(f"{who}: a planes-only activation reached an op that reads fp32 values")
 
 
 class _Conv(torch.autograd.Function):
@@ -72,6 +98,16 @@ class _Conv(torch.autograd.Function):
             w_split = None  # (the padded copy has no planes)
         if be is ref or x.dtype != torch.float32:
             w_split = None
+        # split-plane GEMMs: x's planes (from the producing BN) + the weight planes
+        xp = _planes_of(x)
+        use_pl = (xp is not None and w_split is not None and x.is_contiguous()
+                  and be.conv_planes_ok(x.shape[-1], w.shape[1]))
+        if getattr(x, "_dls_planes_only", False) and not use_pl:
+            raise RuntimeError("conv2d: planes-only input but the split-plane GEMM cannot run here")
+        pl = {"x_planes": xp} if use_pl else {}
+        ctx.xp = xp if use_pl else None
+        if stats is not None:
+            stats.dy_planes_ok = use_pl and b is None
         if stats is not None and be is not ref and x.dtype == torch.float32 and EPILOGUE_BN_STATS:
             K, B, H, W = x.shape[:4]
             KH = w.shape[2]
@@ -79,9 +115,9 @@ class _Conv(torch.autograd.Function):
             stats.part = torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
                                      device=x.device)
             y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid,
-                            **({"w_split": w_split} if w_split is not None else {}))
+                            **({"w_split": w_split} if w_split is not None else {}), **pl)
         elif w_split is not None:
-            y = be.conv_fwd(x, w, stride, pad, bias=b, w_split=w_split)
+            y = be.conv_fwd(x, w, stride, pad, bias=b, w_split=w_split, **pl)
         else:
             y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.w_split = w_split
@@ -103,8 +139,16 @@ class _Conv(torch.autograd.Function):
             link.grad = None
             if acc is None:
                 link.receiver_done = True  # (a late donor hands its dX to autograd instead)
+        dyp = _planes_of(dy)
+        if dyp is not None and ctx.xp is None:
+            raise RuntimeError("conv2d backward: dY planes without the input's planes")
+        if dyp is None:
+            _require_fp32(dy, "conv2d backward")
         if ctx.needs_input_grad[0]:
-            if ctx.w_split is not None:
+            if dyp is not None:
+                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split,
+                                   dy_planes=dyp)
+            elif ctx.w_split is not None:
                 dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split)
             else:
                 dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc)
@@ -120,7 +164,11 @@ class _Conv(torch.autograd.Function):
                 gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (K,) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
                 if ctx.gb is not None:
                     ctx.gb.copy_(dy.float().sum(dim=(1, 2, 3)))
+            elif dyp is not None:
+                be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad, dy_planes=dyp, x_planes=ctx.xp)
             else:
+                if ctx.xp is not None and getattr(x, "_dls_planes_only", False):
+                    raise RuntimeError("conv2d backward: fp32 dY with a planes-only input")
                 be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad)
                 if ctx.gb is not None:
                     be.bias_grad(dy, ctx.gb)
@@ -252,26 +300,40 @@ def linear_shared_input(x, token, w, gw):
 # ------------------------------------------------------------------------ batchnorm
 class _BN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link=None, stats=None):
+    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link=None, stats=None,
+                planes=0):
         be = _be(x)
         K = x.shape[0]
         C = x.shape[-1]
+        _require_fp32(x, "batch_norm")
+        if residual is not None:
+            _require_fp32(residual, "batch_norm residual")
         x3 = x.reshape(K, -1, C)
         r3 = residual.reshape(K, -1, C) if residual is not None else None
         mask = None
+        yp = None
         if be is ref:
             y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
         else:  # native: 1-bit ReLU mask so the backward need not re-read y
             pre = stats.part if stats is not None else None
-            y, mean, rstd, mask = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True, pre_stats=pre)
+            planes = planes if (PLANES and x.dtype == torch.float32 and x.is_contiguous()) else 0
+            out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True, pre_stats=pre, planes=planes)
+            y, mean, rstd, mask = out[:4]
+            if planes:
+                yp = out[4]
             if stats is not None:
                 stats.part = None
-        ctx.save_for_backward(x3, y, mean, rstd, gamma)
+        # (y itself is only read by the backward when there is no ReLU mask)
+        ctx.save_for_backward(x3, y if mask is None else None, mean, rstd, gamma)
         ctx.relu_mask = mask
         ctx.valid_rows, ctx.relu, ctx.has_res = valid_rows, relu, residual is not None
         ctx.link = link
+        ctx.stats = stats
         ctx.ggamma, ctx.gbeta, ctx.shape = ggamma, gbeta, x.shape
-        return y.reshape(x.shape)
+        yo = y.reshape(x.shape)
+        if yp is not None:
+            _tag_planes(yo, yp.view((K, 2) + tuple(x.shape[1:])), planes == 2)
+        return yo
 
     @staticmethod
     def backward(ctx, dy):
@@ -285,18 +347,33 @@ class _BN(torch.autograd.Function):
                 ctx.ggamma.copy_(dgamma)
                 ctx.gbeta.copy_(dbeta)
         else:
-            dx, dpre = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
-                                 ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask)
+            _require_fp32(dy, "batch_norm backward")
+            # the producing conv reads dX as split planes: write only those
+            dxm = 2 if (ctx.stats is not None and ctx.stats.dy_planes_ok and PLANES) else 0
+            out = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
+                            ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask, dx_planes=dxm)
+            dx, dpre = out[0], out[1]
+            if dxm:
+                dxo = dx.reshape(ctx.shape)
+                _tag_planes(dxo, out[2].view((K, 2) + tuple(ctx.shape[1:])), True)
+                dres = dpre.reshape(ctx.shape) if ctx.has_res else None
+                if dres is not None and ctx.link is not None:
+                    ctx.link.grad = dres
+                    dres = None
+                return dxo, None, None, None, None, None, None, None, dres, None, None, None
         dres = dpre.reshape(ctx.shape) if ctx.has_res else None
         if dres is not None and ctx.link is not None:
             ctx.link.grad = dres  # delivered by the block's first conv (ResidualLink)
             dres = None
-        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres, None, None
+        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, dres, None, None, None
 
 
 def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False, residual=None,
-               link: ResidualLink | None = None, stats: BNStats | None = None):
-    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link, stats)
+               link: ResidualLink | None = None, stats: BNStats | None = None, planes: int = 0):
+    """`planes` (fp32 native): 1 = the output also carries its split planes (`_dls_planes`) for
+    the conv(s) that read it, 2 = the output is ONLY planes — for outputs read by nothing but
+    split-plane convs (e.g. a ResNet block's inner BN)."""
+    return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link, stats, planes)
 
 
 # ------------------------------------------------------------------------ layernorm

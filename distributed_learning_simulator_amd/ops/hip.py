@@ -147,10 +147,20 @@ def conv_stats_parts(M: int) -> int:
     return (M + 31) // 32
 
 
+# launches that took the split-plane GEMM path (fwd / dgrad / wgrad), for tests and reports
+planes_launches = collections.Counter()
+
+
 def planes_ok(C: int, N: int, ld: int | None = None) -> bool:
     """Shape contract of the pre-split-operand GEMMs (csrc/conv_pl.hip): a K tile of 32 never
     straddles a tap (C % 32), contiguous planes, 16-B output columns (N % 8)."""
     return C % 32 == 0 and N % 8 == 0 and (ld is None or ld == C)
+
+
+def conv_planes_ok(C: int, Co: int, ldx: int | None = None) -> bool:
+    """A conv with C input / Co output channels can run all three GEMMs on split planes:
+    forward (A = x planes, C % 32), dgrad (A = dY planes, Co % 32; output Ci % 8), wgrad."""
+    return planes_ok(C, Co, ldx) and planes_ok(Co, C)
 
 
 def split_planes(x, out=None):
@@ -214,6 +224,7 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
     xp, x_cs, x_lo = _p(x), x.stride(0), 0
     if x_planes is not None and ws_p and planes_ok(C, Co, ldx):
         xp, x_cs, x_lo = _planes_args(x_planes, x)  # LDS-DMA GEMM on pre-split operands
+        planes_launches["fwd"] += 1
     _C.conv_nt(xp, _p(w), _p(y), _p(bias), x_cs, y.stride(0), w_cs, b_cs, B, H, W, C, OH, OW, KH, KW, stride,
                pad, 1, M, Co, KH * KW * Ci, rep, int(relu), K, 0, nt_f32_variant if f32 else nt_variant, NULL, NULL, f32,
                _s(), ldx, ldy, _p(stats), _p(stats_valid), NULL, 0.0, 0.0, ws_p, ws_cs, ws_plane, x_lo)
@@ -251,6 +262,7 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
     dyp, dy_cs, dy_lo = _p(dy), dy.stride(0), 0
     if dy_planes is not None and ws_p and planes_ok(Co, Ci, ld_dy):
         dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
+        planes_launches["dgrad"] += 1
     _C.conv_dgrad(dyp, _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
                   nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy_cs, ws_p, ws_cs, ws_plane, dy_lo)
     return dx
@@ -282,6 +294,7 @@ def _tn_launch(dy, x, gw, dy_cs, x_cs, B, H, W, C, OH, OW, KH, KW, stride, pad, 
     if planes:
         dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
         xp, x_cs, x_lo = _planes_args(x_planes, x)
+        planes_launches["wgrad"] += 1
     splitk = _C.conv_tn_splitk(K, Co, R, M, C, tv, f32, ldy, ldx, int(planes))
     part = NULL
     if splitk > 1:
@@ -401,17 +414,38 @@ def linear_wgrad(dy, x, gw, gb=None):
 
 
 # ------------------------------------------------------------------------ batchnorm
-def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False, pre_stats=None):
+def planes_buffer(shape, device):
+    """(fp32 tensor of `shape`, its bytes as [K, 2, *shape[1:]] bf16 split planes): client k's
+    hi plane then lo plane occupy exactly the bytes of its fp32 row, so a producer that writes
+    only the planes can hand autograd the fp32-typed alias (consumers read `_dls_planes`)."""
+    buf = torch.empty(shape, dtype=F32, device=device)
+    K = shape[0]
+    return buf, buf.view(K, -1).view(BF16).view((K, 2) + tuple(shape[1:]))
+
+
+def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False, pre_stats=None,
+           planes: int = 0):
     """Returns (y, mean, rstd); with_mask=True (ReLU, C % 8 == 0) also returns the 1-bit ReLU
     mask [K, R, C/8] uint8 that bn_bwd can read instead of y. `x` (and `residual`) may be
     channel slices of a wider buffer ([K, R, C] at row stride ld); y is contiguous.
     `pre_stats`: [K, parts, 2, C] Σx / Σx² partials written by the producing conv's epilogue
-    (conv_fwd(stats=)) — the statistics pass over x is skipped."""
+    (conv_fwd(stats=)) — the statistics pass over x is skipped.
+    `planes` (fp32): 1 = also write y's split planes, 2 = write only the planes (y is then their
+    fp32-typed alias, see planes_buffer); the planes [K, 2, R, C] are returned last."""
     K, R, C = x.shape
     x, ldx = _pix_stride(x)
     assert x.stride(0) == R * ldx, "client stride of a strided BN input must be R*ld"
     g_cs, rep = _client_view(gamma, K)
-    y = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
+    yp = None
+    if planes and x.dtype == F32:
+        if planes == 2:
+            y, yp = planes_buffer((K, R, C), x.device)
+        else:
+            y = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
+            yp = torch.empty((K, 2, R, C), dtype=BF16, device=x.device)
+    else:
+        planes = 0
+        y = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
     mean = torch.empty((K, C), dtype=torch.float32, device=x.device)
     rstd = torch.empty((K, C), dtype=torch.float32, device=x.device)
     ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
@@ -428,15 +462,17 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
     assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
               eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx, _p(pre_stats),
-              0 if pre_stats is None else pre_stats.shape[1])
-    if with_mask:
-        return y, mean, rstd, mask
-    return y, mean, rstd
+              0 if pre_stats is None else pre_stats.shape[1], _p(yp), int(planes != 2))
+    out = (y, mean, rstd, mask) if with_mask else (y, mean, rstd)
+    return out + (yp,) if planes else out
 
 
-def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None):
+def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None,
+           dx_planes: int = 0):
     """`dx_out`: a channel slice of a wider gradient buffer (same strides as `x`) that dX is ADDED
-    into (DenseNet block-buffer gradient); otherwise dX is returned contiguous."""
+    into (DenseNet block-buffer gradient); otherwise dX is returned contiguous. `dx_planes`
+    (fp32, contiguous, no dx_out): 1 = also write dX's split planes, 2 = only the planes (dX is
+    their fp32-typed alias); the planes [K, 2, R, C] are then returned as a third value."""
     K, R, C = x.shape
     x, ldx = _pix_stride(x)
     assert x.stride(0) == R * ldx
@@ -449,7 +485,17 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
         dx = dx_out
     else:
         assert ldx == C, "strided x needs a strided dx_out"
-        dx = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
+    dxp = None
+    if dx_planes and dx_out is None and x.dtype == F32:
+        if dx_planes == 2:
+            dx, dxp = planes_buffer((K, R, C), x.device)
+        else:
+            dx = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
+            dxp = torch.empty((K, 2, R, C), dtype=BF16, device=x.device)
+    else:
+        dx_planes = 0
+        if dx_out is None:
+            dx = torch.empty((K, R, C), dtype=x.dtype, device=x.device)
     dpre = torch.empty((K, R, C), dtype=x.dtype, device=x.device) if need_dpre else None
     ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
@@ -457,7 +503,9 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     assert dy.dtype == x.dtype == gamma.dtype
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
               _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx,
-              int(dx_out is not None))
+              int(dx_out is not None), _p(dxp), int(dx_planes != 2))
+    if dx_planes:
+        return dx, dpre, dxp
     return dx, dpre
 
 

@@ -127,3 +127,25 @@ def test_densenet40_session_matches_cpu(hip, tmp_path):
     gl, cl = _losses(gr), _losses(cr)
     assert abs(gl[0] - cl[0]) < 1e-3, (gl, cl)
     assert _rel(gs.server.global_parameter, cs.server.global_parameter) < 2e-3
+
+
+def test_resnet18_bitwise_reproducible_and_planes(hip, tmp_path, monkeypatch):
+    """Deterministic GPU training: two identical ResNet-18 GPU runs give
+    bitwise-equal global models (split-K weight gradients folded in order, no atomics), and the
+    split-plane GEMM path (csrc/conv_pl.hip, planes written by the BatchNorms) agrees with the
+    register-staged split path to fp32 noise."""
+    from distributed_learning_simulator_amd.ops import functional as Fn
+
+    from distributed_learning_simulator_amd.ops import hip as H
+
+    ov = {"round": 1, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
+          "learning_rate": 0.01}
+    H.planes_launches.clear()
+    a, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    # every ResNet-18 conv but the stem runs its three GEMMs on split planes
+    assert min(H.planes_launches[k] for k in ("fwd", "dgrad", "wgrad")) > 0, H.planes_launches
+    b, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    assert torch.equal(a.server.global_parameter, b.server.global_parameter)
+    monkeypatch.setattr(Fn, "PLANES", False)
+    c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
+    assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4

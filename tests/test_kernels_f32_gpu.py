@@ -542,3 +542,43 @@ def test_wgrad_planes_every_variant(hip, case):
             assert torch.equal(ga, gb), f"variant {v} not reproducible"
     finally:
         hip._C.conv_tn_pl_set_variant(-1)
+
+
+@pytest.mark.parametrize("case", [
+    # K, B, H, Ci, Co  (3x3, stride 1, pad 1, H = W): one case per compiled halo tile shape
+    (2, 2, 32, 32, 64),     # 1 x 8 x 32 rows, BN 64
+    (2, 2, 16, 64, 128),    # 1 x 16 x 16, BN 128
+    (2, 4, 8, 64, 96),      # 2 x 8 x 8, BN 128 (N tail)
+    (3, 8, 4, 128, 128),    # 8 x 4 x 4
+])
+def test_conv_halo(hip, case):
+    """3x3 stride-1 split-plane conv with LDS halo reuse (csrc/conv_halo.hip): forward and
+    dgrad (+acc) within 1e-5 of the fp64 oracle and close to the implicit-GEMM plane kernel
+    (different K-loop order: chunk-major instead of tap-major)."""
+    K, B, H, Ci, Co = case
+    torch.manual_seed(11)
+    x = _f(K, B, H, H, Ci)
+    w = _f(K, Co, 3, 3, Ci, scale=0.2)
+    ws = _wsplit(hip, w)
+    dy = _f(K, B, H, H, Co)
+    acc = _f(K, B, H, H, Ci)
+    xp, dyp = hip.split_planes(x), hip.split_planes(dy)
+    outs = {}
+    try:
+        for mode, v in ((1, 0), (1, 1), (1, 2), (0, -1)):
+            hip._C.conv_halo_set_mode(mode)
+            hip._C.conv_halo_set_variant(v)
+            outs[(mode, v)] = (hip.conv_fwd(x, w, 1, 1, w_split=ws, x_planes=xp),
+                               hip.conv_dgrad(dy, w, (H, H), 1, 1, acc=acc, w_split=ws, dy_planes=dyp))
+    finally:
+        hip._C.conv_halo_set_mode(-1)
+        hip._C.conv_halo_set_variant(-1)
+    y_ref = ref.conv_fwd(_d(x), _d(w), 1, 1)
+    dx_ref = ref.conv_dgrad(_d(dy), _d(w), (H, H), 1, 1) + _d(acc)
+    for key, (y, dx) in outs.items():
+        _close(y, y_ref)
+        _close(dx, dx_ref)
+    for key in ((1, 1), (1, 2)):  # every halo variant: same K order, bitwise equal
+        assert torch.equal(outs[key][0], outs[(1, 0)][0]) and torch.equal(outs[key][1], outs[(1, 0)][1])
+    _close(outs[(1, 0)][0], outs[(0, -1)][0].double(), tol=2e-6)
+    _close(outs[(1, 0)][1], outs[(0, -1)][1].double(), tol=2e-6)
