@@ -113,9 +113,10 @@ def main() -> None:
         if int(os.environ.get("RANK", "0")) == 0:
             build.build()
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            # wait for rank 0's (no-op or incremental) build before other ranks import
-            while not os.path.exists(build.TARGET):
-                time.sleep(1)
+            # every rank waits until the in-tree binary is linked from THESE sources (rank 0's
+            # no-op or incremental build writes the content-hash stamp last), so no rank can
+            # import a stale .so while rank 0 replaces it
+            build.wait_current()
 
     comm = init_distributed()
     emulated = args.emulate_world > 1
@@ -165,6 +166,9 @@ def main() -> None:
         progress("timed")
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    # the timed rounds' metrics rows, taken before any stage-2 round appends its own (FedOBD:
+    # per-round comm bytes / phases / accuracy describe stage 1 only; stage 2 is reported apart)
+    rows = sess.metrics[m0:]
     stage2 = None
     if wl.get("stage2") and not args.no_stage2:
         # FedOBD: the timed rounds above are stage 1; the whole second phase (all clients,
@@ -175,10 +179,12 @@ def main() -> None:
             theta = sess.run_one_round(theta)
             progress("stage2")
         barrier_sync()
-        stage2 = {"seconds": time.perf_counter() - t1, "epochs": len(sess.metrics) - m1,
+        s2 = sess.metrics[m1:]
+        stage2 = {"seconds": time.perf_counter() - t1, "epochs": len(s2),
                   "clients": cfg.worker_number,
-                  "comm_bytes": sum(r["comm_bytes_total"] for r in sess.metrics[m1:]),
-                  "test_accuracy": sess.metrics[-1].get("test_accuracy") if len(sess.metrics) > m1 else None}
+                  "comm_bytes": sum(r["comm_bytes_total"] for r in s2),
+                  "comm_bytes_per_epoch": sum(r["comm_bytes_total"] for r in s2) / max(len(s2), 1),
+                  "test_accuracy": s2[-1].get("test_accuracy") if s2 else None}
     if comm.world > 1 and not emulated:
         t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -187,7 +193,6 @@ def main() -> None:
             t[0] = stage2["seconds"]
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             stage2["seconds"] = float(t.item())
-    rows = sess.metrics[m0:]
     bytes_per_round = sum(r["comm_bytes_total"] for r in rows) / max(len(rows), 1)
     acc = rows[-1].get("test_accuracy") if rows else None
     if comm.rank == 0:

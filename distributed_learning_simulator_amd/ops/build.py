@@ -3,7 +3,8 @@
     python -m distributed_learning_simulator_amd.ops.build [--force] [-j N]
 
 Each `csrc/*.hip` is compiled to an object (incremental, by mtime), `csrc/bindings.cpp`
-(pybind11) likewise, and everything is linked into
+(pybind11) likewise, and everything is linked — with a generated unit holding the sources'
+content hash (`source_hash()`, checked at import by ops/hip.py) — into
 `distributed_learning_simulator_amd/_dls_hip<EXT_SUFFIX>` — in-tree so it travels with the
 repo snapshot to the GPU box. The .so links libamdhip64.so.7 by SONAME; importing torch first
 makes it bind to torch's bundled HIP runtime (one runtime per process).
@@ -13,10 +14,12 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
 import sysconfig
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(ROOT, "csrc")
@@ -54,13 +57,48 @@ def _compile(src: str, obj: str, extra: list[str]) -> tuple[str, str]:
     return src, r.stderr
 
 
+STAMP = TARGET + ".srchash"  # content hash of the sources the in-tree .so was linked from
+
+
+def source_hash() -> str:
+    """Content hash of everything that determines the binary: every csrc/ file (name + bytes),
+    the compiler flags and the target arch. Compiled INTO the extension (`_C.src_hash()`) and
+    checked at import (ops/hip.py), so a binary built from other sources never runs silently."""
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        h.update(f.encode() + b"\0")
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(repr((COMMON_FLAGS, sorted(FILE_FLAGS.items()), ARCH)).encode())
+    return h.hexdigest()[:20]
+
+
+def is_current() -> bool:
+    """The in-tree extension exists and was linked from the current sources (its stamp)."""
+    try:
+        with open(STAMP) as fh:
+            return os.path.exists(TARGET) and fh.read().strip() == source_hash()
+    except OSError:
+        return False
+
+
+def wait_current(timeout: float = 1800.0) -> None:
+    """Block until is_current() (another rank is building), or raise after `timeout` s."""
+    t0 = time.time()
+    while not is_current():
+        if time.time() - t0 > timeout:
+            raise TimeoutError(f"extension not rebuilt from the current sources within {timeout:.0f} s")
+        time.sleep(1.0)
+
+
 def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     import pybind11
 
-    sources = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    if not force and os.path.exists(TARGET) and all(os.path.getmtime(s) <= os.path.getmtime(TARGET) for s in sources):
+    if not force and is_current():
         return TARGET  # up to date (object files need not be present, e.g. on a GPU box snapshot)
     os.makedirs(BUILD, exist_ok=True)
+    digest = source_hash()
     py_inc = sysconfig.get_paths()["include"]
     units = []
     for f in sorted(os.listdir(CSRC)):
@@ -80,14 +118,24 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
                     print("compiled", os.path.basename(src), file=sys.stderr)
                 if err.strip() and verbose:
                     print(err, file=sys.stderr)
-    objs = [u[1] for u in units]
-    if force or todo or not os.path.exists(TARGET) or any(os.path.getmtime(o) > os.path.getmtime(TARGET) for o in objs):
-        tmp = TARGET + ".tmp"
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, TARGET)
+    # the source hash as a one-line translation unit linked into the extension
+    hsrc = os.path.join(BUILD, "srchash.cpp")
+    with open(hsrc, "w") as fh:
+        fh.write(f'extern "C" const char* dls_src_hash() {{ return "{digest}"; }}\n')
+    hobj = os.path.join(BUILD, "srchash.o")
+    r = subprocess.run(["g++", "-O2", "-fPIC", "-c", hsrc, "-o", hobj], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"srchash compile failed: {r.stderr}")
+    objs = [u[1] for u in units] + [hobj]
+    tmp = TARGET + ".tmp"
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, TARGET)
+    with open(STAMP + ".tmp", "w") as fh:
+        fh.write(digest + "\n")
+    os.replace(STAMP + ".tmp", STAMP)  # (written last: waiters see it only after the .so is in place)
     return TARGET
 
 

@@ -23,6 +23,20 @@ except ImportError as e:  # pragma: no cover - exercised only on a GPU box witho
         f"(original error: {e})"
     ) from e
 
+
+def _check_provenance() -> None:
+    """The loaded binary must have been linked from the csrc/ sources in this tree (its
+    compiled-in content hash, ops/build.source_hash): a stale or foreign .so fails loudly."""
+    from . import build as _build
+
+    built, here = _C.src_hash(), _build.source_hash()
+    if built != here and os.environ.get("DLS_SKIP_SRC_HASH") != "1":
+        raise ImportError(f"_dls_hip was built from different sources (binary {built}, tree {here}); "
+                          "rebuild with `python -m distributed_learning_simulator_amd.ops.build`")
+
+
+_check_provenance()
+
 BF16 = torch.bfloat16
 F32 = torch.float32
 NULL = 0
