@@ -459,6 +459,23 @@ class HaloExchange:
             self.policy.observe(flat[pub_rows], self.comm)
         return torch.where(own.view(K, nmax, 1), h, vals.view(K, nmax, F))
 
+    def idle_batch(self, widths: list[int], device) -> None:
+        """A rank with no active client this round still takes part in every collective of a
+        training batch (the other ranks' all-to-alls and the fed_aas all-reduce pair with it):
+        one begin_batch, then for each exchanging layer an exchange with nothing requested and
+        nothing published."""
+        self.begin_batch()
+        for F in widths:
+            if self.last_skip:
+                continue
+            flat = torch.zeros((0, F), dtype=torch.float32, device=device)
+            table = torch.full((self.cg.N,), -1, dtype=torch.int64, device=device)
+            empty = torch.zeros(0, dtype=torch.int64, device=device)
+            if self.comm is not None and self.comm.world > 1:
+                self._exchange(flat, table, empty, empty, flat)
+            if self.policy is not None:
+                self.policy.observe(flat, self.comm)
+
     def _exchange(self, flat, table, rows, gids, vals):
         """Rows owned by clients on other ranks: ids to the owner's rank, embeddings back."""
         comm = self.comm

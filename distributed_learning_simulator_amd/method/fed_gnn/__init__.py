@@ -84,11 +84,32 @@ class GraphWorker(AggregationWorker):
         """All of this rank's clients form ONE cohort: the halo exchange couples the clients of a
         batch, and every rank runs the same batch sequence (its collectives pair up)."""
         self._round_num = round_num
-        if self._share_feature and self.session.comm.world > 1 and not client_ids:
-            raise RuntimeError("fed_gnn with share_feature needs at least one active client per rank")
         if client_ids:
             yield self.train_wave(round_num, theta_g, list(client_ids))
+        else:
+            self._idle_round(round_num)
         self._own_init = False
+
+    def _idle_round(self, round_num) -> None:
+        """This rank has no active client this round (failure_rate, random_client_number or
+        worker_number below the world size): it runs every collective of the round's training
+        with empty contributions — each batch's halo exchanges (share_feature), then the
+        embedding-byte all-reduce — so the other ranks' collectives pair up (no hang)."""
+        comm = self.session.comm
+        if comm.world <= 1:
+            return
+        if self._share_feature:
+            cg = self._client_graph()
+            halo = HaloExchange(cg, comm, self._client_ranks(), self._policy)
+            convs = self.session.model.root.convs
+            widths = [c.lin.fout for c in convs[:-1]]  # input widths of layers >= 1
+            for _ in range(self.local_epochs() * self._batch_number):
+                halo.idle_batch(widths, self.session.device)
+        t = torch.zeros(2, dtype=torch.float64, device=self.session.device)
+        comm.all_reduce_(t)
+        sent, skipped = (int(v) for v in t.cpu().tolist())
+        self._communicated_embedding_bytes += sent
+        self._skipped_embedding_bytes += skipped
 
     def build_schedule(self, round_num, wave):
         # every rank runs the same number of steps: batch size from the largest shard of all clients

@@ -101,17 +101,22 @@ class _Conv(torch.autograd.Function):
         # split-plane GEMMs: x's planes (from the producing BN) + the weight planes
         xp = _planes_of(x)
         use_pl = (xp is not None and w_split is not None and x.is_contiguous()
-                  and be.conv_planes_ok(x.shape[-1], w.shape[1]))
+                  and be.conv_planes_ok(x.shape[-1], w.shape[1]) and be.planes_fit(x[0].numel()))
         if getattr(x, "_dls_planes_only", False) and not use_pl:
             raise RuntimeError("conv2d: planes-only input but the split-plane GEMM cannot run here")
         pl = {"x_planes": xp} if use_pl else {}
         ctx.xp = xp if use_pl else None
         if stats is not None:
             stats.dy_planes_ok = use_pl and b is None
-        if stats is not None and be is not ref and x.dtype == torch.float32 and EPILOGUE_BN_STATS:
-            K, B, H, W = x.shape[:4]
-            KH = w.shape[2]
-            OH, OW = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - w.shape[3]) // stride + 1
+        K, B, H, W = x.shape[:4]
+        KH = w.shape[2]
+        OH, OW = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - w.shape[3]) // stride + 1
+        y_numel = B * OH * OW * w.shape[1]
+        # per-client windows past 2 GiB run batch-chunked (ops.hip): no epilogue statistics there
+        big = be is not ref and max(x[0].numel(), y_numel) * x.element_size() >= (1 << 31)
+        if stats is not None:
+            stats.dy_planes_ok = stats.dy_planes_ok and be.planes_fit(y_numel)
+        if stats is not None and be is not ref and x.dtype == torch.float32 and EPILOGUE_BN_STATS and not big:
             stats.part = torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
                                      device=x.device)
             y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid,
@@ -316,7 +321,8 @@ class _BN(torch.autograd.Function):
             y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
         else:  # native: 1-bit ReLU mask so the backward need not re-read y
             pre = stats.part if stats is not None else None
-            planes = planes if (PLANES and x.dtype == torch.float32 and x.is_contiguous()) else 0
+            planes = planes if (PLANES and x.dtype == torch.float32 and x.is_contiguous()
+                                and be.planes_fit(x[0].numel())) else 0
             out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True, pre_stats=pre, planes=planes)
             y, mean, rstd, mask = out[:4]
             if planes:

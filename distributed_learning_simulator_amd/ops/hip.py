@@ -171,6 +171,21 @@ def planes_ok(C: int, N: int, ld: int | None = None) -> bool:
     return C % 32 == 0 and N % 8 == 0 and (ld is None or ld == C)
 
 
+WINDOW = 1 << 31  # the GEMM loaders address one client's operand window with 32-bit byte offsets
+
+
+def planes_fit(numel_per_client: int) -> bool:
+    """A [K, 2, n] plane buffer fits the kernels' per-client window (hi plane + lo plane)."""
+    return numel_per_client * 4 < WINDOW
+
+
+def _batch_chunks(B: int, bytes_per_sample: int) -> list[tuple[int, int]]:
+    """Split a per-client batch so each chunk's operand window stays under 2 GiB (ADVICE r2:
+    the launchers used to abort on larger windows, e.g. ResNet-50 at 224² with batch ≥ 640)."""
+    per = max(1, (WINDOW - 1) // max(1, bytes_per_sample))
+    return [(b, min(B, b + per)) for b in range(0, B, per)]
+
+
 def conv_planes_ok(C: int, Co: int, ldx: int | None = None) -> bool:
     """A conv with C input / Co output channels can run all three GEMMs on split planes:
     forward (A = x planes, C % 32), dgrad (A = dY planes, Co % 32; output Ci % 8), wgrad."""
@@ -204,11 +219,20 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
     `stats` (fp32 only): a [K, conv_stats_parts(M), 2, Co] fp32 buffer the epilogue fills with the
     BN partial sums Σy, Σy² over the rows of the first `stats_valid[k]` samples (bn_fwd(pre_stats=))."""
     K, B, H, W, C = x.shape
+    Kw, Co, KH, KW, Ci = w.shape
+    OHs, OWs = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    per_sample = max(H * W * (x.stride(-2) if x.dim() == 5 else C), OHs * OWs * Co) * x.element_size()
+    if B * per_sample >= WINDOW and stats is None and x_planes is None:
+        chunks = _batch_chunks(B, per_sample)
+        if out is None:
+            out = torch.empty((K, B, OHs, OWs, Co), dtype=x.dtype, device=x.device)
+        for b0, b1 in chunks:
+            conv_fwd(x[:, b0:b1], w, stride, pad, bias=bias, relu=relu, out=out[:, b0:b1], w_split=w_split)
+        return out
     x, ldx = _pix_stride(x)
     f32 = _f32(x)
     _check(x, x.dtype, contiguous=False, name="x")
     _check(w, x.dtype, contiguous=False, name="w")
-    Kw, Co, KH, KW, Ci = w.shape
     assert Ci == C, (Ci, C)
     w_cs, rep = _client_view(w, K)
     OH = (H + 2 * pad - KH) // stride + 1
@@ -250,13 +274,20 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
     residual branch of a ResNet block, so autograd never materialises the sum separately).
     `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient)."""
     K, B, OH, OW, Co = dy.shape
+    Kw, Co2, KH, KW, Ci = w.shape
+    H, W = int(in_hw[0]), int(in_hw[1])
+    per_sample = max(OH * OW * Co, H * W * Ci) * dy.element_size()
+    if B * per_sample >= WINDOW and dy_planes is None:
+        dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
+        for b0, b1 in _batch_chunks(B, per_sample):
+            dx[:, b0:b1] = conv_dgrad(dy[:, b0:b1], w, in_hw, stride, pad,
+                                      acc=None if acc is None else acc[:, b0:b1].contiguous(), w_split=w_split)
+        return dx
     dy, ld_dy = _pix_stride(dy)
     f32 = _f32(dy)
     _check(w, dy.dtype, contiguous=False, name="w")
-    Kw, Co2, KH, KW, Ci = w.shape
     assert Co2 == Co
     w_cs, rep = _client_view(w, K)
-    H, W = int(in_hw[0]), int(in_hw[1])
     dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
     if acc is not None:
         # (stride > 1: every parity-class launch adds acc at the pixels it writes)
@@ -326,6 +357,16 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int, dy_planes=None, x_planes=None):
     LDS-DMA GEMM of csrc/conv_pl.hip when the shape allows (planes_ok)."""
     K, B, OH, OW, Co = dy.shape
     _, _, H, W, C = x.shape
+    per_sample = max(OH * OW * Co, H * W * C) * dy.element_size()
+    if B * per_sample >= WINDOW and dy_planes is None:
+        # Σ over batch chunks of the chunk weight gradients (fp32, chunk order fixed)
+        chunks = _batch_chunks(B, per_sample)
+        tmp = torch.empty_like(gw) if len(chunks) > 1 else gw
+        for i, (b0, b1) in enumerate(chunks):
+            conv_wgrad(dy[:, b0:b1], x[:, b0:b1], gw if i == 0 else tmp, stride, pad)
+            if i:
+                gw.add_(tmp)
+        return
     dy, ldy = _pix_stride(dy)
     x, ldx = _pix_stride(x)
     f32 = _f32(dy)

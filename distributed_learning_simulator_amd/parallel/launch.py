@@ -25,16 +25,63 @@ import uuid
 _CHILD_FLAG = "DLS_LAUNCHED_RANK"
 
 
+def _kfd_gpus() -> int | None:
+    """GPUs this process may open, from the KFD topology (sysfs, no driver call): nodes whose
+    gfx_target_version is non-zero (CPU nodes report 0) AND whose DRM render node is present
+    and accessible here (a container sees the host's whole topology but only its own
+    /dev/dri/renderD* devices). None when the topology is not readable."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        props = {}
+        try:
+            with open(os.path.join(root, node, "properties")) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+        except OSError:
+            continue
+        try:
+            if int(props.get("gfx_target_version", "0")) == 0:
+                continue
+            minor = int(props.get("drm_render_minor", "-1"))
+        except ValueError:
+            continue
+        if minor >= 0 and os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            n += 1
+    return n
+
+
+def _env_visible(n: int) -> int:
+    """Apply HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES to n devices."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if ids else 0
+    return n
+
+
 def visible_gpus() -> int:
-    """Number of visible GPUs without initialising the HIP runtime in this process
-    (`torch.cuda.device_count()` only enumerates)."""
+    """Number of visible GPUs WITHOUT initialising the HIP runtime in this process (the parent
+    spawns the rank processes afterwards: nothing may touch the GPU before). Read from the KFD
+    sysfs topology and the *_VISIBLE_DEVICES masks; if sysfs is unreadable, counted by a
+    short-lived child process, never by torch.cuda in this one (which falls back to
+    hipGetDeviceCount when amdsmi discovery fails)."""
     if os.environ.get("DLS_FORCE_CPU", "0") == "1":
         return 0
+    n = _kfd_gpus()
+    if n is not None:
+        return _env_visible(n)
     try:
-        import torch
-
-        return int(torch.cuda.device_count())
-    except Exception:  # pragma: no cover - torch without a device runtime
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else 0
+    except Exception:  # pragma: no cover - no python / torch in the child
         return 0
 
 

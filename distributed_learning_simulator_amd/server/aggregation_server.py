@@ -104,8 +104,10 @@ class AggregationServer(Server):
         elif result.end_training:
             self._record_compute_stat(result.parameter)
         self.global_parameter = result.parameter
-        spill = self.config.save_models or self.config.limited_resource
-        if spill and self.session.is_main and "init" not in result.other_data:
+        # (`limited_resource` does not spill here: its memory saving is the smaller HBM budget
+        # fraction the session gives client cohorts, session.py; a per-round file nobody reads
+        # back would only cost disk writes)
+        if self.config.save_models and self.session.is_main and "init" not in result.other_data:
             self._save_model(result.parameter, os.path.join(self.config.save_dir, "aggregated_model",
                                                             f"round_{self._round_number}.pk"))
 

@@ -98,8 +98,8 @@ class Session:
             capacity = per_rank  # halo exchange needs every client of the rank resident at once
         else:
             # `limited_resource` (reference aggregation_worker.py:124-130 spills the worker's model
-            # cache to disk): here the rank keeps a quarter of the HBM budget for clients (more,
-            # smaller waves) and the server spills each round's global model to disk
+            # cache to disk): here the rank gives client cohorts a quarter of the HBM budget it
+            # otherwise would (more, smaller waves); client state never leaves the device
             capacity = plan_capacity(per_rank, self.layout, self.model, self.dc, self.hyper, self.device,
                                      self.compute_dtype, explicit=cfg.cohort_size,
                                      fraction=0.2 if cfg.limited_resource else 0.8)

@@ -170,3 +170,19 @@ def test_bench_self_launch_two_ranks():
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0
+
+
+@pytest.mark.parametrize("share", [True, False])
+def test_fed_gnn_rank_without_clients(tmp_path, share):
+    """a rank left without an active client (here 3 clients, 1 selected per round, on
+    4 ranks) still runs every collective of the round — halo all-to-alls (share_feature), the
+    fed_aas-free embedding-byte all-reduce, FedAvg — with empty contributions: no hang, and the
+    result equals the single-rank run."""
+    extra = {"dataset_name": "Coauthor_CS", "model_name": "TwoGCN", "worker_number": 3, "dataset_kwargs": {"scale": 0.05},
+             "optimizer_name": "Adam", "learning_rate": 0.01, "batch_size": 64,
+             "algorithm_kwargs": {"share_feature": share, "random_client_number": 1}}
+    theta1, res1 = _single("fed_gnn", str(tmp_path / "s"), extra)
+    outs = _run_world(4, "fed_gnn", str(tmp_path / "d"), extra)
+    for o in outs[1:]:
+        torch.testing.assert_close(o[1], outs[0][1], rtol=0, atol=0)
+    torch.testing.assert_close(outs[0][1], theta1, rtol=1e-4, atol=1e-5)

@@ -295,13 +295,19 @@ def test_no_initial_distribution_own_init(tmp_path):
     assert not torch.equal(ref_sess.server.global_parameter, sess.server.global_parameter)
 
 
-def test_limited_resource_spills_global_models(tmp_path):
+def test_limited_resource_shrinks_cohorts_without_spilling(tmp_path):
+    """`limited_resource` gives client cohorts a smaller memory budget (session.plan_capacity
+    fraction) and writes no per-round model files (ADVICE r2: nothing read them back);
+    `save_models` still writes them, weights-only."""
     sess, _ = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 2, "dataset_kwargs.scale": 0.04,
                                           "log_level": "WARNING", "limited_resource": True, "save_models": False},
-                   tmp_path)
-    saved = sorted(os.listdir(tmp_path / "aggregated_model"))
+                   tmp_path / "a")
+    assert not (tmp_path / "a" / "aggregated_model").exists()
+    sess, _ = _run("fed_avg/mnist.yaml", {"round": 2, "epoch": 1, "worker_number": 2, "dataset_kwargs.scale": 0.04,
+                                          "log_level": "WARNING", "save_models": True}, tmp_path / "b")
+    saved = sorted(os.listdir(tmp_path / "b" / "aggregated_model"))
     assert saved == ["round_1.pk", "round_2.pk"]
-    t = torch.load(tmp_path / "aggregated_model" / "round_2.pk", weights_only=True)
+    t = torch.load(tmp_path / "b" / "aggregated_model" / "round_2.pk", weights_only=True)
     assert set(t) == {e.name for e in sess.layout.entries}
 
 
