@@ -261,9 +261,9 @@ static int attn_rows(int L) {
   return ((cdiv(L, nblk) + 63) / 64) * 64;
 }
 
-// head dims 32 / 64 run on the MFMA kernels (attention_mfma.hip) unless DLS_ATTN_MFMA=0; the
-// VALU kernels below keep the small heads (the imdb model's dh = 20, 8, 16), where a 32-wide
-// MFMA operand would be mostly padding
+// every head dim the MFMA kernels cover (attention_mfma.hip: 8 / 16 / 20 padded to 32, 32, 48
+// padded to 64, 64) runs there unless DLS_ATTN_MFMA=0; the VALU kernels below are the fallback
+// (no dropout, no packed layouts)
 static bool use_mfma(int L, int DH) {
   static const int mode = [] {
     const char* e = getenv("DLS_ATTN_MFMA");
@@ -292,9 +292,12 @@ bool attn_supported(int L, int DH) {
 #define MP(p) static_cast<TT*>(p)
 
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
-              int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo) {
-  if (use_mfma(L, DH)) return attn_fwd_mfma(q, k, v, key_valid, o, lse, KBH, H, L, DH, f32, s, ldqkv, ldo);
-  if (ldqkv || ldo) return false;  // packed layouts: MFMA kernels only
+              int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds,
+              int heads_per_client, float drop_p) {
+  if (use_mfma(L, DH))
+    return attn_fwd_mfma(q, k, v, key_valid, o, lse, KBH, H, L, DH, f32, s, ldqkv, ldo, drop_seeds, heads_per_client,
+                         drop_p);
+  if (ldqkv || ldo || drop_p > 0.f) return false;  // packed layouts / dropout: MFMA kernels only
   if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));
@@ -308,10 +311,11 @@ bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid,
 
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
-              hipStream_t s, int ldqkv, int ldo) {
+              hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds, int heads_per_client, float drop_p) {
   if (use_mfma(L, DH))
-    return attn_bwd_mfma(dout, q, k, v, o, lse, key_valid, dq, dk, dv, delta, KBH, H, L, DH, f32, s, ldqkv, ldo);
-  if (ldqkv || ldo) return false;
+    return attn_bwd_mfma(dout, q, k, v, o, lse, key_valid, dq, dk, dv, delta, KBH, H, L, DH, f32, s, ldqkv, ldo,
+                         drop_seeds, heads_per_client, drop_p);
+  if (ldqkv || ldo || drop_p > 0.f) return false;
   if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));

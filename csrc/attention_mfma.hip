@@ -1,4 +1,7 @@
-// Multi-head attention fwd / bwd on the MFMA (gfx950), head dim 32 or 64, any sequence length.
+// Multi-head attention fwd / bwd on the MFMA (gfx950), any head dim ≤ 64 with dh % 4 == 0 (run at
+// the padded width 32 or 64: zero columns past dh, so e.g. the reference imdb model's dh = 20
+// runs here instead of the VALU kernels), any sequence length, optional dropout on the attention
+// probabilities (nn.MultiheadAttention's `dropout`, inside nn.TransformerEncoderLayer).
 //
 //   q, k, v, o, do, dq, dk, dv : [KBH][L][DH] (bf16, or fp32 = reference precision)
 //   lse, delta                 : [KBH][L] fp32;   key_valid [KB] (valid keys per sequence)
@@ -18,6 +21,10 @@
 //   dq  : δ = rowsum(dO∘O); Sᵀ, Pᵀ = exp(Sᵀ − lse); dPᵀ = V·dOᵀ; dSᵀ = Pᵀ(dPᵀ − δ)·s;
 //         dQᵀ += Kᵀ·dSᵀ                                                         (writes δ)
 //   dkv : S = Q·Kᵀ, P, dP = dO·Vᵀ, dS (per 32-query block);  dVᵀ += dOᵀ·P;  dKᵀ += Qᵀ·dS
+// Dropout (p > 0): P̃ = P∘M/(1−p) with M the keep mask hash(head, query, key) of the client's
+// seed — the same mask in all three kernels and in ops/ref.py. The forward normalises with the
+// undropped P (l, lse) and accumulates O = P̃V; the backward uses dP = (dO·Vᵀ)∘M/(1−p) in
+// dS = P∘(dP − δ) with δ = rowsum(dO∘O), and dV = P̃ᵀdO.
 #include "common.h"
 #include "dls.h"
 #include "gemm_common.h"
@@ -41,21 +48,38 @@ __device__ __forceinline__ void mma(f32x16& acc, const Frag<T>& a, const Frag<T>
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
 }
 
-// 8 consecutive elements of a global row → an operand fragment (zeros when !ok)
+// up to 8 consecutive elements of a global row (n valid, n % 4 == 0; the rest read as zeros)
 template <typename T>
-__device__ __forceinline__ Frag<T> frag_global(const T* p, bool ok) {
+__device__ __forceinline__ void load8n(const T* p, int n, float* x) {
+  if (n >= 8) {
+    // (two 4-element loads: a dh = 20 head's bf16 rows are only 8-B aligned)
+    load_vec<4>(p, x);
+    load_vec<4>(p + 4, x + 4);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = 0.f;
+    if (n >= 4) load_vec<4>(p, x);
+  }
+}
+
+// 8 consecutive elements of a global row → an operand fragment (n valid: zeros beyond)
+template <typename T>
+__device__ __forceinline__ Frag<T> frag_global(const T* p, int n) {
   Frag<T> f;
   if constexpr (sizeof(T) == 2) {
-    uint4 u = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (n >= 8) {
+      const uint2 a = *reinterpret_cast<const uint2*>(p), b = *reinterpret_cast<const uint2*>(p + 4);
+      u = make_uint4(a.x, a.y, b.x, b.y);
+    } else if (n >= 4) {
+      const uint2 h = *reinterpret_cast<const uint2*>(p);
+      u.x = h.x;
+      u.y = h.y;
+    }
     f.h = __builtin_bit_cast(bf16x8, u);
   } else {
     float x[8];
-    if (ok) {
-      load_vec<8>(p, x);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = 0.f;
-    }
+    load8n(p, n, x);
     union {
       bf16x8 v;
       bf16_t e[8];
@@ -110,19 +134,15 @@ __device__ __forceinline__ long hbase(const HeadLayout& hl, long head, int H) {
   return (head / H) * hl.s_kb + (head % H) * hl.s_h;
 }
 
-// stage rows [r0, r0+RB) of a head matrix (row stride ld) into an image (zero rows past L)
-template <typename T, int DH>
+// stage rows [r0, r0+RB) of a head matrix (row stride ld, DH real columns) into an image of DP
+// padded columns (zero rows past L, zero columns past DH)
+template <typename T, int DH, int DP>
 __device__ __forceinline__ void stage(const T* __restrict__ src, int ld, int r0, int L, const Img<T>& m) {
-  for (int c = threadIdx.x; c < RB * DH / 8; c += WG) {
-    const int r = c / (DH / 8), d = (c % (DH / 8)) * 8;
-    const bool ok = r0 + r < L;
+  for (int c = threadIdx.x; c < RB * DP / 8; c += WG) {
+    const int r = c / (DP / 8), d = (c % (DP / 8)) * 8;
+    const int n = r0 + r < L ? min(8, max(0, DH - d)) : 0;
     float x[8];
-    if (ok) {
-      load_vec<8>(src + (long)(r0 + r) * ld + d, x);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = 0.f;
-    }
+    load8n(src + (long)(r0 + r) * ld + d, n, x);
     union {
       uint4 v;
       bf16_t e[8];
@@ -165,14 +185,27 @@ __device__ __forceinline__ void put_colrows(const Img<T>& m, const f32x16& v) {
 
 // global store of a transposed accumulator tile (lane column = matrix row `row`, tile rows =
 // 16 of the DH columns starting at d0): out[row][d0 + rows(e)]
-template <typename T>
+template <typename T, int DH>
 __device__ __forceinline__ void store_rowcols(T* out_row, int d0, const f32x16& v, float mul) {
   const int h = (threadIdx.x & 63) >> 5;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float x[4] = {v[4 * j] * mul, v[4 * j + 1] * mul, v[4 * j + 2] * mul, v[4 * j + 3] * mul};
-    store_vec<4>(out_row + d0 + 8 * j + 4 * h, x);
+    if (d0 + 8 * j + 4 * h < DH) store_vec<4>(out_row + d0 + 8 * j + 4 * h, x);  // (DH % 4 == 0)
   }
+}
+
+// attention-probability dropout of one score (client seed, head within the client, query, key)
+struct AttnDropArgs {
+  const uint32_t* seeds;  // [clients]; nullptr = no dropout
+  int hpc;                // heads per client (B·H)
+  float p;
+};
+__device__ __forceinline__ float attn_keep(const AttnDropArgs& d, long head, int L, int qi, int kj) {
+  const uint32_t seed = d.seeds[head / d.hpc];
+  const uint32_t idx = (uint32_t)(((long)(head % d.hpc) * L + qi) * L + kj);
+  const uint32_t thr = (uint32_t)fminf(d.p * 4294967296.f, 4294967040.f);
+  return mix32(idx, seed) >= thr ? 1.f / (1.f - d.p) : 0.f;
 }
 
 __device__ __forceinline__ int crow(int e) { return (e & 3) + 8 * (e >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
@@ -180,13 +213,13 @@ __device__ __forceinline__ int crow(int e) { return (e & 3) + 8 * (e >> 2) + 4 *
 constexpr int pad_ld(int n) { return n + 8; }  // 16-B padded rows: conflict-free ds_read_b128
 
 // ------------------------------------------------------------------------------ forward
-template <typename T, int DH>
+template <typename T, int DH, int DP>
 __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__ q, const T* __restrict__ k,
                                                            const T* __restrict__ v, const int* __restrict__ key_valid,
                                                            T* __restrict__ o, float* __restrict__ lse, int L, int H,
-                                                           float scale, HeadLayout lq, HeadLayout lo) {
+                                                           float scale, HeadLayout lq, HeadLayout lo, AttnDropArgs dr) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
-  constexpr int LDK = pad_ld(DH), LDP = pad_ld(RB);
+  constexpr int LDK = pad_ld(DP), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NP * RB * LDK], Vs[NP * RB * LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Ps[4][NP * RB * LDP];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 31;
@@ -195,22 +228,26 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
   const int nk = key_valid ? min(key_valid[head / H], L) : L;
   const int qrow = blockIdx.y * (4 * RB) + wid * RB + c;
   const bool qok = qrow < L;
+  const bool drop = dr.seeds != nullptr && dr.p > 0.f;
   const Img<T> KI{Ks, LDK, RB * LDK}, VI{Vs, LDK, RB * LDK}, PI{Ps[wid], LDP, RB * LDP};
 
-  Frag<T> qf[DH / 16];
+  Frag<T> qf[DP / 16];
 #pragma unroll
-  for (int ks = 0; ks < DH / 16; ++ks) qf[ks] = frag_global<T>(q + base + (long)qrow * lq.ld + ks * 16 + 8 * (lane >> 5), qok);
-  f32x16 ot[DH / 32];
+  for (int ks = 0; ks < DP / 16; ++ks) {
+    const int d = ks * 16 + 8 * (lane >> 5);
+    qf[ks] = frag_global<T>(q + base + (long)qrow * lq.ld + d, qok ? min(8, max(0, DH - d)) : 0);
+  }
+  f32x16 ot[DP / 32];
 #pragma unroll
-  for (int t = 0; t < DH / 32; ++t) ot[t] = f32x16{};
+  for (int t = 0; t < DP / 32; ++t) ot[t] = f32x16{};
   float m = -INFINITY, l = 0.f;
   for (int k0 = 0; k0 < nk; k0 += RB) {
-    stage<T, DH>(k + base, lq.ld, k0, nk, KI);
-    stage<T, DH>(v + base, lq.ld, k0, nk, VI);
+    stage<T, DH, DP>(k + base, lq.ld, k0, nk, KI);
+    stage<T, DH, DP>(v + base, lq.ld, k0, nk, VI);
     __syncthreads();
     f32x16 st = f32x16{};  // Sᵀ[key][query]
 #pragma unroll
-    for (int ks = 0; ks < DH / 16; ++ks) mma<T>(st, frag_rm<T>(KI, 0, ks * 16), qf[ks]);
+    for (int ks = 0; ks < DP / 16; ++ks) mma<T>(st, frag_rm<T>(KI, 0, ks * 16), qf[ks]);
     float mloc = -INFINITY;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -225,18 +262,18 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const float p = (st[e] == -INFINITY) ? 0.f : __expf(st[e] - mn);
-      st[e] = p;
-      ls += p;
+      ls += p;  // (the normaliser sums the undropped probabilities)
+      st[e] = (drop && p != 0.f) ? p * attn_keep(dr, head, L, qrow, k0 + crow(e)) : p;
     }
     ls += __shfl_xor(ls, 32, 64);
     l = l * corr + ls;
     m = mn;
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t) ot[t] *= corr;
-    put_colrows<T>(PI, st);  // P[query][key]
+    for (int t = 0; t < DP / 32; ++t) ot[t] *= corr;
+    put_colrows<T>(PI, st);  // P̃[query][key]
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t)
+    for (int t = 0; t < DP / 32; ++t)
 #pragma unroll
       for (int ks = 0; ks < RB / 16; ++ks) mma<T>(ot[t], frag_km<T>(VI, ks * 16, t * 32), frag_rm<T>(PI, 0, ks * 16));
     __syncthreads();  // K / V / P tiles are rewritten next block
@@ -244,21 +281,21 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
   if (qok) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t) store_rowcols<T>(o + obase + (long)qrow * lo.ld, t * 32, ot[t], inv);
+    for (int t = 0; t < DP / 32; ++t) store_rowcols<T, DH>(o + obase + (long)qrow * lo.ld, t * 32, ot[t], inv);
     if ((lane >> 5) == 0) lse[head * L + qrow] = l > 0.f ? m + __logf(l) : 0.f;
   }
 }
 
 // ------------------------------------------------------------------------------ dQ
-template <typename T, int DH>
+template <typename T, int DH, int DP>
 __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
                                                               const T* __restrict__ k, const T* __restrict__ v,
                                                               const T* __restrict__ o, const float* __restrict__ lse,
                                                               const int* __restrict__ key_valid, T* __restrict__ dq,
                                                               float* __restrict__ delta, int L, int H, float scale,
-                                                              HeadLayout lq, HeadLayout lo) {
+                                                              HeadLayout lq, HeadLayout lo, AttnDropArgs dr) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
-  constexpr int LDK = pad_ld(DH), LDP = pad_ld(RB);
+  constexpr int LDK = pad_ld(DP), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NP * RB * LDK], Vs[NP * RB * LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Ps[4][NP * RB * LDP];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, c = lane & 31, h = lane >> 5;
@@ -267,75 +304,78 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
   const int nk = key_valid ? min(key_valid[head / H], L) : L;
   const int qrow = blockIdx.y * (4 * RB) + wid * RB + c;
   const bool qok = qrow < L;
+  const bool drop = dr.seeds != nullptr && dr.p > 0.f;
   const Img<T> KI{Ks, LDK, RB * LDK}, VI{Vs, LDK, RB * LDK}, PI{Ps[wid], LDP, RB * LDP};
 
-  Frag<T> qf[DH / 16], df[DH / 16];
+  Frag<T> qf[DP / 16], df[DP / 16];
 #pragma unroll
-  for (int ks = 0; ks < DH / 16; ++ks) {
-    qf[ks] = frag_global<T>(q + base + (long)qrow * lq.ld + ks * 16 + 8 * h, qok);
-    df[ks] = frag_global<T>(dout + obase + (long)qrow * lo.ld + ks * 16 + 8 * h, qok);
+  for (int ks = 0; ks < DP / 16; ++ks) {
+    const int d = ks * 16 + 8 * h, n = qok ? min(8, max(0, DH - d)) : 0;
+    qf[ks] = frag_global<T>(q + base + (long)qrow * lq.ld + d, n);
+    df[ks] = frag_global<T>(dout + obase + (long)qrow * lo.ld + d, n);
   }
-  // δ = dO·O of this lane's query (each half-wave sums half of the head dim)
+  // δ = dO·O of this lane's query (the two half-waves take alternate 4-column chunks)
   float dl = 0.f;
   if (qok) {
-    const T* dr = dout + obase + (long)qrow * lo.ld + h * (DH / 2);
-    const T* orow = o + obase + (long)qrow * lo.ld + h * (DH / 2);
+    const T* dr_ = dout + obase + (long)qrow * lo.ld;
+    const T* orow = o + obase + (long)qrow * lo.ld;
 #pragma unroll
-    for (int d = 0; d < DH / 2; d += 8) {
-      float a[8], b[8];
-      load_vec<8>(dr + d, a);
-      load_vec<8>(orow + d, b);
+    for (int d = 4 * h; d < DH; d += 8) {
+      float a[4], b[4];
+      load_vec<4>(dr_ + d, a);
+      load_vec<4>(orow + d, b);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) dl = fmaf(a[i], b[i], dl);
+      for (int i = 0; i < 4; ++i) dl = fmaf(a[i], b[i], dl);
     }
   }
   dl += __shfl_xor(dl, 32, 64);
   if (qok && h == 0) delta[head * L + qrow] = dl;
   const float lse_q = qok ? lse[head * L + qrow] : 0.f;
-  f32x16 dqt[DH / 32];
+  f32x16 dqt[DP / 32];
 #pragma unroll
-  for (int t = 0; t < DH / 32; ++t) dqt[t] = f32x16{};
+  for (int t = 0; t < DP / 32; ++t) dqt[t] = f32x16{};
   for (int k0 = 0; k0 < nk; k0 += RB) {
-    stage<T, DH>(k + base, lq.ld, k0, nk, KI);
-    stage<T, DH>(v + base, lq.ld, k0, nk, VI);
+    stage<T, DH, DP>(k + base, lq.ld, k0, nk, KI);
+    stage<T, DH, DP>(v + base, lq.ld, k0, nk, VI);
     __syncthreads();
     f32x16 st = f32x16{}, dpt = f32x16{};
 #pragma unroll
-    for (int ks = 0; ks < DH / 16; ++ks) {
+    for (int ks = 0; ks < DP / 16; ++ks) {
       mma<T>(st, frag_rm<T>(KI, 0, ks * 16), qf[ks]);   // Sᵀ = K·Qᵀ
-      mma<T>(dpt, frag_rm<T>(VI, 0, ks * 16), df[ks]);  // dPᵀ = V·dOᵀ
+      mma<T>(dpt, frag_rm<T>(VI, 0, ks * 16), df[ks]);  // dP̃ᵀ = V·dOᵀ
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const bool ok = qok && (k0 + crow(e) < nk);
       const float p = ok ? __expf(st[e] * scale - lse_q) : 0.f;
-      st[e] = p * (dpt[e] - dl) * scale;  // dSᵀ
+      const float dp = (drop && p != 0.f) ? dpt[e] * attn_keep(dr, head, L, qrow, k0 + crow(e)) : dpt[e];
+      st[e] = p * (dp - dl) * scale;  // dSᵀ
     }
     put_colrows<T>(PI, st);  // dS[query][key]
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t)
+    for (int t = 0; t < DP / 32; ++t)
 #pragma unroll
       for (int ks = 0; ks < RB / 16; ++ks) mma<T>(dqt[t], frag_km<T>(KI, ks * 16, t * 32), frag_rm<T>(PI, 0, ks * 16));
     __syncthreads();
   }
   if (qok) {
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t) store_rowcols<T>(dq + base + (long)qrow * lq.ld, t * 32, dqt[t], 1.f);
+    for (int t = 0; t < DP / 32; ++t) store_rowcols<T, DH>(dq + base + (long)qrow * lq.ld, t * 32, dqt[t], 1.f);
   }
 }
 
 // ------------------------------------------------------------------------------ dK, dV
-template <typename T, int DH>
+template <typename T, int DH, int DP>
 __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
                                                                const T* __restrict__ k, const T* __restrict__ v,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
                                                                const int* __restrict__ key_valid, T* __restrict__ dk,
                                                                T* __restrict__ dv, int L, int H, float scale,
-                                                               HeadLayout lq, HeadLayout lo) {
+                                                               HeadLayout lq, HeadLayout lo, AttnDropArgs dr) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
-  constexpr int LDK = pad_ld(DH), LDP = pad_ld(RB);
+  constexpr int LDK = pad_ld(DP), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NP * RB * LDK], Os[NP * RB * LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Ps[4][NP * RB * LDP], Ss[4][NP * RB * LDP];
   __shared__ __attribute__((aligned(16))) float Lq[RB], Dq[RB];
@@ -345,24 +385,26 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   const int nk = key_valid ? min(key_valid[head / H], L) : L;
   const int key = blockIdx.y * (4 * RB) + wid * RB + c;
   const bool kok = key < nk;
+  const bool drop = dr.seeds != nullptr && dr.p > 0.f;
   const Img<T> QI{Qs, LDK, RB * LDK}, OI{Os, LDK, RB * LDK};
   const Img<T> PI{Ps[wid], LDP, RB * LDP}, SI{Ss[wid], LDP, RB * LDP};
 
-  Frag<T> kf[DH / 16], vf[DH / 16];
+  Frag<T> kf[DP / 16], vf[DP / 16];
 #pragma unroll
-  for (int ks = 0; ks < DH / 16; ++ks) {
-    kf[ks] = frag_global<T>(k + base + (long)key * lq.ld + ks * 16 + 8 * h, kok);
-    vf[ks] = frag_global<T>(v + base + (long)key * lq.ld + ks * 16 + 8 * h, kok);
+  for (int ks = 0; ks < DP / 16; ++ks) {
+    const int d = ks * 16 + 8 * h, n = kok ? min(8, max(0, DH - d)) : 0;
+    kf[ks] = frag_global<T>(k + base + (long)key * lq.ld + d, n);
+    vf[ks] = frag_global<T>(v + base + (long)key * lq.ld + d, n);
   }
-  f32x16 dkt[DH / 32], dvt[DH / 32];
+  f32x16 dkt[DP / 32], dvt[DP / 32];
 #pragma unroll
-  for (int t = 0; t < DH / 32; ++t) dkt[t] = dvt[t] = f32x16{};
+  for (int t = 0; t < DP / 32; ++t) dkt[t] = dvt[t] = f32x16{};
   // a workgroup whose keys are all padding still writes their zero gradients (no early exit:
   // every wave must reach every barrier)
   const bool any = blockIdx.y * (4 * RB) < nk;
   for (int q0 = 0; any && q0 < L; q0 += RB) {
-    stage<T, DH>(q + base, lq.ld, q0, L, QI);
-    stage<T, DH>(dout + obase, lo.ld, q0, L, OI);
+    stage<T, DH, DP>(q + base, lq.ld, q0, L, QI);
+    stage<T, DH, DP>(dout + obase, lo.ld, q0, L, OI);
     if (threadIdx.x < RB) {
       const bool ok = q0 + threadIdx.x < L;
       Lq[threadIdx.x] = ok ? lse[head * L + q0 + threadIdx.x] : 0.f;
@@ -371,9 +413,9 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
     __syncthreads();
     f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
-    for (int ks = 0; ks < DH / 16; ++ks) {
+    for (int ks = 0; ks < DP / 16; ++ks) {
       mma<T>(s, frag_rm<T>(QI, 0, ks * 16), kf[ks]);   // S = Q·Kᵀ   [query][key]
-      mma<T>(dp, frag_rm<T>(OI, 0, ks * 16), vf[ks]);  // dP = dO·Vᵀ [query][key]
+      mma<T>(dp, frag_rm<T>(OI, 0, ks * 16), vf[ks]);  // dP̃ = dO·Vᵀ [query][key]
     }
     f32x16 ds;
 #pragma unroll
@@ -381,41 +423,59 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
       const int qr = crow(e);
       const bool ok = kok && (q0 + qr < L);
       const float p = ok ? __expf(s[e] * scale - Lq[qr]) : 0.f;
-      s[e] = p;
-      ds[e] = p * (dp[e] - Dq[qr]) * scale;
+      const float mk = (drop && p != 0.f) ? attn_keep(dr, head, L, q0 + qr, key) : 1.f;
+      s[e] = p * mk;                              // P̃ (dV)
+      ds[e] = p * (dp[e] * mk - Dq[qr]) * scale;  // dS = P∘(dP − δ)
     }
-    put_colrows<T>(PI, s);   // P[key][query]
+    put_colrows<T>(PI, s);   // P̃[key][query]
     put_colrows<T>(SI, ds);  // dS[key][query]
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t)
+    for (int t = 0; t < DP / 32; ++t)
 #pragma unroll
       for (int ks = 0; ks < RB / 16; ++ks) {
-        mma<T>(dvt[t], frag_km<T>(OI, ks * 16, t * 32), frag_rm<T>(PI, 0, ks * 16));  // dVᵀ += dOᵀ·P
+        mma<T>(dvt[t], frag_km<T>(OI, ks * 16, t * 32), frag_rm<T>(PI, 0, ks * 16));  // dVᵀ += dOᵀ·P̃
         mma<T>(dkt[t], frag_km<T>(QI, ks * 16, t * 32), frag_rm<T>(SI, 0, ks * 16));  // dKᵀ += Qᵀ·dS
       }
     __syncthreads();
   }
   if (key < L) {
 #pragma unroll
-    for (int t = 0; t < DH / 32; ++t) {
-      store_rowcols<T>(dk + base + (long)key * lq.ld, t * 32, dkt[t], 1.f);
-      store_rowcols<T>(dv + base + (long)key * lq.ld, t * 32, dvt[t], 1.f);
+    for (int t = 0; t < DP / 32; ++t) {
+      store_rowcols<T, DH>(dk + base + (long)key * lq.ld, t * 32, dkt[t], 1.f);
+      store_rowcols<T, DH>(dv + base + (long)key * lq.ld, t * 32, dvt[t], 1.f);
     }
   }
 }
 
-#define MFMA_DH(DHV, CALL) \
-  switch (DHV) {           \
-    case 32: {             \
-      constexpr int D = 32; \
-      CALL;                \
-    } break;               \
-    case 64: {             \
-      constexpr int D = 64; \
-      CALL;                \
-    } break;               \
-    default: return false; \
+// (logical head dim, padded MFMA width) pairs compiled
+#define MFMA_DH(DHV, CALL)                      \
+  switch (DHV) {                                \
+    case 8: {                                   \
+      constexpr int D = 8, DPAD = 32;           \
+      CALL;                                     \
+    } break;                                    \
+    case 16: {                                  \
+      constexpr int D = 16, DPAD = 32;          \
+      CALL;                                     \
+    } break;                                    \
+    case 20: {                                  \
+      constexpr int D = 20, DPAD = 32;          \
+      CALL;                                     \
+    } break;                                    \
+    case 32: {                                  \
+      constexpr int D = 32, DPAD = 32;          \
+      CALL;                                     \
+    } break;                                    \
+    case 48: {                                  \
+      constexpr int D = 48, DPAD = 64;          \
+      CALL;                                     \
+    } break;                                    \
+    case 64: {                                  \
+      constexpr int D = 64, DPAD = 64;          \
+      CALL;                                     \
+    } break;                                    \
+    default: return false;                      \
   }
 
 #define DISPATCH_T(F32, ...) \
@@ -431,7 +491,9 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
 
 }  // namespace
 
-bool attn_mfma_supported(int L, int DH) { return (DH == 32 || DH == 64) && L >= 1; }
+bool attn_mfma_supported(int L, int DH) {
+  return (DH == 8 || DH == 16 || DH == 20 || DH == 32 || DH == 48 || DH == 64) && L >= 1;
+}
 
 // ldqkv / ldo = 0: contiguous [KBH][L][DH]; otherwise packed [KB][L][ld] rows (module docs)
 static HeadLayout head_layout(int ld, int H, int L, int DH) {
@@ -440,28 +502,32 @@ static HeadLayout head_layout(int ld, int H, int L, int DH) {
 }
 
 bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
-                   int H, int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo) {
+                   int H, int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds,
+                   int heads_per_client, float drop_p) {
   if (!attn_mfma_supported(L, DH)) return false;
   const dim3 grid((unsigned)KBH, cdiv(L, 4 * RB));
   const float scale = 1.0f / sqrtf((float)DH);
   const HeadLayout lq = head_layout(ldqkv, H, L, DH), lo = head_layout(ldo, H, L, DH);
-  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_fwd_mfma_kernel<TT, D>), grid, dim3(WG), 0, s, CP(q), CP(k),
-                                                 CP(v), key_valid, MP(o), lse, L, H, scale, lq, lo)));
+  const AttnDropArgs dr{drop_p > 0.f ? drop_seeds : nullptr, heads_per_client > 0 ? heads_per_client : 1, drop_p};
+  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_fwd_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s, CP(q),
+                                                 CP(k), CP(v), key_valid, MP(o), lse, L, H, scale, lq, lo, dr)));
   return true;
 }
 
 bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                    const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
-                   int f32, hipStream_t s, int ldqkv, int ldo) {
+                   int f32, hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds, int heads_per_client,
+                   float drop_p) {
   if (!attn_mfma_supported(L, DH)) return false;
   const dim3 grid((unsigned)KBH, cdiv(L, 4 * RB));
   const float scale = 1.0f / sqrtf((float)DH);
   const HeadLayout lq = head_layout(ldqkv, H, L, DH), lo = head_layout(ldo, H, L, DH);
-  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dq_mfma_kernel<TT, D>), grid, dim3(WG), 0, s, CP(dout),
-                                                 CP(q), CP(k), CP(v), CP(o), lse, key_valid, MP(dq), delta, L, H,
-                                                 scale, lq, lo)));
-  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dkv_mfma_kernel<TT, D>), grid, dim3(WG), 0, s, CP(dout),
-                                                 CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk), MP(dv), L, H,
-                                                 scale, lq, lo)));
+  const AttnDropArgs dr{drop_p > 0.f ? drop_seeds : nullptr, heads_per_client > 0 ? heads_per_client : 1, drop_p};
+  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dq_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s,
+                                                 CP(dout), CP(q), CP(k), CP(v), CP(o), lse, key_valid, MP(dq), delta,
+                                                 L, H, scale, lq, lo, dr)));
+  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dkv_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s,
+                                                 CP(dout), CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk), MP(dv),
+                                                 L, H, scale, lq, lo, dr)));
   return true;
 }

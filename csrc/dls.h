@@ -287,17 +287,23 @@ bool attn_supported(int L, int DH);
 bool attn_mfma_supported(int L, int DH);
 // ldqkv / ldo > 0: q/k/v (and dq/dk/dv) are column blocks of packed [KB][L][ldqkv] rows, o / do
 // of [KB][L][ldo] rows (the QKV / out projections' own layouts; attention_mfma.hip)
+// drop_p > 0: dropout on the attention probabilities, keep mask = mix32(((head % hpc)·L + q)·L +
+// key, drop_seeds[head / hpc]) >= p·2³², hpc = heads per client (B·H); MFMA kernels only
 bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
-                   int H, int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0);
+                   int H, int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0,
+                   const uint32_t* drop_seeds = nullptr, int heads_per_client = 1, float drop_p = 0.f);
 bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                    const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
-                   int f32, hipStream_t s, int ldqkv = 0, int ldo = 0);
+                   int f32, hipStream_t s, int ldqkv = 0, int ldo = 0, const uint32_t* drop_seeds = nullptr,
+                   int heads_per_client = 1, float drop_p = 0.f);
 bool attn_packed_supported(int L, int DH);
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
-              int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0);
+              int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0, const uint32_t* drop_seeds = nullptr,
+              int heads_per_client = 1, float drop_p = 0.f);
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
-              hipStream_t s, int ldqkv = 0, int ldo = 0);
+              hipStream_t s, int ldqkv = 0, int ldo = 0, const uint32_t* drop_seeds = nullptr,
+              int heads_per_client = 1, float drop_p = 0.f);
 void spmm(const int* rowptr, const int* col, const float* val, const void* x, void* y, int K, int N, int Nx, int F,
           long x_cs, long y_cs, int f32, hipStream_t s);
 void gather_rows(const void* src, const int* idx, void* dst, long n, long row_bytes, hipStream_t s);

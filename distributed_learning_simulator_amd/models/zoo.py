@@ -277,18 +277,23 @@ class MultiheadAttention(Module):
         self.child("in_proj", Linear(d, 3 * d))
         self.child("out_proj", Linear(d, d))
 
-    def forward(self, x, ctx, key_valid, residual=None, **drop):
+    def forward(self, x, ctx, key_valid, residual=None, attn_drop: float = 0.0, attn_seeds=None, **drop):
         """Returns out_proj(attention) (+ residual, added in the projection's epilogue; `drop`:
-        dropout of the projection output before that add)."""
+        dropout of the projection output before that add). `attn_drop`: dropout on the
+        attention probabilities (nn.MultiheadAttention(dropout=...)), masks from this step's
+        next dropout site."""
         K, B, L, D = x.shape
         qkv = self.in_proj.forward(x, ctx)
+        ad = {}
+        if attn_drop:
+            ad = {"drop_p": attn_drop, "drop_seeds": attn_seeds if attn_seeds is not None else ctx.dropout_seeds()}
         if Fn.packed_attention_ok(qkv, L, D // self.h):
             # heads read / written in place in the projections' row layouts (no permute copies)
-            o = Fn.attention_packed(qkv, key_valid, self.h)
+            o = Fn.attention_packed(qkv, key_valid, self.h, **ad)
             return self.out_proj.forward(o, ctx, residual=residual, **drop)
         qkv = qkv.reshape(K, B, L, 3, self.h, D // self.h)
         qkv = qkv.permute(3, 0, 1, 4, 2, 5)  # 3,K,B,H,L,dh
-        o = Fn.attention(qkv[0].contiguous(), qkv[1].contiguous(), qkv[2].contiguous(), key_valid)
+        o = Fn.attention(qkv[0].contiguous(), qkv[1].contiguous(), qkv[2].contiguous(), key_valid, **ad)
         o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
         return self.out_proj.forward(o, ctx, residual=residual, **drop)
 
@@ -303,9 +308,9 @@ class TransformerEncoderLayer(Module):
     - the FFN ReLU output is masked in linear1's epilogue, and linear2's ReLU'-gated dgrad
       epilogue (h > 0 iff kept and positive) carries the 1/(1-p).
     Masks come from (step seed, site, client id) hashes (RunCtx.dropout_seeds), so they do not
-    depend on which rank or cohort row trains a client. Attention-probability dropout (nn.MHA's
-    own `dropout`) is not simulated: a per-score mask would cost more than the attention itself
-    on the MFMA path."""
+    depend on which rank or cohort row trains a client. The attention probabilities get the same
+    dropout (nn.MultiheadAttention(dropout=p) inside nn.TransformerEncoderLayer), applied inside
+    the flash-attention kernels from a (client, head, query, key) hash."""
 
     kind = "TransformerEncoderLayer"
 
@@ -326,7 +331,9 @@ class TransformerEncoderLayer(Module):
 
         # residual adds, the FFN ReLU and the dropout masks (forward and backward) ride in the
         # GEMM epilogues
-        x = self.norm1.forward(self.self_attn.forward(x, ctx, key_valid, residual=x, **drop()), ctx)
+        sa = ctx.dropout_seeds() if p else None  # (the attention's site first: same order as unfused)
+        x = self.norm1.forward(self.self_attn.forward(x, ctx, key_valid, residual=x, attn_drop=p, attn_seeds=sa,
+                                                      **drop()), ctx)
         h = self.linear1.forward(x, ctx, relu=True, premasked=True, **drop())
         y = self.linear2.forward(h, ctx, gate_input=True, residual=x, gate_scale=1.0 / (1.0 - p), **drop())
         return self.norm2.forward(y, ctx)

@@ -531,21 +531,24 @@ def seq_mean(x, lengths):
 # ------------------------------------------------------------------------ attention
 class _Attn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, key_valid):
-        o, lse = _be(q).attn_fwd(q, k, v, key_valid)
+    def forward(ctx, q, k, v, key_valid, drop_p=0.0, drop_seeds=None):
+        dr = {"drop_p": drop_p, "drop_seeds": drop_seeds} if drop_p else {}
+        o, lse = _be(q).attn_fwd(q, k, v, key_valid, **dr)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.key_valid = key_valid
+        ctx.key_valid, ctx.dr = key_valid, dr
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = _be(do).attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.key_valid)
-        return dq, dk, dv, None
+        dq, dk, dv = _be(do).attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.key_valid, **ctx.dr)
+        return dq, dk, dv, None, None, None
 
 
-def attention(q, k, v, key_valid=None):
-    return _Attn.apply(q, k, v, key_valid)
+def attention(q, k, v, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
+    """Softmax attention over [K, B, H, L, dh]; `drop_p` / `drop_seeds` [K]: dropout on the
+    attention probabilities (hash mask per client, head, query, key — ops/ref.py attn_drop_scale)."""
+    return _Attn.apply(q, k, v, key_valid, drop_p, drop_seeds)
 
 
 class _AttnPacked(torch.autograd.Function):
@@ -554,18 +557,19 @@ class _AttnPacked(torch.autograd.Function):
     MFMA kernels read / write the heads in place (no permute copies either way)."""
 
     @staticmethod
-    def forward(ctx, qkv, key_valid, H):
+    def forward(ctx, qkv, key_valid, H, drop_p=0.0, drop_seeds=None):
         be = _be(qkv)
         K, B, L, D3 = qkv.shape
         D = D3 // 3
+        dr = {"drop_p": drop_p, "drop_seeds": drop_seeds} if drop_p else {}
         if be is ref:
             t = qkv.reshape(K, B, L, 3, H, D // H).permute(3, 0, 1, 4, 2, 5)
-            o, lse = ref.attn_fwd(t[0], t[1], t[2], key_valid)
+            o, lse = ref.attn_fwd(t[0], t[1], t[2], key_valid, **dr)
             o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
         else:
-            o, lse = be.attn_fwd_packed(qkv, H, key_valid)
+            o, lse = be.attn_fwd_packed(qkv, H, key_valid, **dr)
         ctx.save_for_backward(qkv, o, lse)
-        ctx.key_valid, ctx.H = key_valid, H
+        ctx.key_valid, ctx.H, ctx.dr = key_valid, H, dr
         return o
 
     @staticmethod
@@ -579,15 +583,15 @@ class _AttnPacked(torch.autograd.Function):
             t = qkv.reshape(K, B, L, 3, H, D // H).permute(3, 0, 1, 4, 2, 5)
             op = o.reshape(K, B, L, H, D // H).permute(0, 1, 3, 2, 4)
             dop = do.reshape(K, B, L, H, D // H).permute(0, 1, 3, 2, 4)
-            dq, dk, dv = ref.attn_bwd(dop, t[0], t[1], t[2], op, lse, ctx.key_valid)
+            dq, dk, dv = ref.attn_bwd(dop, t[0], t[1], t[2], op, lse, ctx.key_valid, **ctx.dr)
             dqkv = torch.stack([dq, dk, dv]).permute(1, 2, 4, 0, 3, 5).reshape(K, B, L, D3)
         else:
-            dqkv = be.attn_bwd_packed(do.contiguous(), qkv, o, lse, H, ctx.key_valid)
-        return dqkv, None, None
+            dqkv = be.attn_bwd_packed(do.contiguous(), qkv, o, lse, H, ctx.key_valid, **ctx.dr)
+        return dqkv, None, None, None, None
 
 
-def attention_packed(qkv, key_valid, H: int):
-    return _AttnPacked.apply(qkv, key_valid, H)
+def attention_packed(qkv, key_valid, H: int, drop_p: float = 0.0, drop_seeds=None):
+    return _AttnPacked.apply(qkv, key_valid, H, drop_p, drop_seeds)
 
 
 def packed_attention_ok(t: torch.Tensor, L: int, DH: int) -> bool:

@@ -717,9 +717,17 @@ def _key_valid(key_valid, q):
     return key_valid.to(device=q.device, dtype=torch.int32).reshape(-1).contiguous()
 
 
-def attn_fwd(q, k, v, key_valid=None):
+def _attn_drop(drop_p: float, drop_seeds, K: int, t):
+    if not drop_p:
+        return NULL, 0.0
+    assert drop_seeds is not None and drop_seeds.numel() == K
+    return _p(drop_seeds.to(device=t.device, dtype=torch.int32).contiguous()), float(drop_p)
+
+
+def attn_fwd(q, k, v, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     """q,k,v [K,B,Hh,L,dh] bf16 → (o [K,B,Hh,L,dh] bf16, lse [K,B,Hh,L] fp32); flash-style
-    kernel (csrc/attention.hip), never materialising the L×L scores."""
+    kernel (csrc/attention.hip), never materialising the L×L scores. drop_p / drop_seeds [K]:
+    dropout on the attention probabilities (MFMA kernels)."""
     q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
     _check(q, q.dtype, name="q")
     assert k.dtype == v.dtype == q.dtype
@@ -729,18 +737,25 @@ def attn_fwd(q, k, v, key_valid=None):
     kv = _key_valid(key_valid, q)
     o = torch.empty_like(q)
     lse = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
-    _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _f32(q), _s(), 0, 0)
+    sp, dp_ = _attn_drop(drop_p, drop_seeds, q.shape[0], q)
+    ok = _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _f32(q), _s(), 0, 0, sp,
+                     KBH // q.shape[0], dp_)
+    if not ok:
+        raise NotImplementedError(f"attention kernel: L={L} dh={DH} drop_p={drop_p} not supported")
     return o, lse
 
 
-def attn_bwd(do, q, k, v, o, lse, key_valid=None):
+def attn_bwd(do, q, k, v, o, lse, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     do, q, k, v, o = do.contiguous(), q.contiguous(), k.contiguous(), v.contiguous(), o.contiguous()
     KBH, H, L, DH = _attn_shape(q)
     kv = _key_valid(key_valid, q)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     delta = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
-    _C.attn_bwd(_p(do), _p(q), _p(k), _p(v), _p(o), _p(lse.contiguous()), _p(kv), _p(dq), _p(dk), _p(dv), _p(delta),
-                KBH, H, L, DH, _f32(q), _s(), 0, 0)
+    sp, dp_ = _attn_drop(drop_p, drop_seeds, q.shape[0], q)
+    ok = _C.attn_bwd(_p(do), _p(q), _p(k), _p(v), _p(o), _p(lse.contiguous()), _p(kv), _p(dq), _p(dk), _p(dv),
+                     _p(delta), KBH, H, L, DH, _f32(q), _s(), 0, 0, sp, KBH // q.shape[0], dp_)
+    if not ok:
+        raise NotImplementedError(f"attention kernel: L={L} dh={DH} drop_p={drop_p} not supported")
     return dq, dk, dv
 
 
@@ -748,7 +763,7 @@ def attn_packed_supported(L: int, DH: int) -> bool:
     return bool(_C.attn_packed_supported(L, DH))
 
 
-def attn_fwd_packed(qkv, H: int, key_valid=None):
+def attn_fwd_packed(qkv, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     """Attention straight from the QKV projection's output rows qkv [K, B, L, 3·D] (q | k | v
     column blocks, heads of dh = D/H inside each): returns o [K, B, L, D] — the out projection's
     input layout — and lse [K, B, H, L]. No permute / contiguous copies."""
@@ -763,13 +778,14 @@ def attn_fwd_packed(qkv, H: int, key_valid=None):
     base = qkv.data_ptr()
     es = qkv.element_size()
     _keepalive.append(qkv)
+    sp, dp_ = _attn_drop(drop_p, drop_seeds, K, qkv)
     ok = _C.attn_fwd(base, base + D * es, base + 2 * D * es, _p(kv), _p(o), _p(lse), K * B * H, H, L, DH,
-                     _f32(qkv), _s(), D3, D)
+                     _f32(qkv), _s(), D3, D, sp, B * H, dp_)
     assert ok
     return o, lse
 
 
-def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None):
+def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     """dqkv [K, B, L, 3·D] (the QKV projection's gradient layout) from do / o [K, B, L, D]."""
     K, B, L, D3 = qkv.shape
     D = D3 // 3
@@ -781,8 +797,9 @@ def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None):
     b, g, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
     _keepalive.append(qkv)
     _keepalive.append(dqkv)
+    sp, dp_ = _attn_drop(drop_p, drop_seeds, K, qkv)
     ok = _C.attn_bwd(_p(do), b, b + D * es, b + 2 * D * es, _p(o), _p(lse.contiguous()), _p(kv), g, g + D * es,
-                     g + 2 * D * es, _p(delta), K * B * H, H, L, DH, _f32(qkv), _s(), D3, D)
+                     g + 2 * D * es, _p(delta), K * B * H, H, L, DH, _f32(qkv), _s(), D3, D, sp, B * H, dp_)
     assert ok
     return dqkv
 

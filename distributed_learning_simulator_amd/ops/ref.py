@@ -314,9 +314,28 @@ def seq_mean_bwd(dy, lengths, L: int):
 
 
 # ----------------------------------------------------------------------- attention
-def attn_fwd(q, k, v, key_valid=None):
-    """q,k,v [K,B,Hh,L,dh]; key_valid [K,B] number of valid keys (padding mask) or None.
-    Returns o and the log-sum-exp [K,B,Hh,L] (fp32)."""
+def attn_drop_scale(shape, seeds, p: float, device) -> torch.Tensor:
+    """[K,B,Hh,L,L] attention-probability dropout factor M/(1−p) (attention_mfma.hip attn_keep):
+    keep iff mix32(((b·Hh + h)·L + q)·L + key, seed_k) >= p·2³² (32-bit index)."""
+    import numpy as np
+
+    from .fl import _mix
+
+    K, B, Hh, L = shape[:4]
+    thr = int(min(float(np.float32(p) * np.float32(4294967296.0)), 4294967040.0))
+    hl = torch.arange(B * Hh, dtype=torch.int64, device=device).view(B, Hh, 1, 1)
+    qi = torch.arange(L, dtype=torch.int64, device=device).view(1, 1, L, 1)
+    kj = torch.arange(L, dtype=torch.int64, device=device).view(1, 1, 1, L)
+    idx = ((hl * L + qi) * L + kj) & 0xFFFFFFFF
+    sk = (seeds.long().to(device) & 0xFFFFFFFF).view(K, 1, 1, 1, 1)
+    keep = _mix(idx.unsqueeze(0), sk) >= thr
+    return keep.float() * (1.0 / (1.0 - p))
+
+
+def attn_fwd(q, k, v, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
+    """q,k,v [K,B,Hh,L,dh]; key_valid [K,B] number of valid keys (padding mask) or None;
+    drop_p / drop_seeds [K]: dropout on the attention probabilities (nn.MultiheadAttention's
+    `dropout`). Returns o and the log-sum-exp [K,B,Hh,L] (fp32, of the undropped scores)."""
     scale = q.shape[-1] ** -0.5
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if key_valid is not None:
@@ -325,11 +344,13 @@ def attn_fwd(q, k, v, key_valid=None):
         s = s.masked_fill(~km[:, :, None, None, :], float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
     p = torch.exp(s - lse[..., None])
+    if drop_p:
+        p = p * attn_drop_scale(q.shape, drop_seeds, drop_p, q.device)
     o = torch.matmul(p, v.float())
     return o.to(q.dtype), lse
 
 
-def attn_bwd(do, q, k, v, o, lse, key_valid=None):
+def attn_bwd(do, q, k, v, o, lse, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     scale = q.shape[-1] ** -0.5
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if key_valid is not None:
@@ -337,9 +358,12 @@ def attn_bwd(do, q, k, v, o, lse, key_valid=None):
         km = torch.arange(L, device=q.device)[None, None, :] < key_valid[..., None].to(q.device)
         s = s.masked_fill(~km[:, :, None, None, :], float("-inf"))
     p = torch.exp(s - lse[..., None])
+    msk = attn_drop_scale(q.shape, drop_seeds, drop_p, q.device) if drop_p else None
     dof = do.float()
-    dv = torch.matmul(p.transpose(-1, -2), dof)
+    dv = torch.matmul((p * msk if msk is not None else p).transpose(-1, -2), dof)
     dp = torch.matmul(dof, v.float().transpose(-1, -2))
+    if msk is not None:
+        dp = dp * msk
     delta = (dof * o.float()).sum(-1, keepdim=True)
     ds = p * (dp - delta) * scale
     dq = torch.matmul(ds, k.float())

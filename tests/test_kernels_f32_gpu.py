@@ -582,3 +582,39 @@ def test_conv_halo(hip, case):
         assert torch.equal(outs[key][0], outs[(1, 0)][0]) and torch.equal(outs[key][1], outs[(1, 0)][1])
     _close(outs[(1, 0)][0], outs[(0, -1)][0].double(), tol=2e-6)
     _close(outs[(1, 0)][1], outs[(0, -1)][1].double(), tol=2e-6)
+
+
+@pytest.mark.parametrize("L,H,D", [(300, 5, 100), (128, 8, 512), (37, 2, 16)])
+@pytest.mark.parametrize("drop_p", [0.0, 0.1])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 3e-5), (torch.bfloat16, 2.5e-2)])
+def test_attention_padded_heads_and_dropout(hip, L, H, D, drop_p, dtype, tol):
+    """MFMA flash attention at the reference imdb model's dh = 20 (d_model 100, 5 heads: padded
+    to 32 on the MFMA, packed QKV rows read in place) and with attention-probability dropout
+    (nn.MultiheadAttention's dropout): against the float64 oracle with the same hash mask."""
+    K, B = 2, 3
+    dh = D // H
+    assert hip.attn_packed_supported(L, dh)
+    torch.manual_seed(L + D)
+    qkv = _f(K, B, L, 3 * D).to(dtype)
+    kv = torch.randint(1, L + 1, (K, B), device=DEV, dtype=torch.int32)
+    seeds = torch.tensor([5, -9], dtype=torch.int32, device=DEV)
+    dr = {"drop_p": drop_p, "drop_seeds": seeds} if drop_p else {}
+    rdr = {"drop_p": drop_p, "drop_seeds": seeds.cpu()} if drop_p else {}
+    o, lse = hip.attn_fwd_packed(qkv, H, kv, **dr)
+
+    def heads(t):
+        return t.reshape(K, B, L, H, dh).permute(0, 1, 3, 2, 4)
+
+    q, k, v = (heads(_d(t)) for t in qkv.split(D, dim=-1))
+    o2, lse2 = ref.attn_fwd(q, k, v, kv.cpu(), **rdr)
+    flat = lambda t: t.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)  # noqa: E731
+    _close(o, flat(o2), tol)
+    _close(lse, lse2, max(tol, 1e-5))
+    do = _f(K, B, L, D).to(dtype)
+    dqkv = hip.attn_bwd_packed(do, qkv, o, lse, H, kv, **dr)
+    rq, rk, rv = ref.attn_bwd(heads(_d(do)), q, k, v, o2, lse2, kv.cpu(), **rdr)
+    _close(dqkv, torch.cat([flat(rq), flat(rk), flat(rv)], -1), tol * 2)
+    # the unpacked layout agrees with the packed one
+    qc, kc, vc = (heads(t).contiguous() for t in qkv.split(D, dim=-1))
+    o3, _ = hip.attn_fwd(qc, kc, vc, kv, **dr)
+    _close(flat(o3), o.double(), 1e-6)

@@ -239,7 +239,7 @@ def test_transformer_dropout_epilogues_match_explicit_masks(monkeypatch):
 
     def plain(self, x, ctx, key_valid):
         p = self.dropout
-        a = self.self_attn.forward(x, ctx, key_valid)
+        a = self.self_attn.forward(x, ctx, key_valid, attn_drop=p)
         x = self.norm1.forward(x + ref.dropout_apply(a, ctx.dropout_seeds(), p), ctx)
         h = ref.dropout_apply(torch.relu(self.linear1.forward(x, ctx)), ctx.dropout_seeds(), p)
         f = self.linear2.forward(h, ctx)
@@ -253,3 +253,31 @@ def test_transformer_dropout_epilogues_match_explicit_masks(monkeypatch):
     seeds = torch.tensor([11, 12], dtype=torch.int32)
     keep = ref.dropout_keep(2, 48, 16, seeds, 0.3)
     assert 0.6 < keep.float().mean().item() < 0.8 and not torch.equal(keep[0], keep[1])
+
+
+def test_attention_dropout_reference_matches_autograd():
+    """Attention-probability dropout (nn.MultiheadAttention(dropout=p)): ops.ref attn_fwd /
+    attn_bwd with a hash mask == float64 autograd of softmax(QKᵀ/√d)∘M/(1−p)·V with the same
+    mask; about p of the probabilities are dropped and the mask differs between clients."""
+    from distributed_learning_simulator_amd.ops import ref
+
+    torch.manual_seed(1)
+    K, B, H, L, dh, p = 2, 2, 3, 11, 20, 0.25
+    q, k, v, do = (torch.randn(K, B, H, L, dh, dtype=torch.float64) for _ in range(4))
+    kv = torch.tensor([[11, 7], [4, 11]])
+    seeds = torch.tensor([123, -77], dtype=torch.int32)
+    o, lse = ref.attn_fwd(q, k, v, kv, drop_p=p, drop_seeds=seeds)
+    dq, dk, dv = ref.attn_bwd(do, q, k, v, o, lse, kv, drop_p=p, drop_seeds=seeds)
+    m = ref.attn_drop_scale(q.shape, seeds, p, q.device).double()
+    qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+    s = qa @ ka.transpose(-1, -2) * dh ** -0.5
+    km = torch.arange(L)[None, None, :] < kv[..., None]
+    s = s.masked_fill(~km[:, :, None, None, :], float("-inf"))
+    oa = (torch.softmax(s, -1) * m) @ va
+    oa.backward(do)
+    # (ops.ref computes in fp32)
+    torch.testing.assert_close(o, oa.detach(), rtol=1e-5, atol=2e-6)
+    for got, exp in ((dq, qa.grad), (dk, ka.grad), (dv, va.grad)):
+        torch.testing.assert_close(got, exp, rtol=1e-5, atol=2e-6)
+    kept = (m > 0).float().mean().item()
+    assert abs(kept - (1 - p)) < 0.05 and not torch.equal(m[0], m[1])
