@@ -703,8 +703,11 @@ int resolve_tn_f32_variant(int variant, int K, int Co, int R, int va, int vb) {
 }
 
 void tn_f32_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
+  // per-client decision (a reference cohort of 32): the deterministic fold's order must not
+  // depend on how many clients share the launch (see conv_pl.hip tn_pl_split)
+  (void)K;
   const TnTile t = kTnF32Tiles[variant];
-  const long tiles = (long)K * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  const long tiles = (long)32 * cdiv(Co, t.bm) * cdiv(R, t.bn);
   splitk = 1;
   const int target = 1024;  // >= 4 blocks per CU
   if (tiles < target) {

@@ -585,9 +585,14 @@ int tn_pl_default_variant(int K, int Co, int R) {
   return Co <= 64 ? 1 : 0;
 }
 
+// split-K factor from PER-CLIENT quantities only (as if KREF clients shared the launch): a
+// client's weight gradient — summation order included — is then the same whatever cohort size,
+// stream or rank trains it (1-rank ≡ N-rank, bitwise)
+constexpr int KREF = 32;
 void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
+  (void)K;
   const TnPlTile t = kTnPlTiles[variant];
-  const long tiles = (long)K * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  const long tiles = (long)KREF * cdiv(Co, t.bm) * cdiv(R, t.bn);
   splitk = 1;
   const int target = 512;  // ≥ 2 blocks per CU
   if (tiles < target) {

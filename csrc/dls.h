@@ -197,7 +197,10 @@ void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* 
 void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,
             long rows_per_client, int C, void* dx, float* dgamma, float* dbeta, long dg_cs, float* ws, int f32,
             hipStream_t s);
-void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, int f32, hipStream_t s);
+long col_sum_workspace_floats(int K, long rows, int C);
+long ln_workspace_floats(int K, long rows_per_client, int C);
+void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, int f32, hipStream_t s,
+             float* ws = nullptr);
 
 // ------------------------------------------------------------------- elementwise
 void pool_fwd(const void* x, void* y, int* idx, int K, int B, int H, int W, int C, int OH, int OW, int k, int stride,
@@ -207,7 +210,7 @@ void pool_bwd(const void* dy, const int* idx, void* dx, int K, int B, int H, int
 void gap_fwd(const void* x, void* y, int KB, int HW, int C, int f32, hipStream_t s);
 void gap_bwd(const void* dy, void* dx, int KB, int HW, int C, int f32, hipStream_t s);
 void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* loss, float* correct, void* dlogits,
-                int K, int B, int NC, int f32, hipStream_t s);
+                int K, int B, int NC, int f32, hipStream_t s, float* rowbuf = nullptr);  // rowbuf [2][K][B]: deterministic row-order loss / correct sums
 void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStream_t s);
 
 // ------------------------------------------------------------- FL / optimiser
@@ -278,6 +281,10 @@ void embedding_fwd(const int* tokens, const void* table, void* out, int K, long 
                    int f32, hipStream_t s, float scale = 1.f, const float* pe = nullptr, int L = 0);
 void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long n_tok, int D, long t_cs, int f32,
                    hipStream_t s, float scale = 1.f);
+// deterministic form: keys [n] = client·V + token sorted (stable), order [n] their row indices;
+// dtable rows of absent tokens are left untouched (zero them first)
+void embedding_bwd_sorted(const int* keys, const int* order, const void* dy, float* dtable, long n, int D, int V,
+                          long t_cs, int f32, hipStream_t s, float scale = 1.f);
 // masked mean over the sequence axis of x [S][L][D] (valid length per sequence)
 void seq_mean_fwd(const void* x, const int* len, void* y, long S, int L, int D, int f32, hipStream_t s);
 void seq_mean_bwd(const void* dy, const int* len, void* dx, long S, int L, int D, int f32, hipStream_t s);

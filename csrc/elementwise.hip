@@ -157,7 +157,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) ce_kernel(const T* __restrict__ logits, const int* __restrict__ labels,
                                                  const int* __restrict__ valid, float* __restrict__ loss,
                                                  float* __restrict__ correct, T* __restrict__ dlogits, int B,
-                                                 int NC) {
+                                                 int NC, float* __restrict__ rowbuf) {
   const int k = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -166,6 +166,7 @@ __global__ void __launch_bounds__(256) ce_kernel(const T* __restrict__ logits, c
   const long off = ((long)k * B + row) * NC;
   if (row >= nv) {
     for (int c = lane; c < NC; c += 64) stf(dlogits + off + c, 0.f);
+    if (rowbuf && lane == 0) rowbuf[(long)k * B + row] = rowbuf[((long)gridDim.y + k) * B + row] = 0.f;
     return;
   }
   const float inv_n = 1.f / (float)max(nv, 1);
@@ -198,9 +199,28 @@ __global__ void __launch_bounds__(256) ce_kernel(const T* __restrict__ logits, c
   }
   if (lane == 0) {
     const float nll = lse - ldf(logits + off + lab);
-    atomicAdd(&loss[k], nll * inv_n);
-    if (amax == lab) atomicAdd(&correct[k], 1.f);
+    if (rowbuf) {  // per-row terms, summed in row order by ce_fold_kernel (deterministic)
+      rowbuf[(long)k * B + row] = nll * inv_n;
+      rowbuf[((long)gridDim.y + k) * B + row] = amax == lab ? 1.f : 0.f;
+    } else {
+      atomicAdd(&loss[k], nll * inv_n);
+      if (amax == lab) atomicAdd(&correct[k], 1.f);
+    }
   }
+}
+
+// loss[k] = Σ_row rowbuf[0][k][row], correct[k] = Σ_row rowbuf[1][k][row], rows in order
+__global__ void ce_fold_kernel(const float* __restrict__ rowbuf, float* __restrict__ loss, float* __restrict__ correct,
+                               int K, int B) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float a = 0.f, c = 0.f;
+  for (int r = 0; r < B; ++r) {
+    a += rowbuf[(long)k * B + r];
+    c += rowbuf[((long)K + k) * B + r];
+  }
+  loss[k] = a;
+  correct[k] = c;
 }
 
 template <typename T>
@@ -616,6 +636,39 @@ __global__ void embedding_bwd_kernel(const int* __restrict__ tok, const T* __res
   atomicAdd(&dtable[(long)k * t_cs + (long)tok[row] * D + d], ldf(dy + i) * scale);
 }
 
+// Deterministic embedding backward: rows sorted by key = client·V + token (stable, so equal keys
+// keep their sequence order); the wave of a segment's first row sums the segment's dY rows in
+// that order and writes the table row once — no atomics, bitwise-reproducible
+template <typename T>
+__global__ void __launch_bounds__(256) embedding_bwd_sorted_kernel(const int* __restrict__ keys,
+                                                                   const int* __restrict__ order,
+                                                                   const T* __restrict__ dy, float* __restrict__ dtable,
+                                                                   long n, int D, int V, long t_cs, float scale) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  const int key = keys[r];
+  if (r > 0 && keys[r - 1] == key) return;
+  const int k = key / V, tok = key - k * V;
+  float* out = dtable + (long)k * t_cs + (long)tok * D;
+  for (int d0 = 0; d0 < D; d0 += 64 * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long i = r; i < n && keys[i] == key; ++i) {
+      const T* row = dy + (long)order[i] * D;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = d0 + j * 64 + lane;
+        if (d < D) acc[j] += ldf(row + d);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = d0 + j * 64 + lane;
+      if (d < D) out[d] = acc[j] * scale;
+    }
+  }
+}
+
 // masked mean over the sequence: y[s, :] = Σ_{t < len[s]} x[s, t, :] / max(len[s], 1)
 template <typename T>
 __global__ void seq_mean_fwd_kernel(const T* __restrict__ x, const int* __restrict__ len, T* __restrict__ y, int L,
@@ -698,11 +751,14 @@ void gap_bwd(const void* dy, void* dx, int KB, int HW, int C, int f32, hipStream
 }
 
 void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* loss, float* correct, void* dlogits,
-                int K, int B, int NC, int f32, hipStream_t s) {
-  DLS_CHECK(hipMemsetAsync(loss, 0, sizeof(float) * K, s));
-  DLS_CHECK(hipMemsetAsync(correct, 0, sizeof(float) * K, s));
+                int K, int B, int NC, int f32, hipStream_t s, float* rowbuf) {
+  if (!rowbuf) {
+    DLS_CHECK(hipMemsetAsync(loss, 0, sizeof(float) * K, s));
+    DLS_CHECK(hipMemsetAsync(correct, 0, sizeof(float) * K, s));
+  }
   DISPATCH_T(f32, hipLaunchKernelGGL(ce_kernel<TT>, dim3(cdiv(B, 4), K), dim3(256), 0, s, CP(logits), labels, valid,
-                                     loss, correct, MP(dlogits), B, NC));
+                                     loss, correct, MP(dlogits), B, NC, rowbuf));
+  if (rowbuf) hipLaunchKernelGGL(ce_fold_kernel, dim3(cdiv(K, 64)), dim3(64), 0, s, rowbuf, loss, correct, K, B);
 }
 
 void relu_bwd(const void* dy, const void* y, void* dx, long n, int f32, hipStream_t s) {
@@ -816,6 +872,12 @@ void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long
   const long total = (long)K * n_tok * D;
   DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_kernel<TT>, dim3(cdiv(total, 256)), dim3(256), 0, s, tokens, CP(dy),
                                      dtable, n_tok, D, t_cs, total, scale));
+}
+
+void embedding_bwd_sorted(const int* keys, const int* order, const void* dy, float* dtable, long n, int D, int V,
+                          long t_cs, int f32, hipStream_t s, float scale) {
+  DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_sorted_kernel<TT>, dim3(cdiv(n, 4)), dim3(256), 0, s, keys, order,
+                                     CP(dy), dtable, n, D, V, t_cs, scale));
 }
 
 void seq_mean_fwd(const void* x, const int* len, void* y, long S, int L, int D, int f32, hipStream_t s) {

@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
             s0[i] += va[i];
             s1[i] += va[i] * va[i];
           }
-        } else if (MODE == 2) {
+        } else if (MODE >= 2) {
 #pragma unroll
           for (int i = 0; i < V; ++i) s0[i] += va[i];
         } else {
@@ -165,6 +165,10 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
       if (MODE == 2) {  // column sums straight into a (pre-zeroed) strided output
 #pragma unroll
         for (int i = 0; i < V; ++i) atomicAdd(&ws[(long)k * ws_cs + c0 + i], s0[i]);
+      } else if (MODE == 3) {  // column-sum partials [K][gridDim.x][C], folded in order
+        float* part = ws + ((long)k * gridDim.x + blockIdx.x) * C;
+#pragma unroll
+        for (int i = 0; i < V; ++i) part[c0 + i] = s0[i];
       } else {  // per-workgroup partials [K][gridDim.x][2C]: deterministic, no memset, no atomics
         float* part = ws + ((long)k * gridDim.x + blockIdx.x) * 2 * C;
 #pragma unroll
@@ -176,7 +180,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
     }
     __syncthreads();
   }
-  if (MODE == 2 || ca.counters == nullptr) return;
+  if (MODE >= 2 || ca.counters == nullptr) return;
   // ---- last-arriver coefficient stage (cdna_hip_programming.md Guideline 16 protocol)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's partials issued+done
   __syncthreads();
@@ -534,7 +538,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const T* __restrict__ gamma, long g_cs, long rpc, int C,
                                                      T* __restrict__ dx, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, long dg_cs, int rows_per_wave) {
+                                                     float* __restrict__ dbeta, long dg_cs, int rows_per_wave,
+                                                     float* __restrict__ part) {
   // grid: (row-groups, K); each wave handles rows_per_wave rows of client k
   const int k = blockIdx.y;
   const int lane = threadIdx.x & 63;
@@ -574,16 +579,37 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
-  if (rend > rbeg) {
+  if (rend > rbeg || part) {  // (partials: every wave writes its row, zeros included)
 #pragma unroll
     for (int i = 0; i < LN_MAXC; ++i) {
       const int c = lane + 64 * i;
       if (c < C) {
-        atomicAdd(&dgamma[(long)k * dg_cs + c], dg[i]);
-        atomicAdd(&dbeta[(long)k * dg_cs + c], db[i]);
+        if (part) {  // this wave's partial row [2C], folded in wave order (deterministic)
+          float* pw = part + ((long)k * gridDim.x * 4 + wave) * 2 * C;
+          pw[c] = dg[i];
+          pw[C + c] = db[i];
+        } else {
+          atomicAdd(&dgamma[(long)k * dg_cs + c], dg[i]);
+          atomicAdd(&dbeta[(long)k * dg_cs + c], db[i]);
+        }
       }
     }
   }
+}
+
+// out0[k·out_cs + c] = Σ_b part[(k·nparts + b)·W + c] (b ascending), out1 likewise at column C + c
+__global__ void __launch_bounds__(256) part_sum_kernel(const float* __restrict__ part, int nparts, int W, int C,
+                                                       float* __restrict__ out0, float* __restrict__ out1, long out_cs) {
+  const int k = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* p = part + (long)k * nparts * W;
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < nparts; ++i) {
+    a += p[(long)i * W + c];
+    if (out1) b += p[(long)i * W + C + c];
+  }
+  out0[(long)k * out_cs + c] = a;
+  if (out1) out1[(long)k * out_cs + c] = b;
 }
 
 }  // namespace
@@ -691,11 +717,25 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   });
 }
 
-void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, int f32, hipStream_t s) {
-  // out must be zeroed by the caller (it is a strided view of the grad buffer)
+long col_sum_workspace_floats(int K, long rows, int C) {
+  const int rpb = rows_per_block(rows, K);
+  return (long)K * cdiv(rows, rpb) * C;
+}
+
+void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, int f32, hipStream_t s, float* ws) {
+  // ws (col_sum_workspace_floats): per-workgroup partials folded in order into out (any prior
+  // contents overwritten, deterministic); without ws, atomics into out (zeroed by the caller)
   const int rpb = rows_per_block(rows, K);
   dim3 grid(cdiv(rows, rpb), K);
   const int V = vw(C);
+  if (ws) {
+    DISPATCH_T(f32, DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 3>), grid, dim3(256), 0, s, CP(x),
+                                                     nullptr, nullptr, nullptr, nullptr, nullptr, (int)rows, C, 0, ws,
+                                                     0L, rpb, nullptr, BNCoefArgs{}, C, C)));
+    hipLaunchKernelGGL(part_sum_kernel, dim3(cdiv(C, 256), K), dim3(256), 0, s, ws, (int)grid.x, C, C, out,
+                       (float*)nullptr, out_cs);
+    return;
+  }
   DISPATCH_T(f32, DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 2>), grid, dim3(256), 0, s, CP(x),
                                                    nullptr, nullptr, nullptr, nullptr, nullptr, (int)rows, C, 0, out,
                                                    out_cs, rpb, nullptr, BNCoefArgs{}, C, C)));
@@ -708,11 +748,23 @@ void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* 
                                      CP(beta), MP(y), mean, rstd, g_cs, nrows, rpc, C, eps, rep));
 }
 
+static int ln_rows_per_wave(long rpc) { return rpc >= 4096 ? 64 : 16; }
+
+long ln_workspace_floats(int K, long rpc, int C) {
+  const long waves = (rpc + ln_rows_per_wave(rpc) - 1) / ln_rows_per_wave(rpc);
+  return (long)K * cdiv(waves, 4) * 4 * 2 * C;
+}
+
 void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,
             long rpc, int C, void* dx, float* dgamma, float* dbeta, long dg_cs, float* ws, int f32, hipStream_t s) {
-  const int rows_per_wave = 16;
+  // ws (ln_workspace_floats): per-wave dγ / dβ partials folded in wave order (deterministic,
+  // overwrites dgamma / dbeta); without ws, atomics into zeroed dgamma / dbeta
+  const int rows_per_wave = ln_rows_per_wave(rpc);
   const long waves = (rpc + rows_per_wave - 1) / rows_per_wave;
   dim3 grid(cdiv(waves, 4), K);
   DISPATCH_T(f32, hipLaunchKernelGGL(ln_bwd_kernel<TT>, grid, dim3(256), 0, s, CP(dy), CP(x), mean, rstd, CP(gamma),
-                                     g_cs, rpc, C, MP(dx), dgamma, dbeta, dg_cs, rows_per_wave));
+                                     g_cs, rpc, C, MP(dx), dgamma, dbeta, dg_cs, rows_per_wave, ws));
+  if (ws)
+    hipLaunchKernelGGL(part_sum_kernel, dim3(cdiv(C, 256), K), dim3(256), 0, s, ws, (int)grid.x * 4, 2 * C, C, dgamma,
+                       dbeta, dg_cs);
 }

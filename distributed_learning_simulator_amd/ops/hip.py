@@ -382,13 +382,23 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int, dy_planes=None, x_planes=None):
                ldy, ldx, dy_planes if use_pl else None, x_planes if use_pl else None)
 
 
+def _col_sum(x, out, K: int, rows: int, C: int):
+    """out[k, c] = Σ_rows x[k, row, c] (fp32, into a strided gradient view): partials folded in
+    order when deterministic, else fp32 atomics into the zeroed view."""
+    if deterministic:
+        ws = _tn_part(_C.col_sum_workspace_floats(K, rows, C), x.device)
+        _C.col_sum(_p(x), _p(out), out.stride(0), K, rows, C, _f32(x), _s(), _p(ws))
+    else:
+        out.zero_()
+        _C.col_sum(_p(x), _p(out), out.stride(0), K, rows, C, _f32(x), _s(), NULL)
+
+
 def bias_grad(dy, gb):
     """gb[k, c] = Σ_{b,h,w} dy[k, b, h, w, c] (conv bias gradient)."""
     K = dy.shape[0]
     C = dy.shape[-1]
     rows = dy.numel() // (K * C)
-    gb.zero_()
-    _C.col_sum(_p(dy.contiguous()), _p(gb), gb.stride(0), K, rows, C, _f32(dy), _s())
+    _col_sum(dy.contiguous(), gb, K, rows, C)
 
 
 # --------------------------------------------------------------------------- linear
@@ -464,8 +474,7 @@ def linear_wgrad(dy, x, gw, gb=None):
     assert gw.shape == (K, Fo, Fi) and gw[0].is_contiguous()
     _tn_launch(dy, x, gw, N * Fo, N * Fi, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, N, Fo, Fi, K, f32, 0, 0)
     if gb is not None:
-        gb.zero_()
-        _C.col_sum(_p(dy), _p(gb), gb.stride(0), K, N, Fo, f32, _s())
+        _col_sum(dy, gb, K, N, Fo)
 
 
 # ------------------------------------------------------------------------ batchnorm
@@ -586,10 +595,16 @@ def ln_bwd(dy, x, mean, rstd, gamma):
     g_cs, rep = _client_view(gamma, K)
     rpc = x.numel() // (K * C)
     dx = torch.empty_like(x)
-    dgamma = torch.zeros((K, C), dtype=torch.float32, device=x.device)
-    dbeta = torch.zeros((K, C), dtype=torch.float32, device=x.device)
+    if deterministic:
+        dgamma = torch.empty((K, C), dtype=torch.float32, device=x.device)
+        dbeta = torch.empty((K, C), dtype=torch.float32, device=x.device)
+        ws = _p(_tn_part(_C.ln_workspace_floats(K, rpc, C), x.device))
+    else:
+        dgamma = torch.zeros((K, C), dtype=torch.float32, device=x.device)
+        dbeta = torch.zeros((K, C), dtype=torch.float32, device=x.device)
+        ws = NULL
     _C.ln_bwd(_p(dy.contiguous()), _p(x), _p(mean), _p(rstd), _p(gamma), g_cs, K, rpc, C, _p(dx), _p(dgamma),
-              _p(dbeta), C, _f32(x), _s())
+              _p(dbeta), C, _f32(x), _s(), ws)
     return dx, dgamma, dbeta
 
 
@@ -653,7 +668,9 @@ def ce_fwd_bwd(logits, labels, valid=None):
     loss = torch.empty(K, dtype=torch.float32, device=logits.device)
     correct = torch.empty(K, dtype=torch.float32, device=logits.device)
     dlogits = torch.empty_like(logits)
-    _C.ce_fwd_bwd(_p(logits), _p(lab), _p(v), _p(loss), _p(correct), _p(dlogits), K, B, NC, _f32(logits), _s())
+    rowbuf = torch.empty((2, K, B), dtype=torch.float32, device=logits.device) if deterministic else None
+    _C.ce_fwd_bwd(_p(logits), _p(lab), _p(v), _p(loss), _p(correct), _p(dlogits), K, B, NC, _f32(logits), _s(),
+                  _p(rowbuf))
     return loss, correct, dlogits
 
 
@@ -679,6 +696,14 @@ def embedding_bwd(dy, tokens, gtable, scale: float = 1.0):
     tok = tokens.to(torch.int32).contiguous()
     D = dy.shape[-1]
     gtable.zero_()
+    if deterministic:
+        # rows grouped by (client, token) with a stable sort; each group summed in sequence order
+        V = gtable.shape[1]
+        keys = (tok.view(K, -1) + torch.arange(K, device=tok.device, dtype=torch.int32)[:, None] * V).reshape(-1)
+        sk, order = torch.sort(keys, stable=True)
+        _C.embedding_bwd_sorted(_p(sk.contiguous()), _p(order.to(torch.int32).contiguous()), _p(dy.contiguous()),
+                                _p(gtable), keys.numel(), D, V, gtable.stride(0), _f32(dy), _s(), float(scale))
+        return
     _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _f32(dy), _s(),
                      float(scale))
 

@@ -149,3 +149,18 @@ def test_resnet18_bitwise_reproducible_and_planes(hip, tmp_path, monkeypatch):
     monkeypatch.setattr(Fn, "PLANES", False)
     c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
     assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
+
+
+def test_transformer_imdb_bitwise_reproducible_and_matches_cpu(hip, tmp_path):
+    """The reference's imdb Transformer (d_model 100, 5 heads: dh 20 on the MFMA attention, with
+    attention-probability dropout): two GPU runs are bitwise equal (deterministic LN / bias /
+    embedding / CE reductions, no atomics) and the GPU agrees with the CPU oracle, which applies
+    the same dropout masks."""
+    ov = {"round": 1, "epoch": 1, "worker_number": 2, "dataset_kwargs.scale": 0.004, "dataset_kwargs.max_len": 64,
+          "model_kwargs.max_len": 64}
+    a, ra = _run("fed_avg/imdb.yaml", ov, tmp_path / "a", "cuda")
+    b, _ = _run("fed_avg/imdb.yaml", ov, tmp_path / "b", "cuda")
+    assert torch.equal(a.server.global_parameter, b.server.global_parameter)
+    c, rc = _run("fed_avg/imdb.yaml", ov, tmp_path / "c", "cpu")
+    assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
+    assert abs(_losses(ra)[-1] - _losses(rc)[-1]) < 1e-3
