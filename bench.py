@@ -79,6 +79,9 @@ def main() -> None:
     ap.add_argument("--amp", action="store_true",
                     help="bf16 fast mode (use_amp: true). Default: fp32, the reference's precision "
                          "(conf/global.yaml use_amp: false) — split-bf16 MFMA GEMMs, fp32 storage/accumulate")
+    ap.add_argument("--shard-scale", type=float, default=0.1,
+                    help="signsgd_resnet50: fraction of ImageNet dealt to the 128 clients (1.0 = full shards, "
+                         "10k images per client, 79 vote steps per round)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostic: time rank 0's share of an N-rank round alone on one GPU "
                          "(collectives are no-ops; not the benchmark contract)")
@@ -233,6 +236,8 @@ def main() -> None:
         }
         if stage2 is not None:
             out["stage2"] = stage2
+        if "extra" in wl:
+            out.update(wl["extra"](sess, elapsed / args.steps))
         print(json.dumps(out), flush=True)
     # tear the process group down on every rank (an exiting rank with a live gloo/RCCL group
     # aborts in the communicator's destructor)
@@ -313,14 +318,32 @@ def workload_config(args, rounds: int) -> dict:
                 "metric": "FL rounds/sec (FedOBD stage 1, 100 clients / 50 per round, Transformer-base, AG-News-shaped)",
                 "data": "synthetic (AG-News-shaped token sequences, max_len 128, iid shards, random-init weights)"}
     if args.workload == "signsgd_resnet50":
+        scale = float(args.shard_scale)
         cfg = {"distributed_algorithm": "sign_SGD", "dataset_name": "ImageNet", "model_name": "Resnet50",
-               "dataset_kwargs": {"scale": 0.1}, "worker_number": 128, "epoch": 1, "batch_size": 128,
+               "dataset_kwargs": {"scale": scale}, "worker_number": 128, "epoch": 1, "batch_size": 128,
                "optimizer_name": "SGD", "learning_rate": 0.001, "momentum": 0.0, "distribute_init_parameters": False}
+
+        def vote_steps(sess):
+            name = sess.dc.spec.name
+            B = sess.config.batch_size
+            return max(1, max((p.dataset_size(name) + B - 1) // B for p in sess.practitioners.values()))
+
+        def extra(sess, s_per_round):
+            # a round is one local epoch of synchronous steps; every step is one 1-bit majority vote
+            # over all 128 clients (reference gradient_worker.py:86-91 exchanges per optimizer step)
+            n = vote_steps(sess) * sess.config.epoch
+            return {"vote_steps_per_round": n, "ms_per_vote_step": s_per_round / n * 1e3,
+                    "vote_steps_per_s": n / s_per_round,
+                    "wire": ("1 bit/param/client accounted each way (packed sign words); the cross-rank vote "
+                             "all-reduce carries 16-bit counts (fp16, exact up to 2048 clients)")}
+
+        pct = f"{scale * 100:g}%"
         return {"config": {**cfg, **common}, "metric": "FL rounds/sec (sign-SGD, 128 clients, ResNet-50, ImageNet-shaped)",
-                # 10 % of ImageNet dealt to 128 clients (1,000 images each): a round is one local epoch,
-                # 8 synchronous steps of batch 128, each a 1-bit vote exchange across all clients
-                "data": "synthetic (ImageNet-shaped 224x224, 10% scale shards, random-init weights)",
-                "samples_per_round": shard_samples}
+                # `scale` of ImageNet dealt to 128 clients (0.1: 1,000 images each, 8 steps of batch 128 per
+                # round; 1.0: the full 1.28M images, 10k per client, 79 steps)
+                "data": f"synthetic (ImageNet-shaped 224x224, {pct} scale shards, random-init weights)",
+                "samples_per_round": shard_samples, "extra": extra,
+                "config_extra": {"shard_scale": scale}}
     # utility v(S) = test accuracy of the subset model on the FULL test split (reference
     # shapley_value_algorithm.py:67-76); 5 local epochs as conf/gtg_sv/cifar10.yaml
     cfg = {"distributed_algorithm": "GTG_shapley_value", "dataset_name": "CIFAR10", "model_name": "ResNet18",

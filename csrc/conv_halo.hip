@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   const auto ar = make_rsrc(p.x + (long)client * p.x_cs, (uint32_t)((p.x_lo + a_img) * 2));
   const uint32_t a_lo = (uint32_t)(p.x_lo * 2);
   const long w_ext = BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R;
-  const auto br = make_rsrc(p.wsplit + (long)client * p.ws_cs, (uint32_t)((p.ws_plane + w_ext) * 2));
+  const auto br = make_rsrc(p.wsplit + (long)(client / p.rep) * p.ws_cs, (uint32_t)((p.ws_plane + w_ext) * 2));
   const uint32_t b_lo = (uint32_t)(p.ws_plane * 2);
 
   // ---- halo loader: instruction i of wave w fills halo rows (i·NW + w)·16 + lane/4, physical
@@ -273,7 +273,7 @@ void conv_halo_set_variant(int v) { g_halo_variant = v; }
 static int halo_config(const ConvNTParams& p) {
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.pad_w != 1 || p.dil != 1) return -1;
   if (p.OH != p.H || p.OW != p.W || p.out_s > 1 || p.C % 32 || p.N % 8 || p.ldx % 8 || p.R != 9 * p.C) return -1;
-  if (p.x_lo == 0 || p.wsplit == nullptr || p.rep != 1) return -1;
+  if (p.x_lo == 0 || p.wsplit == nullptr) return -1;
   if (p.OW == 32 && p.OH % 8 == 0 && p.N <= 64) return 0;  // 1 × 8 × 32, BN 64
   if (p.OW == 16 && p.OH == 16) return 1;                   // 1 × 16 × 16, BN 128
   if (p.OW == 8 && p.OH == 8 && p.B % 2 == 0) return 2;     // 2 × 8 × 8, BN 128

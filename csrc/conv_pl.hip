@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
   const auto ar = make_rsrc(p.x + (long)client * p.x_cs, (uint32_t)((p.x_lo + a_img) * 2));
   const uint32_t a_lo = (uint32_t)(p.x_lo * 2);
   const long w_ext = BKM ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R;
-  const auto br = make_rsrc(p.wsplit + (long)client * p.ws_cs, (uint32_t)((p.ws_plane + w_ext) * 2));
+  const auto br = make_rsrc(p.wsplit + (long)(client / p.rep) * p.ws_cs, (uint32_t)((p.ws_plane + w_ext) * 2));
   const uint32_t b_lo = (uint32_t)(p.ws_plane * 2);
 
   // ---- A loader: instruction i of wave w fills tile rows (i·NW + w)·RI + lane / CR, physical
@@ -281,7 +281,7 @@ void conv_nt_pl_set_variant(int v) { g_pl_variant = v; }
 int conv_nt_pl_num_variants() { return 8; }
 
 bool conv_nt_pl_supported(const ConvNTParams& p) {
-  return p.x_lo != 0 && p.wsplit != nullptr && p.rep == 1 && p.dil == 1 && p.C % PK == 0 && p.ldx % 8 == 0 &&
+  return p.x_lo != 0 && p.wsplit != nullptr && p.dil == 1 && p.C % PK == 0 && p.ldx % 8 == 0 &&
          p.N % 8 == 0 && (p.R == p.KH * p.KW * p.C || p.R == 0);
 }
 

@@ -40,6 +40,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         self._block_ids: torch.Tensor | None = None
         self._kind: str | None = None
         self._dataset_size = 0.0
+        self._reported = 0  # clients whose upload this round's accumulator holds (all ranks after _reduce)
 
     # weights hook (reference `_get_weight`): dataset size
     def _weights(self, msg: CohortMessage) -> torch.Tensor:
@@ -65,6 +66,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 self._w_block = bw if self._w_block is None else self._w_block + bw
                 self._block_ids = msg.extra["block_ids"]
         self._w_total += w.sum()
+        self._reported += len(msg.client_ids)
         self._dataset_size += float(msg.dataset_sizes.sum().item()) if not msg.dataset_sizes.is_cuda else 0.0
 
     @property
@@ -93,20 +95,30 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             self._block_ids = self.block_ids
 
     def _reduce(self) -> None:
+        """fp64 accumulator + weights summed over ranks. The host-side round flags (end_training,
+        whether any rank carries other_data, how many clients reported) ride in the same small
+        all-reduce, read with ONE host transfer; the pickled all_gather_object runs only in a
+        round where some rank actually has other_data to merge."""
         comm = self.comm
-        if comm.world > 1:
-            # end_training / other_data must agree on every server replica
-            flags = comm.all_gather_object((self._end_training, self._other_data))
-            for end, other in flags:
-                if end is not None:
-                    self._end_training = bool(self._end_training) or end
-                for k, v in other.items():
-                    self._other_data.setdefault(k, v)
-        comm.all_reduce_(self._acc)
         small = [self._w_total] + ([self._w_block] if self._w_block is not None else [])
+        flags = None
+        if comm.world > 1:
+            flags = torch.tensor([1.0 if self._end_training else 0.0, 1.0 if self._other_data else 0.0,
+                                  float(self._reported)], dtype=torch.float64, device=self.device)
+            small.append(flags)
+        comm.all_reduce_(self._acc)
         comm.all_reduce_many_(small)
         if self._w_elem is not None:
             comm.all_reduce_(self._w_elem)
+        if flags is not None:
+            end, other, reported = flags.tolist()
+            self._reported = int(reported)
+            if end > 0:
+                self._end_training = True
+            if other > 0:  # end_training / other_data must agree on every server replica
+                for _, od in comm.all_gather_object((self._end_training, self._other_data)):
+                    for k, v in od.items():
+                        self._other_data.setdefault(k, v)
 
     def aggregate_worker_data(self, old_parameter: torch.Tensor) -> FlatParameterMessage:
         self._ensure_acc()
@@ -137,7 +149,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 new = torch.where(wt > 0, old + acc / wt.clamp(min=1e-300), old)
             else:
                 new = torch.where(wt > 0, acc / wt.clamp(min=1e-300), old)
-            if not bool(wt.item() > 0):
+            if self._reported == 0:  # (host-side count: no device read)
                 get_logger().warning("round without any reported client: global model unchanged")
         self.last_fp64 = new  # pre-cast fp64 result (golden tests)
         new = new.to(old_dtype)
@@ -149,6 +161,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
         return msg
 
     def _reset_acc(self) -> None:
+        self._reported = 0
         self._acc = None
         self._w_total = None
         self._w_elem = None

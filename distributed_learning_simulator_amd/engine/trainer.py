@@ -555,6 +555,15 @@ class CohortTrainer:
         rank, world = shard
         lo, hi = nb * rank // world, nb * (rank + 1) // world
         compute = theta_rows.to(self.compute_dtype)
+        # fp32 on the GPU: the models' (hi, lo) weight planes, so the evaluation's convolutions run
+        # the split-plane LDS-DMA GEMMs (the BatchNorms then emit activation planes, as in training);
+        # every virtual client (model m, batch b) reads model m's planes (rep = batches per launch)
+        split = None
+        if (self.buffers.split is not None and self.model.input_kind == "image" and compute.dtype == torch.float32
+                and compute.is_cuda):
+            compute = compute.contiguous()
+            split = torch.empty((M, 2, compute.shape[1]), dtype=torch.bfloat16, device=self.device)
+            fl.split_rows(compute, split)
         loss_tot = torch.zeros(M, dtype=torch.float32, device=self.device)
         corr_tot = torch.zeros(M, dtype=torch.float32, device=self.device)
         g = max(1, min(nb, max_images // max(B * M, 1)))
@@ -568,7 +577,7 @@ class CohortTrainer:
                 x = _repeat_leading(x, M)
                 y = y.repeat(M, 1)
                 c = c.repeat(M)
-            params = BoundParams(self.layout, compute, None, K=M * (b1 - b0))
+            params = BoundParams(self.layout, compute, None, K=M * (b1 - b0), split=split)
             ctx = RunCtx(params, c, training=False)
             logits = self.model.forward(x, ctx)
             loss, correct = Fn.cross_entropy(logits, y, c)

@@ -323,10 +323,13 @@ class _BN(torch.autograd.Function):
             pre = stats.part if stats is not None else None
             planes = planes if (PLANES and x.dtype == torch.float32 and x.is_contiguous()
                                 and be.planes_fit(x[0].numel())) else 0
-            out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=True, pre_stats=pre, planes=planes)
-            y, mean, rstd, mask = out[:4]
+            # (inference passes — evaluation, GTG utilities — write no ReLU mask: no backward reads it)
+            wm = torch.is_grad_enabled()
+            out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=wm, pre_stats=pre, planes=planes)
+            y, mean, rstd = out[:3]
+            mask = out[3] if wm else None
             if planes:
-                yp = out[4]
+                yp = out[-1]
             if stats is not None:
                 stats.part = None
         # (y itself is only read by the backward when there is no ReLU mask)

@@ -258,7 +258,7 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
         _C.conv_gl_fwd(_p(x), _p(w), _p(y), _p(bias), B * H * W * C, M * Co, w_cs, b_cs, K, rep, B, H, W, C, OH, OW,
                        KH, KW, stride, pad, Co, int(relu), _s())
         return y
-    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if f32 else None, w)
     xp, x_cs, x_lo = _p(x), x.stride(0), 0
     if x_planes is not None and ws_p and planes_ok(C, Co, ldx):
         xp, x_cs, x_lo = _planes_args(x_planes, x)  # LDS-DMA GEMM on pre-split operands
@@ -303,7 +303,7 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
         return dx
     # B operand read straight from the forward weight (flip + transpose in the loader);
     # stride > 1 splits into stride² dense parity-class GEMMs (csrc/conv_nt.hip: conv_dgrad)
-    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if f32 else None, w)
     dyp, dy_cs, dy_lo = _p(dy), dy.stride(0), 0
     if dy_planes is not None and ws_p and planes_ok(Co, Ci, ld_dy):
         dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
@@ -416,7 +416,7 @@ def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_see
     y = torch.empty((K, N, Fo), dtype=x.dtype, device=x.device)
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
-    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if f32 else None, w)
     _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
                int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL,
                _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, ws_p, ws_cs, ws_plane, 0)
@@ -437,7 +437,7 @@ def linear_dgrad(dy, w, gate=None, gate_scale: float = 1.0, w_split=None):
     if gate is not None:
         assert gate.shape == dx.shape and gate.dtype == dy.dtype and gate.is_contiguous()
     # dX = dY W: B[n=fi][k=fo] = W[fo][fi] is k-major in W's own layout
-    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if (f32 and rep == 1) else None, w)
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split if f32 else None, w)
     _C.conv_nt(_p(dy), _p(w), _p(dx), NULL, N * Fo, N * Fi, w_cs, 0, 1, N, 1, Fo, N, 1, 1, 1,
                1, 0, 1, N, Fi, Fo, rep, 0, K, 1, nt_f32_variant if f32 else nt_variant, NULL, _p(gate), f32, _s(), 0, 0,
                NULL, NULL, NULL, 0.0, float(gate_scale), ws_p, ws_cs, ws_plane, 0)
