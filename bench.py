@@ -350,7 +350,16 @@ def workload_config(args, rounds: int) -> dict:
            "worker_number": 32, "epoch": args.epoch, "batch_size": 64, "optimizer_name": "SGD", "learning_rate": 0.1,
            "learning_rate_scheduler_name": "CosineAnnealingLR",
            "dataset_sampling": "random_label_iid", "dataset_sampling_kwargs": {"sampled_class_number": 5}}
-    return {"config": {**cfg, **common}, "metric": "FL rounds/sec (GTG-Shapley, 32 clients, ResNet-18, CIFAR-10-shaped)",
+    def gtg_extra(sess, s_per_round):
+        sv = getattr(sess.server.algorithm, "sv_algorithm", None)
+        if sv is None:
+            return {}
+        ev = sv.evaluations_per_round.get(max(sv.evaluations_per_round, default=0), 0)
+        return {"subset_evaluations_last_round": ev, "gtg_iterations_last_round": sv.iterations_last,
+                "subset_evaluations_per_s": ev / s_per_round, "utility_images_per_evaluation": sess.dc.spec.n_test}
+
+    return {"config": {**cfg, **common}, "extra": gtg_extra,
+            "metric": "FL rounds/sec (GTG-Shapley, 32 clients, ResNet-18, CIFAR-10-shaped)",
             "data": "synthetic (CIFAR-10-shaped, full 10k test split as the utility set, random_label_iid non-IID "
                     "shards, random-init weights)",
             "samples_per_round": shard_samples}

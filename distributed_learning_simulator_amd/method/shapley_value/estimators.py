@@ -42,6 +42,8 @@ class _Base:
         self._batch_fn: Callable | None = None
         self.kwargs = kwargs
         self.evaluations = 0
+        self.evaluations_per_round: dict[int, int] = {}  # round -> utilities evaluated (cache misses)
+        self.iterations_last = 0
 
     def set_metric_function(self, fn: Callable) -> None:
         self._batch_fn = lambda subsets: [fn(s) for s in subsets]
@@ -143,9 +145,12 @@ class GTGShapleyValue(_Base):
         players = self.players
         n = len(players)
         v0 = self.last_round_metric
+        e0 = self.evaluations
         vN = self.values([frozenset(players)])[0]
         if abs(vN - v0) < self.round_trunc_threshold:
             get_logger().info("GTG: between-round truncation (|v(N)-v0| = %.5f)", abs(vN - v0))
+            self.evaluations_per_round[round_number] = self.evaluations - e0
+            self.iterations_last = 0
             self._finish({p: 0.0 for p in players})
             return
         rng = random.Random(self.seed * 1_000_003 + round_number)
@@ -186,6 +191,8 @@ class GTGShapleyValue(_Base):
                     break
                 prev_means = means
         get_logger().info("GTG round %s: %d iterations, %d subset evaluations", round_number, it, self.evaluations)
+        self.evaluations_per_round[round_number] = self.evaluations - e0
+        self.iterations_last = it
         self._finish(means)
 
 
