@@ -42,19 +42,51 @@ def _headers() -> list[str]:
     return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
 
 
-def _needs(obj: str, src: str) -> bool:
+def _unit_hash(src: str, extra: list[str]) -> str:
+    """Content hash of one translation unit's inputs: its source, every csrc/ header, the flags."""
+    h = hashlib.sha256()
+    for d in [src] + sorted(_headers()):
+        h.update(d.encode() + b"\0")
+        with open(d, "rb") as fh:
+            h.update(fh.read())
+    h.update(repr((COMMON_FLAGS, extra, ARCH)).encode())
+    return h.hexdigest()[:20]
+
+
+def _needs(obj: str, src: str, extra: list[str] | None = None) -> bool:
+    """An object is reused only if its sidecar records the CONTENT hash of the inputs it was
+    compiled from (mtimes are not trusted: an edit during a concurrent build, or a checkout,
+    can leave an object newer than a source it was not compiled from)."""
     if not os.path.exists(obj):
         return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(d) > t for d in [src] + _headers())
+    if extra is None:  # (host-check build: mtime rule)
+        t = os.path.getmtime(obj)
+        return any(os.path.getmtime(d) > t for d in [src] + _headers())
+    try:
+        with open(obj + ".srchash") as fh:
+            return fh.read().strip() != _unit_hash(src, extra)
+    except OSError:
+        return True
 
 
-def _compile(src: str, obj: str, extra: list[str]) -> tuple[str, str]:
-    cmd = [HIPCC, *COMMON_FLAGS, *extra, "-c", src, "-o", obj]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    return src, r.stderr
+def _compile(src: str, obj: str, extra: list[str], record: bool = False) -> tuple[str, str]:
+    """Compile to a temporary object, then move it in place; with `record`, the inputs' content
+    hash (taken before and after the compile, which must agree) goes to the sidecar."""
+    while True:
+        before = _unit_hash(src, extra) if record else ""
+        tmp = f"{obj}.{os.getpid()}.tmp.o"
+        cmd = [HIPCC, *COMMON_FLAGS, *extra, "-c", src, "-o", tmp]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if record and _unit_hash(src, extra) != before:
+            os.remove(tmp)  # an input changed while compiling: compile again
+            continue
+        os.replace(tmp, obj)
+        if record:
+            with open(obj + ".srchash", "w") as fh:
+                fh.write(before + "\n")
+        return src, r.stderr
 
 
 STAMP = TARGET + ".srchash"  # content hash of the sources the in-tree .so was linked from
@@ -93,11 +125,23 @@ def wait_current(timeout: float = 1800.0) -> None:
 
 
 def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
-    import pybind11
-
     if not force and is_current():
         return TARGET  # up to date (object files need not be present, e.g. on a GPU box snapshot)
     os.makedirs(BUILD, exist_ok=True)
+    import fcntl
+
+    # one build at a time per tree (concurrent builders — a test, a second shell — serialise;
+    # the one that waited finds the tree current and returns)
+    with open(os.path.join(BUILD, ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and is_current():
+            return TARGET
+        return _build_locked(force, jobs, verbose)
+
+
+def _build_locked(force: bool, jobs: int, verbose: bool) -> str:
+    import pybind11
+
     digest = source_hash()
     py_inc = sysconfig.get_paths()["include"]
     units = []
@@ -109,11 +153,11 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
             if f.endswith(".cpp"):
                 extra += [f"-I{pybind11.get_include()}", f"-I{py_inc}", "-x", "hip"]
             units.append((src, obj, extra))
-    todo = [u for u in units if force or _needs(u[1], u[0])]
+    todo = [u for u in units if force or _needs(u[1], u[0], u[2])]
     jobs = jobs or min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 8) or 1
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            for src, err in ex.map(lambda u: _compile(*u), todo):
+            for src, err in ex.map(lambda u: _compile(*u, record=True), todo):
                 if verbose:
                     print("compiled", os.path.basename(src), file=sys.stderr)
                 if err.strip() and verbose:
@@ -133,6 +177,8 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, TARGET)
+    if source_hash() != digest:  # a source changed during the build: rebuild what it touched
+        return _build_locked(False, jobs, verbose)
     with open(STAMP + ".tmp", "w") as fh:
         fh.write(digest + "\n")
     os.replace(STAMP + ".tmp", STAMP)  # (written last: waiters see it only after the .so is in place)

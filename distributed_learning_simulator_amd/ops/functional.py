@@ -323,8 +323,9 @@ class _BN(torch.autograd.Function):
             pre = stats.part if stats is not None else None
             planes = planes if (PLANES and x.dtype == torch.float32 and x.is_contiguous()
                                 and be.planes_fit(x[0].numel())) else 0
-            # (inference passes — evaluation, GTG utilities — write no ReLU mask: no backward reads it)
-            wm = torch.is_grad_enabled()
+            # (inference passes — evaluation, GTG utilities — write no ReLU mask: no backward reads
+            # it. Autograd is off inside Function.forward, so ask which inputs need a gradient)
+            wm = any(ctx.needs_input_grad)
             out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=wm, pre_stats=pre, planes=planes)
             y, mean, rstd = out[:3]
             mask = out[3] if wm else None
