@@ -67,6 +67,8 @@ case "$mode" in
     # into gpurun_out/pmc_summary.csv by scripts/pmc_summary.py; the raw per-dispatch CSVs are removed
     rm -rf gpurun_out/pmcA gpurun_out/pmcB
     timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc_list.txt 2>&1 || true
+    # (HIP-graph replay under --pmc segfaults in CUDAGraph::replay: counters are taken on eager steps)
+    export DLS_GRAPHS=0
     timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
       SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmcA -o run -- \
       python -u bench.py "$@" > gpurun_out/pmcA.log 2>&1 || { tail -5 gpurun_out/pmcA.log; exit 1; }
