@@ -48,7 +48,16 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM, "wave tile");
   constexpr int HW2 = TW + 2, HH2 = TH + 2;
-  constexpr int HP = IMG * HH2 * HW2;              // halo pixels (rows of the A image)
+  // LDS row pitch of one halo image row, and the chunk-swizzle key of halo row hr:
+  //   key(hr) = ((hr >> 2) + (hr / PITCH) * KC) & 3
+  // The A fragment rows of a tap are TW-pixel runs of consecutive halo rows that jump by
+  // PITCH - TW at each image row. With the plain key ((hr >> 2) & 3) and pitch TW + 2, the 16
+  // rows one ds_read_b128 lane group reads collide on banks for TW = 16 / 8 (PMC: 33-40 % of
+  // LDS cycles were conflicts). Pitch TW + 4 with KC = 3 makes every group of every tap shift
+  // conflict-free (searched exhaustively over the 9 taps and both lane groups); TW = 32 already
+  // is with the plain key. The pad columns are never loaded (DMA offset out of window).
+  constexpr int PITCH = TW == 32 ? HW2 : TW + 4, KC = TW == 32 ? 0 : 3;
+  constexpr int HP = IMG * HH2 * PITCH;            // halo rows of the A image (pads included)
   constexpr int HI = (HP + 16 * NW - 1) / (16 * NW);  // halo DMA instructions per wave per plane
   constexpr int H_PL = HI * 16 * NW * 64;          // bytes per halo plane (64-B rows)
   constexpr int B_PL = BN * 64;                    // bytes per weight plane ([BN][32] or [32][BN])
@@ -84,16 +93,16 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   const uint32_t b_lo = (uint32_t)(p.ws_plane * 2);
 
   // ---- halo loader: instruction i of wave w fills halo rows (i·NW + w)·16 + lane/4, physical
-  // chunk lane & 3 ← logical chunk lc (row swizzle key (row >> 2) & 3 = (lane >> 4) & 3)
-  const int lc = (lane & 3) ^ ((lane >> 4) & 3);
+  // chunk lane & 3 ← logical chunk lc = (lane & 3) ^ key(row)
   int h_off[HI];
 #pragma unroll
   for (int i = 0; i < HI; ++i) {
     const int hr = (i * NW + wid) * 16 + (lane >> 2);
-    const int img = hr / (HH2 * HW2), rem = hr - img * (HH2 * HW2);
-    const int hh = rem / HW2, ww = rem - hh * HW2;
+    const int img = hr / (HH2 * PITCH), rem = hr - img * (HH2 * PITCH);
+    const int hh = rem / PITCH, ww = rem - hh * PITCH;
     const int ih = h0 - p.pad + hh, iw = ww - p.pad_w;
-    const bool ok = hr < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    const int lc = (lane & 3) ^ (((hr >> 2) + (hr / PITCH) * KC) & 3);
+    const bool ok = hr < HP && ww < HW2 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
     h_off[i] = ok ? (((b0 + img) * p.H + ih) * p.W + iw) * p.ldx + lc * 8 : -1;
   }
   // ---- weight loader (as conv_pl.hip): row-major rows (i·NW + w)·16 + lane/4; k-major k-rows
@@ -101,12 +110,13 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   constexpr int CPR = BN / 8, RPI = 64 / CPR;
   constexpr int SD = (128 / BN) > 1 ? 128 / BN : 1, SS = (BN / 32) < 4 ? BN / 32 : 4;
   const long wkhwn = (long)p.wKH * p.wKW * p.N;
+  const int wlc = (lane & 3) ^ ((lane >> 4) & 3);  // row-major weight rows: key (row >> 2) & 3
   int b_off[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     if constexpr (!BKM) {
       const int n = n0 + (i * NW + wid) * 16 + (lane >> 2);
-      b_off[i] = n < p.N ? n * p.R + lc * 8 : -1;
+      b_off[i] = n < p.N ? n * p.R + wlc * 8 : -1;
     } else {
       const int kr = (i * NW + wid) * RPI + lane / CPR;
       const int f = SS > 1 ? (kr / SD) & (SS - 1) : 0;
@@ -160,17 +170,18 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
 
   const int wm0 = (wid / WN) * (TM * 32), wn0 = (wid % WN) * (TN * 32);
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
-  // halo row of each A fragment row at tap (0, 0); tap (dh, dw) adds dh·HW2 + dw
-  int hbase[TM];
+  // halo row of each A fragment row at tap (0, 0); tap (dh, dw) adds dh·PITCH + dw
+  int hbase[TM], hkey[TM];  // (hkey: the image-row term of key(hr) at tap row 0, premultiplied)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int pix = wm0 + i * 32 + (lane & 31);
     const int img = pix / (TH * TW), rr = pix - img * (TH * TW);
     const int th = rr / TW, tw = rr - th * TW;
-    hbase[i] = img * HH2 * HW2 + th * HW2 + tw;
+    hbase[i] = img * HH2 * PITCH + th * PITCH + tw;
+    hkey[i] = (img * HH2 + th) * KC;  // = (hbase + dh·PITCH + dw) / PITCH · KC − dh·KC (tw + dw < PITCH)
   }
   const int rsw = (lane >> 2) & 3;  // row-major weight image key of fragment row (lane & 31)
-  auto compute = [&](int hb, int slot, int shift) {
+  auto compute = [&](int hb, int slot, int shift, int dh) {
     const unsigned char* Hs = smem + H_OFF + hb * 2 * H_PL;
     const unsigned char* Bs = smem + B_OFF + slot * 2 * B_PL;
 #pragma unroll
@@ -179,7 +190,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int hr = hbase[i] + shift;
-        const unsigned char* a = Hs + hr * 64 + (((ks * 2 + h) ^ ((hr >> 2) & 3)) << 4);
+        const unsigned char* a = Hs + hr * 64 + (((ks * 2 + h) ^ (((hr >> 2) + hkey[i] + dh * KC) & 3)) << 4);
         ah[i] = *reinterpret_cast<const bf16x8*>(a);
         al[i] = *reinterpret_cast<const bf16x8*>(a + H_PL);
       }
@@ -238,7 +249,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
     if constexpr (HB == 2)
       if (tap == 0) issue_halo(c + 1, (c + 1) & 1);
     const int dh = tap / 3;
-    compute(HB == 2 ? (c & 1) : 0, s % NBS, dh * HW2 + (tap - dh * 3));
+    compute(HB == 2 ? (c & 1) : 0, s % NBS, dh * PITCH + (tap - dh * 3), dh);
     if (++tap == 9) {
       tap = 0;
       ++c;

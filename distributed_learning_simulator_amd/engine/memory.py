@@ -60,9 +60,25 @@ def probe_activation_bytes(model, dc, hyper, device, compute_dtype) -> int:
             seen[t.untyped_storage().data_ptr()] = t.untyped_storage().nbytes()
         return t
 
-    with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
-        loss, _ = trainer.forward_loss(1, x, y, valid)
-    loss.sum().backward()
+    # the step as training runs it: with the weight planes live, BatchNorms also emit activation
+    # planes (kept by the convs' autograd contexts, outside saved_tensors: the allocator's peak
+    # over the step is taken as well, and the larger figure wins)
+    if trainer.buffers.split is not None:
+        from ..ops import fl
+
+        fl.split_rows(trainer.buffers.theta[:1], trainer.buffers.split[:1])
+        trainer._split_live = True
+    torch.cuda.synchronize(device)
+    base = torch.cuda.memory_allocated(device)
+    torch.cuda.reset_peak_memory_stats(device)
+    try:
+        with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+            loss, _ = trainer.forward_loss(1, x, y, valid)
+        loss.sum().backward()
+    finally:
+        trainer._split_live = False
+    torch.cuda.synchronize(device)
+    peak = torch.cuda.max_memory_allocated(device) - base
     # parameter / gradient rows are state (counted by state_bytes_per_client), not activations
     b = trainer.buffers
     state = {t.untyped_storage().data_ptr() for t in (b.theta, b.grad, b.state1, b.state2, b.shadow, b.split)
@@ -71,7 +87,7 @@ def probe_activation_bytes(model, dc, hyper, device, compute_dtype) -> int:
     saved = sum(acts)
     biggest = max(acts, default=0)
     del trainer, x, y, loss
-    return int(saved + 2 * biggest)
+    return int(max(saved + 2 * biggest, peak))
 
 
 def plan_capacity(wanted: int, layout, model, dc, hyper, device, compute_dtype,

@@ -233,7 +233,8 @@ class CohortTrainer:
         separate rows of `grad_rows` (default grad[row0:row0+K])."""
         b = self.buffers
         grad = grad_rows if grad_rows is not None else b.grad[row0 : row0 + K]
-        split = b.split[row0 : row0 + K] if (self._split_live and not shared) else None
+        # weight planes: per-client rows, or the shared row's planes read by all K clients (rep = K)
+        split = (b.split[:1] if shared else b.split[row0 : row0 + K]) if self._split_live else None
         params = BoundParams(self.layout, b.compute[:1] if shared else b.compute[row0 : row0 + K], grad, K=K,
                              split=split)
         ctx = RunCtx(params, valid, training=True, client_ids=client_ids, seed=step_seed)

@@ -91,10 +91,33 @@ class GradientWorker(AggregationWorker):
         epochs = self.local_epochs()
         S = steps_per_epoch * epochs
         stats = TrainStats(epochs, max(len(local), 1), tr.device)
-        up = down = 0
         wd = tr.hyper.weight_decay
         theta0 = b.theta[:1]
         nbytes = self._wire_bytes_per_client()
+        # DLS_SHARED_PLANES=1: the shared row's (hi, lo) weight planes feed the split-plane GEMMs
+        # of every client (rep = K; the SGD kernel keeps them current with θ). Off by default:
+        # measured on sign-SGD ResNet-50 (224², batch 128) it lost to the register-staged split
+        # kernels (29.4 s/round at 8 clients per wave vs 26.5 s), and the planes' activation
+        # memory shrinks the wave (tests/test_gpu_sessions.py covers the path)
+        split = b.split[:1] if (b.split is not None and os.environ.get("DLS_SHARED_PLANES", "0") == "1") else None
+        if split is not None:
+            fl.split_rows(theta0, split)
+        tr._split_live = split is not None
+        lr_e = [torch.full((1,), tr.hyper.lr_at_epoch(i, epochs), device=tr.device) for i in range(epochs)]
+        one = torch.ones(1, dtype=torch.bool, device=tr.device)
+        firsts = (torch.ones(1, dtype=torch.bool, device=tr.device), torch.zeros(1, dtype=torch.bool, device=tr.device))
+        e = 0
+        try:
+            self._steps(S, sched, local, cap, tr, sess, b, wd, theta0, sizes, stats, epochs, P, clients, nbytes,
+                        steps_per_epoch, on_epoch, split, lr_e, one, firsts)
+        finally:
+            tr._split_live = False
+        self.last_stats = stats
+        up = down = S * len(clients) * nbytes  # every client sends its gradient each step (M9) and receives
+        return b.theta[0].clone(), up, down    # the aggregate (M10)
+
+    def _steps(self, S, sched, local, cap, tr, sess, b, wd, theta0, sizes, stats, epochs, P, clients, nbytes,
+               steps_per_epoch, on_epoch, split, lr_e, one, firsts):
         e = 0
         for s in range(S):
             acc = self._new_accumulator(P, tr.device)
@@ -121,19 +144,14 @@ class GradientWorker(AggregationWorker):
             self._reduce(acc)
             with torch.no_grad():
                 grad = self._finalize(acc)
-                lr = torch.full((1,), tr.hyper.lr_at_epoch(e, epochs), device=tr.device)
-                one = torch.ones(1, dtype=torch.bool, device=tr.device)
-                first = torch.tensor([s == 0], device=tr.device)
-                fl.sgd_step(theta0, grad, b.state1[:1], lr, one, first, 0.0, tr.hyper.momentum,
-                            tr.hyper.dampening, tr.hyper.nesterov, b.shadow[:1] if b.shadow is not None else None)
-            up += len(clients) * nbytes  # every client sends its gradient each step (M9)
-            down += len(clients) * nbytes  # and receives the aggregate (M10)
+                # (lr / flag tensors made once per round: no host-built tensor per step)
+                fl.sgd_step(theta0, grad, b.state1[:1], lr_e[min(e, epochs - 1)], one, firsts[0 if s == 0 else 1],
+                            0.0, tr.hyper.momentum, tr.hyper.dampening, tr.hyper.nesterov,
+                            b.shadow[:1] if b.shadow is not None else None, split)
             if (s + 1) % steps_per_epoch == 0:
                 if on_epoch is not None:
                     on_epoch(e, stats)
                 e += 1
-        self.last_stats = stats
-        return b.theta[0].clone(), up, down
 
 
 class GradientServer(AggregationServer):

@@ -164,3 +164,32 @@ def test_transformer_imdb_bitwise_reproducible_and_matches_cpu(hip, tmp_path):
     c, rc = _run("fed_avg/imdb.yaml", ov, tmp_path / "c", "cpu")
     assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
     assert abs(_losses(ra)[-1] - _losses(rc)[-1]) < 1e-3
+
+
+def test_sign_sgd_resnet18_planes_shared_weights(hip, tmp_path, monkeypatch):
+    """sign-SGD on ResNet-18: every client reads the ONE shared model's weight planes (rep = K)
+    on the split-plane GEMMs. Votes are integers, so the only differences between arithmetic
+    paths are vote flips where a client's gradient sits within rounding noise of zero: the
+    planes path must disagree with the CPU fp32 oracle no more often than the plain fp32 GPU
+    path (no planes) does."""
+    from distributed_learning_simulator_amd.ops import functional as Fn
+    from distributed_learning_simulator_amd.ops import hip as H
+
+    # (5 clients: an even count makes 2-2 vote ties, which any last-bit gradient change breaks)
+    ov = {"round": 1, "epoch": 1, "worker_number": 5, "model_name": "ResNet18", "dataset_name": "CIFAR10",
+          "dataset_kwargs.scale": 0.004, "learning_rate": 0.001}
+    monkeypatch.setenv("DLS_SHARED_PLANES", "1")
+    H.planes_launches.clear()
+    a, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    assert min(H.planes_launches[k] for k in ("fwd", "dgrad", "wgrad")) > 0, H.planes_launches
+    c, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "c", "cpu")
+    monkeypatch.setattr(Fn, "PLANES", False)
+    b, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    ga, gb, gc = (s.server.global_parameter.cpu() for s in (a, b, c))
+
+    def flips(x, y):  # each step moves a weight by ±lr (0 on a tie): a flipped vote differs by ≥ lr
+        return ((x - y).abs() > 1e-6).float().mean().item()
+
+    fa, fb = flips(ga, gc), flips(gb, gc)
+    assert fa <= 2 * fb + 1e-4, (fa, fb)
+    assert fa < 1e-2, fa
