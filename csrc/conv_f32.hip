@@ -780,6 +780,8 @@ int conv_tn_f32_num_variants() { return kTnF32Variants; }
 
 void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s) {
   if (p.dy_lo != 0) {  // pre-split dY / X planes: the LDS-DMA kernels of conv_pl.hip
+    // 3x3 stride 1: the halo wgrad (conv_wgrad_halo.hip) unless a tile variant was forced
+    if (variant < 0 && conv_wgrad_halo(p, K, s)) return;
     if (!conv_tn_pl(p, K, variant, s)) {
       fprintf(stderr, "conv_tn_f32: pre-split operands in an unsupported shape (C %d, Co %d)\n", p.C, p.Co);
       abort();

@@ -418,7 +418,7 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
 
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
-                int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane, long x_lo) {
+                int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane, long x_lo, int acc_compact) {
   ConvNTParams p{};
   p.x_lo = x_lo;
   p.wsplit = wsplit;  // (fp32 kernels: pre-split weight planes, read k-major in place like w)
@@ -487,6 +487,11 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
       q.OH = Hc;
       q.OW = Wc;
       q.M = B * Hc * Wc;
+      if (acc_compact) {  // acc: the class-(0, 0) grid only, [K][B][Hc][Wc][Ci]
+        q.acc = (ph == 0 && pw == 0) ? acc : nullptr;
+        q.acc_compact = 1;
+        q.acc_cs = (long)B * Hc * Wc * Ci;
+      }
       q.out_s = stride;
       q.out_ph = ph;
       q.out_pw = pw;

@@ -32,6 +32,11 @@ struct ConvNTParams {
   bf16_t* y;        // [K][M][N]
   const bf16_t* bias;
   const bf16_t* acc;   // optional [K][rows][N] (y layout) added to the result in the epilogue
+  // acc_compact (stride-s dgrad parity class (0, 0) only): acc holds the class grid compactly —
+  // GEMM row m reads acc row m (client stride acc_cs), not the dx pixel it writes. A 1x1 stride-s
+  // downsample shortcut's input gradient lives only on that grid (ResNet blocks)
+  long acc_cs;
+  int acc_compact;
   const bf16_t* gate;  // optional, y layout: result zeroed where gate <= 0 (ReLU' of the next layer's input)
   long x_cs, y_cs, w_cs, b_cs;
   int B, H, W, C;
@@ -140,7 +145,7 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
                 int ld_dy = 0, long dy_cs = 0, const bf16_t* wsplit = nullptr, long ws_cs = 0, long ws_plane = 0,
-                long x_lo = 0);  // x_lo: dy is the hi plane of pre-split planes (ConvNTParams::x_lo)
+                long x_lo = 0, int acc_compact = 0);  // x_lo: dy is the hi plane of pre-split planes (ConvNTParams::x_lo)
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
@@ -169,6 +174,12 @@ void conv_tn_pl_set_variant(int v);
 int conv_tn_pl_splitk(int K, int Co, int R, int M, int variant);
 // dw[k][i] = Σ_s part[(s·K + k)·CoR + i] in split order (deterministic split-K fold)
 void tn_fold(const float* part, float* dw, long dw_cs, int K, int splitk, long CoR, hipStream_t s);
+// 3x3 stride-1 wgrad with LDS halo reuse on pre-split planes (conv_wgrad_halo.hip): false = the
+// shape is outside its contract (conv_tn_pl serves it)
+bool conv_wgrad_halo_supported(const ConvTNParams& p);
+bool conv_wgrad_halo(ConvTNParams p, int K, hipStream_t s);
+int conv_wgrad_halo_splitk(int Co, int C, int M);
+void conv_wgrad_halo_set_mode(int m);  // -1 shape rule, 0 never, 1 whenever supported
 int conv_tn_f32_num_variants();
 int conv_tn_f32_splitk(int K, int Co, int R, int M, int gco, int gc, int variant);
 

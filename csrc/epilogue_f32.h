@@ -13,7 +13,8 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
                                                 int client, int m0, int n0, int wm0, int wn0, int wid, int lane) {
   constexpr int SW = TN * 32 + 4;  // slab row (fp32), 16-B aligned
   float* __restrict__ y = reinterpret_cast<float*>(p.y) + (long)client * p.y_cs;
-  const float* accp = p.acc ? reinterpret_cast<const float*>(p.acc) + (long)client * p.y_cs : nullptr;
+  const float* accp =
+      p.acc ? reinterpret_cast<const float*>(p.acc) + (long)client * (p.acc_compact ? p.acc_cs : p.y_cs) : nullptr;
   const float* gatep = p.gate ? reinterpret_cast<const float*>(p.gate) + (long)client * p.y_cs : nullptr;
   const float* bias = p.bias ? reinterpret_cast<const float*>(p.bias) + (long)(client / p.rep) * p.b_cs : nullptr;
   // epilogue scale (dropout's 1/(1-p), or the dgrad gate's) and dropout mask of this client row
@@ -89,6 +90,7 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
       }
       float* dst = y + row * p.ldy + n;
       const float* src = slab + r * SW + cc;
+      const long arow = p.acc_compact ? (long)m : row;  // (compact acc: the class-grid row)
       if (vec_ok && n + 4 <= p.N) {
         float4 v = *reinterpret_cast<const float4*>(src);
         if (gatep) {
@@ -99,7 +101,7 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
           v.w = gv.w > 0.f ? v.w : 0.f;
         }
         if (accp) {
-          const float4 av = *reinterpret_cast<const float4*>(accp + row * p.ldy + n);
+          const float4 av = *reinterpret_cast<const float4*>(accp + arow * p.ldy + n);
           v.x += av.x;
           v.y += av.y;
           v.z += av.z;
@@ -110,7 +112,7 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
         for (int t2 = 0; t2 < 4 && n + t2 < p.N; ++t2) {
           float o = src[t2];
           if (gatep && !(gatep[row * p.ldy + n + t2] > 0.f)) o = 0.f;
-          if (accp) o += accp[row * p.ldy + n + t2];
+          if (accp) o += accp[arow * p.ldy + n + t2];
           dst[t2] = o;
         }
       }

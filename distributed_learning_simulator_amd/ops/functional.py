@@ -29,13 +29,19 @@ class ResidualLink:
     - identity shortcut: the block's last BN (whose backward runs first) deposits dX_shortcut;
     - downsample shortcut: the shortcut conv (`donor`) deposits its dX. Autograd normally runs
       it before the main branch reaches the first conv; if not, the first conv marks
-      `receiver_done` and the donor returns its dX to autograd as usual (same result)."""
+      `receiver_done` and the donor returns its dX to autograd as usual (same result).
+      A 1x1 stride-s donor (fp32 native) deposits only the stride grid — the only pixels its dX
+      is non-zero on — as a dense [K, B, ceil(H/s), ceil(W/s), C] tensor (`compact` = s): one
+      stride-1 GEMM instead of s² parity launches (s² − 1 of them writing zeros), and the
+      receiver's class-(0, 0) launch alone reads it (ops.hip.conv_dgrad acc_compact)."""
 
-    __slots__ = ("grad", "receiver_done")
+    __slots__ = ("grad", "receiver_done", "compact", "receiver_stride")
 
     def __init__(self):
         self.grad = None
         self.receiver_done = False
+        self.compact = 0
+        self.receiver_stride = 1  # stride of the receiving conv (set by its forward)
 
 
 # DLS_BN_EPILOGUE_STATS=0: BatchNorm computes its statistics in its own pass (A/B switch)
@@ -130,6 +136,8 @@ class _Conv(torch.autograd.Function):
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         ctx.link = link
         ctx.donor = donor
+        if link is not None:
+            link.receiver_stride = stride
         return y
 
     @staticmethod
@@ -140,8 +148,17 @@ class _Conv(torch.autograd.Function):
         dx = None
         link = ctx.link
         acc = link.grad if link is not None else None
+        acc_compact = False
         if link is not None:
+            if acc is not None and link.compact:
+                if link.compact == ctx.stride and ctx.stride > 1 and be is not ref and ctx.needs_input_grad[0]:
+                    acc_compact = True
+                else:  # (a receiver that cannot take the stride grid: expand it)
+                    full = torch.zeros(x.shape, dtype=acc.dtype, device=acc.device)
+                    full[:, :, :: link.compact, :: link.compact] = acc
+                    acc = full
             link.grad = None
+            link.compact = 0
             if acc is None:
                 link.receiver_done = True  # (a late donor hands its dX to autograd instead)
         dyp = _planes_of(dy)
@@ -149,8 +166,20 @@ class _Conv(torch.autograd.Function):
             raise RuntimeError("conv2d backward: dY planes without the input's planes")
         if dyp is None:
             _require_fp32(dy, "conv2d backward")
-        if ctx.needs_input_grad[0]:
-            if dyp is not None:
+        donor = ctx.donor
+        compact = (donor is not None and not donor.receiver_done and be is not ref and dy.dtype == torch.float32
+                   and ctx.stride > 1 and ctx.pad == 0 and w.shape[2] == 1 and w.shape[3] == 1 and acc is None
+                   and w.shape[-1] == ctx.ci and donor.receiver_stride == ctx.stride)
+        if ctx.needs_input_grad[0] and compact:
+            # 1x1 stride-s downsample shortcut: dX is non-zero only on the stride grid, where it is
+            # the stride-1 1x1 dgrad of dY — computed compactly and handed to the block's first conv
+            dx = be.conv_dgrad(dy, w, dy.shape[2:4], 1, 0, w_split=ctx.w_split,
+                               **({"dy_planes": dyp} if dyp is not None else {}))
+        elif ctx.needs_input_grad[0]:
+            if acc_compact:
+                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split,
+                                   acc_compact=True, **({"dy_planes": dyp} if dyp is not None else {}))
+            elif dyp is not None:
                 dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split,
                                    dy_planes=dyp)
             elif ctx.w_split is not None:
@@ -179,9 +208,9 @@ class _Conv(torch.autograd.Function):
                     be.bias_grad(dy, ctx.gb)
             if padded:
                 ctx.gw.copy_(gw[..., : ctx.ci])
-        donor = ctx.donor
         if donor is not None and dx is not None and not donor.receiver_done:
             donor.grad = dx  # added by the block's first conv in its dgrad epilogue
+            donor.compact = ctx.stride if compact else 0
             dx = None
         return dx, None, None, None, None, None, None, None, None, None, None, None
 

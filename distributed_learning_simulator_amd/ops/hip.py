@@ -269,15 +269,26 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
     return y
 
 
-def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None):
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None, acc_compact=False):
     """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
     residual branch of a ResNet block, so autograd never materialises the sum separately).
-    `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient)."""
+    `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient).
+    `acc_compact` (fp32, stride > 1): `acc` holds only the stride grid (pixels (s·i, s·j)) as a
+    dense [K, B, ceil(H/s), ceil(W/s), Ci] tensor — a 1x1 stride-s shortcut's input gradient —
+    added by the parity class (0, 0) launch alone."""
     K, B, OH, OW, Co = dy.shape
     Kw, Co2, KH, KW, Ci = w.shape
     H, W = int(in_hw[0]), int(in_hw[1])
     per_sample = max(OH * OW * Co, H * W * Ci) * dy.element_size()
+    if acc_compact:
+        assert stride > 1 and acc is not None and _f32(dy), "compact acc: fp32 strided dgrad only"
+        assert acc.shape == (K, B, (H + stride - 1) // stride, (W + stride - 1) // stride, Ci), acc.shape
+        assert acc.dtype == dy.dtype and acc.is_contiguous()
     if B * per_sample >= WINDOW and dy_planes is None:
+        if acc_compact:  # (chunked launches take the full-size acc)
+            full = torch.zeros((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
+            full[:, :, ::stride, ::stride] = acc
+            acc, acc_compact = full, False
         dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
         for b0, b1 in _batch_chunks(B, per_sample):
             dx[:, b0:b1] = conv_dgrad(dy[:, b0:b1], w, in_hw, stride, pad,
@@ -289,10 +300,10 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
     assert Co2 == Co
     w_cs, rep = _client_view(w, K)
     dx = torch.empty((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
-    if acc is not None:
+    if acc is not None and not acc_compact:
         # (stride > 1: every parity-class launch adds acc at the pixels it writes)
         assert acc.shape == dx.shape and acc.dtype == dy.dtype and acc.is_contiguous(), acc.shape
-    if (not f32 and ld_dy == Co and (stride == 1 or (gl_mode == 1 and acc is None))
+    if (not f32 and not acc_compact and ld_dy == Co and (stride == 1 or (gl_mode == 1 and acc is None))
             and _gl(K, B * H * W, Ci, Co, KH * KW)):
         # (strided dgrad splits into stride² short-K parity classes: conv_nt's smaller tiles win
         # there, l3a dgrad 447 vs 396 TFLOP/s). Large tiles want a k-contiguous B: one flip+transpose pass over the weight rows
@@ -309,7 +320,8 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
         dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
         planes_launches["dgrad"] += 1
     _C.conv_dgrad(dyp, _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
-                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy_cs, ws_p, ws_cs, ws_plane, dy_lo)
+                  nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy_cs, ws_p, ws_cs, ws_plane, dy_lo,
+                  int(bool(acc_compact)))
     return dx
 
 
@@ -341,6 +353,9 @@ def _tn_launch(dy, x, gw, dy_cs, x_cs, B, H, W, C, OH, OW, KH, KW, stride, pad, 
         xp, x_cs, x_lo = _planes_args(x_planes, x)
         planes_launches["wgrad"] += 1
     splitk = _C.conv_tn_splitk(K, Co, R, M, C, tv, f32, ldy, ldx, int(planes))
+    if planes and tv < 0 and KH == 3 and KW == 3 and stride == 1 and pad == 1 and W in (8, 16, 32):
+        # the halo wgrad may serve it (csrc/conv_wgrad_halo.hip): slabs for either split
+        splitk = max(splitk, _C.conv_wgrad_halo_splitk(Co, C, M))
     part = NULL
     if splitk > 1:
         if f32 and (deterministic or planes):

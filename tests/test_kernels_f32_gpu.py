@@ -92,7 +92,7 @@ def test_conv_f32_every_variant(hip, case):
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
-                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0)
+                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0, 0)
         _close(dx, dx_ref)
     for v in range(hip._C.conv_tn_f32_num_variants()):
         gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
@@ -618,3 +618,64 @@ def test_attention_padded_heads_and_dropout(hip, L, H, D, drop_p, dtype, tol):
     qc, kc, vc = (heads(t).contiguous() for t in qkv.split(D, dim=-1))
     o3, _ = hip.attn_fwd(qc, kc, vc, kv, **dr)
     _close(flat(o3), o.double(), 1e-6)
+
+
+@pytest.mark.parametrize("H,planes", [(16, True), (15, True), (8, False)])
+def test_dgrad_compact_shortcut_acc(hip, H, planes):
+    """Stride-2 dgrad adding a 1x1 stride-2 shortcut's input gradient held only on the stride grid
+    (acc_compact: read by the parity class (0, 0) launch alone) == the same dgrad with that
+    gradient expanded to full size; and the compact gradient itself == the stride-1 1x1 dgrad
+    of the shortcut's dY (its value on the grid), odd sizes included."""
+    torch.manual_seed(7)
+    K, B, Ci, Co = 2, 3, 64, 128
+    W = H
+    OH = (H + 2 - 3) // 2 + 1
+    w = _f(K, Co, 3, 3, Ci, scale=0.2)
+    wsc = _f(K, Co, 1, 1, Ci, scale=0.2)
+    dy = _f(K, B, OH, OH, Co)
+    dysc = _f(K, B, (H + 1) // 2, (W + 1) // 2, Co)
+    kw = {}
+    if planes:
+        kw = {"w_split": _wsplit(hip, w), "dy_planes": hip.split_planes(dy)}
+    comp = hip.conv_dgrad(dysc, wsc, dysc.shape[2:4], 1, 0)
+    full = hip.conv_dgrad(dysc, wsc, (H, W), 2, 0)
+    assert torch.equal(full[:, :, ::2, ::2], comp)
+    assert float(full[:, :, 1::2].abs().max()) == 0.0 and float(full[:, :, :, 1::2].abs().max()) == 0.0
+    a = hip.conv_dgrad(dy, w, (H, W), 2, 1, acc=comp, acc_compact=True, **kw)
+    b = hip.conv_dgrad(dy, w, (H, W), 2, 1, acc=full, **kw)
+    assert torch.equal(a, b)
+    _close(a, ref.conv_dgrad(_d(dy), _d(w), (H, W), 2, 1) + _d(full))
+
+
+@pytest.mark.parametrize("case", [
+    # K, B, H (= W), Ci, Co: every compiled (BMc, W) shape of the halo wgrad, split-K and not
+    (2, 2, 32, 64, 64),     # BMc 64, W 32
+    (2, 3, 16, 32, 128),    # BMc 128, W 16
+    (3, 4, 8, 64, 64),      # BMc 64, W 8
+    (2, 2, 8, 256, 256),    # BMc 128, W 8
+    (1, 64, 32, 32, 64),    # a full CIFAR batch: many split-K slabs
+])
+def test_wgrad_halo(hip, case):
+    """3x3 stride-1 weight gradient with LDS halo reuse (csrc/conv_wgrad_halo.hip): within 1e-5 of
+    the fp64 oracle, bitwise-reproducible run to run, and the default wgrad route for these shapes."""
+    K, B, H, Ci, Co = case
+    torch.manual_seed(11)
+    x = _f(K, B, H, H, Ci)
+    dy = _f(K, B, H, H, Co)
+    exp = ref.conv_wgrad(_d(dy), _d(x), (K, Co, 3, 3, Ci), 1, 1)
+    xp, dyp = hip.split_planes(x), hip.split_planes(dy)
+    try:
+        hip._C.conv_wgrad_halo_set_mode(1)
+        ga = torch.full((K, Co, 3, 3, Ci), 5.0, device=DEV)
+        hip.conv_wgrad(dy, x, ga, 1, 1, dy_planes=dyp, x_planes=xp)
+        _close(ga, exp)
+        gb = torch.full_like(ga, -5.0)
+        hip.conv_wgrad(dy, x, gb, 1, 1, dy_planes=dyp, x_planes=xp)
+        assert torch.equal(ga, gb), "halo wgrad not reproducible"
+        hip._C.conv_wgrad_halo_set_mode(0)
+        gc = torch.full_like(ga, 7.0)
+        hip.conv_wgrad(dy, x, gc, 1, 1, dy_planes=dyp, x_planes=xp)
+        _close(gc, exp)
+        assert not torch.equal(ga, gc), "the halo wgrad did not run (same bits as the implicit GEMM)"
+    finally:
+        hip._C.conv_wgrad_halo_set_mode(-1)
