@@ -61,10 +61,10 @@ struct KmSwzW {  // k-major [32][BMc] image: segment key of k-row kr (as conv_pl
   static __device__ __forceinline__ int f(int kr) { return SS > 1 ? (kr / SD) & (SS - 1) : 0; }
 };
 
-template <int BMc, int W, int NST>
-__global__ void __launch_bounds__((BMc / 32) * 3 * 64) conv_wgrad_halo_kernel(ConvTNParams p) {
+template <int BMc, int TMW, int W, int NST>
+__global__ void __launch_bounds__((BMc / (32 * TMW)) * 3 * 64) conv_wgrad_halo_kernel(ConvTNParams p) {
   using G = HaloGeo<W>;
-  constexpr int WM = BMc / 32, NW = WM * 3;
+  constexpr int WM = BMc / (32 * TMW), NW = WM * 3;
   constexpr int A_PL = 32 * BMc * 2;  // bytes of one dY plane image
   constexpr int AI = A_PL / 1024;     // 1-KiB pieces per dY plane
   constexpr int H_PL = G::HI * 1024;  // bytes of one halo plane image
@@ -161,9 +161,11 @@ __global__ void __launch_bounds__((BMc / 32) * 3 * 64) conv_wgrad_halo_kernel(Co
     }
   };
 
-  f32x16 acc[3];
+  f32x16 acc[TMW][3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) acc[j] = f32x16{};
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x16{};
 
   const int wm = wid % WM, kh = wid / WM;
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, h = lane >> 5;
@@ -173,18 +175,25 @@ __global__ void __launch_bounds__((BMc / 32) * 3 * 64) conv_wgrad_halo_kernel(Co
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kr = ks * 16 + 8 * h + q;  // pixel of the step (kr + 4: same image row, +4 halo rows)
-      const bf16_t* a0 = As + kr * BMc + ((wm * 32 + 16 * (g & 1) + 4 * pp) ^ (KmSwzW<BMc>::f(kr) << 5));
-      const bf16x8 ah = tr_frag(a0, a0 + 4 * BMc);
-      const bf16x8 al = tr_frag(a0 + A_PL / 2, a0 + A_PL / 2 + 4 * BMc);
+      bf16x8 ah[TMW], al[TMW];
+#pragma unroll
+      for (int i = 0; i < TMW; ++i) {
+        const bf16_t* a0 = As + kr * BMc + (((wm * TMW + i) * 32 + 16 * (g & 1) + 4 * pp) ^ (KmSwzW<BMc>::f(kr) << 5));
+        ah[i] = tr_frag(a0, a0 + 4 * BMc);
+        al[i] = tr_frag(a0 + A_PL / 2, a0 + A_PL / 2 + 4 * BMc);
+      }
       const int hrow = (kr / W + kh) * G::PITCH + (kr % W);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         const bf16_t* b0 = Hs + (hrow + kw) * 32 + 16 * (g & 1) + 4 * pp;
         const bf16x8 bh = tr_frag(b0, b0 + 4 * 32);
         const bf16x8 bl = tr_frag(b0 + H_PL / 2, b0 + H_PL / 2 + 4 * 32);
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[kw], 0, 0, 0);
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[kw], 0, 0, 0);
-        acc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[kw], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TMW; ++i) {
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc[i][kw], 0, 0, 0);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc[i][kw], 0, 0, 0);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc[i][kw], 0, 0, 0);
+        }
       }
     }
   };
@@ -211,23 +220,35 @@ __global__ void __launch_bounds__((BMc / 32) * 3 * 64) conv_wgrad_halo_kernel(Co
   float* __restrict__ dst = slab ? p.part + ((long)split * nclients + client) * p.Co * p.R : p.dw + (long)client * p.dw_cs;
   const int c = c0 + (lane & 31);
 #pragma unroll
-  for (int kw = 0; kw < 3; ++kw) {
-    const int r = (kh * 3 + kw) * p.C + c;
+  for (int i = 0; i < TMW; ++i)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int co = co0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-      dst[(long)co * p.R + r] = acc[kw][e];
+    for (int kw = 0; kw < 3; ++kw) {
+      const int r = (kh * 3 + kw) * p.C + c;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + (wm * TMW + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        dst[(long)co * p.R + r] = acc[i][kw][e];
+      }
     }
-  }
 }
 
-template <int BMc, int W>
+template <int BMc, int TMW, int W>
 void launch_wh(const ConvTNParams& p, int K, hipStream_t s) {
   const int grid = K * (p.Co / BMc) * (p.C / 32) * p.splitk;
-  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BMc, W, 3>), dim3(grid), dim3((BMc / 32) * 3 * 64), 0, s, p);
+  hipLaunchKernelGGL((conv_wgrad_halo_kernel<BMc, TMW, W, 3>), dim3(grid), dim3((BMc / (32 * TMW)) * 3 * 64), 0, s, p);
 }
 
-int g_wh_mode = -1;  // -1 shape rule, 0 never, 1 whenever supported (tests / A-B)
+template <int BMc, int TMW>
+void launch_wh_w(const ConvTNParams& p, int K, hipStream_t s) {
+  if (p.W == 32) launch_wh<BMc, TMW, 32>(p, K, s);
+  else if (p.W == 16) launch_wh<BMc, TMW, 16>(p, K, s);
+  else launch_wh<BMc, TMW, 8>(p, K, s);
+}
+
+// -1 shape rule (off: measured slower than the implicit GEMM at 32 co per wave — l1 / l2 / l3
+// 187 / 288 / 286 vs 221 / 316 / 346 TFLOP/s at 50 clients — LDS-read bound: 1.8 transposed
+// reads per MFMA), 0 never, 1 = 32 co per wave, 2 = 64 co per wave (tests / A-B)
+int g_wh_mode = -1;
 
 }  // namespace
 
@@ -246,7 +267,7 @@ static void wh_split(int Co, int C, int M, int bm, int& splitk, int& mps) {
 static int wh_bm(const ConvTNParams& p) { return p.Co % 128 == 0 ? 128 : 64; }
 
 bool conv_wgrad_halo_supported(const ConvTNParams& p) {
-  if (g_wh_mode == 0) return false;
+  if (g_wh_mode <= 0) return false;
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.OH != p.H || p.OW != p.W) return false;
   if (p.dy_lo == 0 || p.x_lo == 0 || p.C % 32 || p.Co % 64 || p.ldy != p.Co || p.ldx != p.C) return false;
   if (!(p.W == 8 || p.W == 16 || p.W == 32) || (p.OH * p.OW) % 32) return false;
@@ -265,14 +286,12 @@ bool conv_wgrad_halo(ConvTNParams p, int K, hipStream_t s) {
   const int bm = wh_bm(p);
   wh_split(p.Co, p.C, p.M, bm, p.splitk, p.m_per_split);
   if (p.splitk > 1 && p.part == nullptr) return false;
-  if (bm == 128) {
-    if (p.W == 32) launch_wh<128, 32>(p, K, s);
-    else if (p.W == 16) launch_wh<128, 16>(p, K, s);
-    else launch_wh<128, 8>(p, K, s);
+  if (g_wh_mode == 2) {
+    if (bm == 128) launch_wh_w<128, 2>(p, K, s);
+    else launch_wh_w<64, 2>(p, K, s);
   } else {
-    if (p.W == 32) launch_wh<64, 32>(p, K, s);
-    else if (p.W == 16) launch_wh<64, 16>(p, K, s);
-    else launch_wh<64, 8>(p, K, s);
+    if (bm == 128) launch_wh_w<128, 1>(p, K, s);
+    else launch_wh_w<64, 1>(p, K, s);
   }
   if (p.splitk > 1) tn_fold(p.part, p.dw, p.dw_cs, K, p.splitk, (long)p.Co * p.R, s);
   return true;

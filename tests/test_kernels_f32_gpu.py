@@ -665,7 +665,11 @@ def test_wgrad_halo(hip, case):
     exp = ref.conv_wgrad(_d(dy), _d(x), (K, Co, 3, 3, Ci), 1, 1)
     xp, dyp = hip.split_planes(x), hip.split_planes(dy)
     try:
-        hip._C.conv_wgrad_halo_set_mode(1)
+        hip._C.conv_wgrad_halo_set_mode(2)  # 64 output channels per wave
+        g2 = torch.full((K, Co, 3, 3, Ci), 4.0, device=DEV)
+        hip.conv_wgrad(dy, x, g2, 1, 1, dy_planes=dyp, x_planes=xp)
+        _close(g2, exp)
+        hip._C.conv_wgrad_halo_set_mode(1)  # 32 per wave
         ga = torch.full((K, Co, 3, 3, Ci), 5.0, device=DEV)
         hip.conv_wgrad(dy, x, ga, 1, 1, dy_planes=dyp, x_planes=xp)
         _close(ga, exp)
@@ -676,6 +680,11 @@ def test_wgrad_halo(hip, case):
         gc = torch.full_like(ga, 7.0)
         hip.conv_wgrad(dy, x, gc, 1, 1, dy_planes=dyp, x_planes=xp)
         _close(gc, exp)
-        assert not torch.equal(ga, gc), "the halo wgrad did not run (same bits as the implicit GEMM)"
+        # (where both kernels pick the same pixel split, they sum every element in the same order
+        # — 16 pixels per MFMA triple, splits folded in order — and agree bitwise)
+        if hip._C.conv_wgrad_halo_splitk(Co, Ci, B * H * H) == hip._C.conv_tn_splitk(K, Co, 9 * Ci, B * H * H, Ci, -1,
+                                                                                    1, Co, Ci, 1):
+            assert torch.equal(ga, gc)
+        assert torch.equal(ga, g2)  # (same split and order: the wave tiling changes nothing)
     finally:
         hip._C.conv_wgrad_halo_set_mode(-1)
