@@ -8,7 +8,8 @@
 //   row_off[k] + seg_byte_off[k][s] + (j0 / 8)·b      (j0 = element index within s)
 // A tensor's tail group writes only ceil(n·b / 8) bytes. One thread per (client, group): no two
 // threads touch the same byte. Codes:
-//   stochastic (FedPAQ, 255 levels): q = clamp(floor((x − lo) / scale + u), 0, 2^b − 1),
+//   stochastic (FedPAQ, QSGD with 255 signed levels: lo = −‖x‖, scale = ‖x‖/127, ops/quant.py):
+//                                    q = clamp(floor((x − lo) / scale + u), 0, 2^b − 2),
 //                                    u = mix32(flat index, seed_k)
 //   deterministic (NNADQ):           q = clamp(rint((x − lo) / scale), 0, 2^b − 1)
 // and x̂ = lo + q·scale (contraction disabled in the decoders: bit-identical to the CPU oracle;
@@ -37,7 +38,7 @@ __global__ void quant_pack_kernel(const float* __restrict__ x, long ld, const in
   const long j0 = e0 - seg_off[s];
   const int n = (int)min(8L, seg_numel[s] - j0);
   const float l = lo[q0], sc = scale[q0];
-  const float top = (float)((1 << b) - 1);
+  const float top = (float)((1 << b) - (stochastic ? 2 : 1));  // QSGD: codes 0..2s, s = 2^(b-1) − 1
   const float* xr = x + (long)k * ld + e0;
   unsigned long long word = 0;
   for (int e = 0; e < n; ++e) {

@@ -418,8 +418,21 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
 
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
-                int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane, long x_lo, int acc_compact) {
+                int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane, long x_lo, int acc_compact,
+                const BNBwdPartials* bnb) {
   ConvNTParams p{};
+  if (bnb) {  // (the epilogue's partial rows are the dX rows of a single stride-1 launch)
+    if (!f32 || stride != 1 || Ci % 8 != 0) {
+      fprintf(stderr, "conv_dgrad: BN-backward partials need an fp32 stride-1 dgrad with Ci %% 8 == 0\n");
+      abort();
+    }
+    p.bnb = bnb->part;
+    p.bnb_x = bnb->x;
+    p.bnb_mask = bnb->mask;
+    p.bnb_mean = bnb->mean;
+    p.bnb_rstd = bnb->rstd;
+    p.bnb_valid = bnb->valid;
+  }
   p.x_lo = x_lo;
   p.wsplit = wsplit;  // (fp32 kernels: pre-split weight planes, read k-major in place like w)
   p.ws_cs = ws_cs;

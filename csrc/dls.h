@@ -80,6 +80,27 @@ struct ConvNTParams {
   // producing BatchNorm (bn_fwd / bn_bwd planes outputs): with wsplit the GEMM moves both
   // operands HBM → LDS by LDS-DMA and spends no VALU on the split.
   long x_lo;
+  // optional BN-backward partials (fp32 stride-1 dgrad whose dX is the dY of a BatchNorm with
+  // input bnb_x [K][M][N], statistics bnb_mean / bnb_rstd [K][N] and 1-bit ReLU mask bnb_mask
+  // [K][M][N/8] or none): per 32-row group g and column n, bnb[client][g][0][n] = Σ ĝ and
+  // bnb[client][g][1][n] = Σ ĝ·x̂ over rows < bnb_valid[client] (ĝ = dX·relu', x̂ = (x − μ)·rstd)
+  // — the [K][parts][2N] layout bn_bwd(pre_part) consumes, so BN skips its reduction pass over dY
+  float* bnb;
+  const float* bnb_x;
+  const uint8_t* bnb_mask;
+  const float* bnb_mean;
+  const float* bnb_rstd;
+  const int* bnb_valid;
+};
+
+// BN-backward partial request handed to conv_dgrad (see ConvNTParams::bnb)
+struct BNBwdPartials {
+  float* part;
+  const float* x;
+  const uint8_t* mask;
+  const float* mean;
+  const float* rstd;
+  const int* valid;
 };
 
 struct ConvTNParams {
@@ -145,7 +166,8 @@ int conv_nt_default_variant(int M, int N, int R, int b_kmajor);
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
                 int ld_dy = 0, long dy_cs = 0, const bf16_t* wsplit = nullptr, long ws_cs = 0, long ws_plane = 0,
-                long x_lo = 0, int acc_compact = 0);  // x_lo: dy is the hi plane of pre-split planes (ConvNTParams::x_lo)
+                long x_lo = 0, int acc_compact = 0,  // x_lo: dy is the hi plane of pre-split planes (ConvNTParams::x_lo)
+                const BNBwdPartials* bnb = nullptr);  // (fp32, stride 1, Ci % 8 == 0)
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
@@ -201,8 +223,10 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
             float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, unsigned* counters, int f32,
             hipStream_t s, int ldx = 0,
             int acc_dx = 0, bf16_t* dxp = nullptr,
-            int dx_f32 = 1);  // dxp / dx_f32: split planes of dX (fp32, contiguous) with or without dX; relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
-                              // stride ldx, acc_dx: dx += (DenseNet block-buffer gradient)
+            int dx_f32 = 1,  // dxp / dx_f32: split planes of dX (fp32, contiguous) with or without dX; relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
+                             // stride ldx, acc_dx: dx += (DenseNet block-buffer gradient)
+            const float* pre_part = nullptr,  // [K][pre_nparts][2C] Σĝ / Σĝx̂ partials from the dgrad
+            int pre_nparts = 0);              // epilogue that produced dy (ConvNTParams::bnb): no reduction pass
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
             long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s);
 void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,

@@ -31,6 +31,22 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
   const bool vec_ok = (p.N % 4) == 0 && (p.ldy % 4) == 0 && ((uintptr_t)y & 15) == 0;
   // BN statistics rows: GEMM rows of this client's valid samples
   const int stat_rows = p.stats ? (p.stats_valid ? min(p.M, p.stats_valid[client] * p.OH * p.OW) : p.M) : 0;
+  // BN-backward partials (ConvNTParams::bnb, stride-1 dgrad: GEMM row m is dX row m). In the store
+  // loop below a lane always handles the same 4 columns (64 is a multiple of the Q = 8·TN column
+  // quads per row), so it sums ĝ and ĝ·x̂ of its rows in registers; the Q-strided lanes then
+  // combine with xor-shuffles and lanes < Q write the group's partial row
+  static_assert(TN == 1 || TN == 2 || TN == 4 || TN == 8, "column quads per row must divide the wave");
+  constexpr int Q = TN * 8;
+  const bool bnb = p.bnb != nullptr;
+  const int bnb_rows = bnb ? (p.bnb_valid ? min(p.M, p.bnb_valid[client]) : p.M) : 0;
+  float4 bmu = make_float4(0.f, 0.f, 0.f, 0.f), brs = bmu;
+  {
+    const int n = n0 + wn0 + (lane % Q) * 4;
+    if (bnb && n < p.N) {
+      bmu = *reinterpret_cast<const float4*>(p.bnb_mean + (long)client * p.N + n);
+      brs = *reinterpret_cast<const float4*>(p.bnb_rstd + (long)client * p.N + n);
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -76,6 +92,7 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
       }
     }
     __syncthreads();
+    float4 bs0 = make_float4(0.f, 0.f, 0.f, 0.f), bs1 = bs0;
     for (int qd = lane; qd < 32 * TN * 8; qd += 64) {
       const int r = qd / (TN * 8), cc = (qd % (TN * 8)) * 4;
       const int m = m0 + wm0 + i * 32 + r, n = n0 + wn0 + cc;
@@ -108,6 +125,21 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
           v.w += av.w;
         }
         *reinterpret_cast<float4*>(dst) = v;
+        if (bnb && m < bnb_rows) {  // ĝ = dX·relu', x̂ = (x − μ)·rstd of the BN whose dY this is
+          const float4 xv = *reinterpret_cast<const float4*>(p.bnb_x + (long)client * p.y_cs + row * p.ldy + n);
+          const uint32_t mb =
+              p.bnb_mask ? (p.bnb_mask[((long)client * p.M + m) * (p.N >> 3) + (n >> 3)] >> (n & 4)) : 0xFu;
+          const float g0 = (mb & 1u) ? v.x : 0.f, g1 = (mb & 2u) ? v.y : 0.f;
+          const float g2 = (mb & 4u) ? v.z : 0.f, g3 = (mb & 8u) ? v.w : 0.f;
+          bs0.x += g0;
+          bs0.y += g1;
+          bs0.z += g2;
+          bs0.w += g3;
+          bs1.x = fmaf(g0, (xv.x - bmu.x) * brs.x, bs1.x);
+          bs1.y = fmaf(g1, (xv.y - bmu.y) * brs.y, bs1.y);
+          bs1.z = fmaf(g2, (xv.z - bmu.z) * brs.z, bs1.z);
+          bs1.w = fmaf(g3, (xv.w - bmu.w) * brs.w, bs1.w);
+        }
       } else {
         for (int t2 = 0; t2 < 4 && n + t2 < p.N; ++t2) {
           float o = src[t2];
@@ -115,6 +147,25 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
           if (accp) o += accp[arow * p.ldy + n + t2];
           dst[t2] = o;
         }
+      }
+    }
+    if (bnb) {
+#pragma unroll
+      for (int off = Q; off < 64; off <<= 1) {
+        bs0.x += __shfl_xor(bs0.x, off, 64);
+        bs0.y += __shfl_xor(bs0.y, off, 64);
+        bs0.z += __shfl_xor(bs0.z, off, 64);
+        bs0.w += __shfl_xor(bs0.w, off, 64);
+        bs1.x += __shfl_xor(bs1.x, off, 64);
+        bs1.y += __shfl_xor(bs1.y, off, 64);
+        bs1.z += __shfl_xor(bs1.z, off, 64);
+        bs1.w += __shfl_xor(bs1.w, off, 64);
+      }
+      const int g0 = m0 + wm0 + i * 32, n = n0 + wn0 + lane * 4;
+      if (lane < Q && g0 < p.M && n < p.N) {
+        float* part = p.bnb + ((long)client * ((p.M + 31) / 32) + g0 / 32) * 2 * p.N;
+        *reinterpret_cast<float4*>(part + n) = bs0;
+        *reinterpret_cast<float4*>(part + p.N + n) = bs1;
       }
     }
     __syncthreads();

@@ -691,7 +691,7 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
             float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s,
-            int ldx, int acc_dx, bf16_t* dxp, int dx_f32) {
+            int ldx, int acc_dx, bf16_t* dxp, int dx_f32, const float* pre_part, int pre_nparts) {
   if (!f32 || acc_dx || (ldx != 0 && ldx != C)) {  // planes: fp32, contiguous dX only
     dxp = nullptr;
     dx_f32 = 1;
@@ -705,9 +705,25 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   if (V != 8) rmask = nullptr;
   BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1, counters};
   DISPATCH_T(f32, {
-    DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
-                                     mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
-    if (!counters)
+    if (pre_part) {  // Σĝ / Σĝx̂ from the dgrad epilogue that produced dy: coefficients only
+      if (pre_nparts > FOLD && pre_nparts <= cdiv(R, 32)) {
+        const int nfold = cdiv(pre_nparts, FOLD);
+        double* folds = reinterpret_cast<double*>(ws + bn_fold_offset(K, R, C));
+        hipLaunchKernelGGL(part_fold_kernel, dim3(nfold, K), dim3(256), 0, s, pre_part, pre_nparts, 2 * C, folds,
+                           nfold);
+        launch_coef<TT, double>(dim3(cdiv(C, 32), K), s, (const double*)folds, nfold, CP(gamma), (const TT*)nullptr,
+                                valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs,
+                                g_cs, K, R, C, 0.f, 1, 1);
+      } else {
+        launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, pre_part, pre_nparts, CP(gamma), (const TT*)nullptr,
+                               valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs,
+                               g_cs, K, R, C, 0.f, 1, 1);
+      }
+    } else {
+      DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
+                                       mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
+    }
+    if (!counters && !pre_part)
       launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, (const float*)part, (int)grid.x, CP(gamma), (const TT*)nullptr,
                              valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K,
                              R, C, 0.f, 1, 1);

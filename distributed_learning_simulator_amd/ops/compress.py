@@ -7,16 +7,17 @@ uint8 buffer per cohort:
 - client k's bytes start at `row_off[k]`;
 - tensor s of client k occupies ceil(bits·numel / 8) bytes at `seg_byte_off[k, s]`, with b-bit
   codes packed LSB-first in 8-element groups (csrc/compress.hip);
-- per sent tensor there are fp32 `lo` and `scale` (+ one uint8 bit-width for NNADQ).
+- per sent tensor there is the fp32 norm (stochastic) or fp32 `lo` and `scale` + one uint8
+  bit-width (NNADQ).
 
 Wire bytes per client are the sizes of those buffers (`QuantPayload.row_bytes`), not a formula.
 The server either decodes to dense rows or, for FedAvg-style weighted sums, dequantises inside
 the fp64 accumulation kernel (`accumulate`: no dense [K, P] materialisation).
 
 Codes:
-- stochastic (FedPAQ / fed_obd_sq, 255 levels = 8 bits):
-  q = clamp(floor((x − lo)/scale + u), 0, 255), with u the shared per-element hash uniform
-  (`fl.uniform_rows`; unbiased);
+- stochastic (FedPAQ / fed_obd_sq, QSGD with 255 signed levels = 8 bits, ops.quant): lo = −‖x‖,
+  scale = ‖x‖/127, q = clamp(floor((x − lo)/scale + u), 0, 254), with u the shared per-element
+  hash uniform (`fl.uniform_rows`; unbiased); per sent tensor only the fp32 norm travels;
 - NNADQ (FedOBD): round-to-nearest with the per-tensor adaptive bit-width of `quant.nnadq_bits`.
 
 x̂ = lo + q·scale; the CPU path below writes the identical buffer and decodes to identical bits.
@@ -66,7 +67,7 @@ class QuantPayload:
 
     def row_bytes(self) -> list[int]:
         """Per client: code bytes + the metadata tensors of the tensors it sent."""
-        per_seg = 8 + (1 if self.kind == "nnadq" else 0)  # lo, scale (+ bit-width)
+        per_seg = 9 if self.kind == "nnadq" else 4  # lo, scale, bit-width | the QSGD norm
         sent = (self.bits > 0).sum(1).cpu().tolist()
         off = self.row_off_host
         return [off[k + 1] - off[k] + per_seg * sent[k] for k in range(self.K)]
@@ -140,14 +141,12 @@ def _pack(kind: str, x: torch.Tensor, meta: LayoutMeta, bits, lo, scale, seeds) 
 
 def pack_stochastic(x: torch.Tensor, meta: LayoutMeta, seeds: list[int], seg_mask: torch.Tensor | None = None,
                     levels: int = 255) -> QuantPayload:
-    """255-level stochastic quantisation of rows x [K, P] into an 8-bit payload."""
+    """255-level QSGD stochastic quantisation of rows x [K, P] into an 8-bit payload."""
+    from .quant import qsgd_range
+
     assert levels == 255, "the stochastic payload packs 8-bit codes"
     mn, mx, _ = _segment_stats(x, meta)
-    lo = torch.where(torch.isfinite(mn), mn, torch.zeros_like(mn))
-    # tensor / tensor: true division on every device (a Python-scalar divisor becomes a
-    # reciprocal multiply on the GPU, one ulp off the CPU oracle)
-    scale = ((mx - mn) / torch.full_like(mx, float(levels))).clamp(min=1e-30)
-    scale = torch.where(torch.isfinite(scale), scale, torch.ones_like(scale))
+    lo, scale, _ = qsgd_range(mn, mx, levels)
     bits = torch.full_like(mn, 8, dtype=torch.uint8)
     if seg_mask is not None:
         bits = torch.where(seg_mask.to(bits.device), bits, torch.zeros_like(bits))
@@ -188,7 +187,8 @@ def _codes_torch(p: QuantPayload, x: torch.Tensor, seeds) -> torch.Tensor:
     K = x.shape[0]
     sid = p.meta.seg_ids.long().clamp(max=p.meta.nseg - 1)
     lo, sc = p.lo[:, sid], p.scale[:, sid]
-    top = (2 ** p.bits.long()[:, sid] - 1).float()
+    # QSGD codes stop at 2s = 2^b − 2 (255 signed levels); NNADQ uses all 2^b levels
+    top = (2 ** p.bits.long()[:, sid] - (2 if p.kind == "sq8" else 1)).float()
     r = (x.float() - lo) / sc
     if p.kind == "sq8":
         q = torch.floor(r + uniform_rows(seeds, x.shape[1], x.device))

@@ -68,6 +68,32 @@ class BNStats:
         self.dy_planes_ok = False
 
 
+# DLS_BN_BWD_PARTS=0: BatchNorm backward always runs its own reduction pass (A/B switch)
+BN_BWD_PARTS = os.environ.get("DLS_BN_BWD_PARTS", "1") != "0"
+# BN backward passes that used a dgrad's partials ("used") / ran their own pass despite a link
+# ("fallback"): for tests and reports
+bn_bwd_parts_count = {"used": 0, "fallback": 0}
+
+
+class BNBwdLink:
+    """Links a training BatchNorm's output to the stride-1 conv that consumes it: that conv's dgrad
+    epilogue writes the BN backward's partial sums Σĝ, Σĝ·x̂ (ĝ = dY·relu') while it stores dX
+    (= the BN's dY), so the BN backward skips its reduction pass over dY and x (ops.hip.conv_dgrad
+    bnb=). The BN uses them only if the dY autograd hands it is that very dgrad output, unmodified
+    (`key` = storage pointer + version): any other gradient summed in (a second consumer, a late
+    residual donor) makes it fall back to its own pass."""
+
+    __slots__ = ("x", "mask", "mean", "rstd", "valid", "part", "key")
+
+    def __init__(self, x, mask, mean, rstd, valid):
+        self.x, self.mask, self.mean, self.rstd, self.valid = x, mask, mean, rstd, valid
+        self.part = None
+        self.key = None
+
+    def args(self, part):
+        return (part, self.x, self.mask, self.mean, self.rstd, self.valid)
+
+
 # Split-plane operands (csrc/conv_pl.hip). A tensor produced together with its bf16 (hi, lo)
 # planes carries them as attribute `_dls_planes` ([K, 2, *shape[1:]], ops.hip.planes_buffer
 # layout); `_dls_planes_only` marks a tensor whose fp32 bytes ARE those planes (the producer
@@ -132,6 +158,11 @@ class _Conv(torch.autograd.Function):
         else:
             y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.w_split = w_split
+        bnb = getattr(x, "_dls_bnb", None) if BN_BWD_PARTS else None
+        if bnb is not None and not (be is not ref and donor is None and x.shape[-1] == ci
+                                    and be.bn_bwd_parts_ok(x.shape, stride, x.dtype)):
+            bnb = None
+        ctx.bnb = bnb
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         ctx.link = link
@@ -179,13 +210,21 @@ class _Conv(torch.autograd.Function):
             if acc_compact:
                 dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split,
                                    acc_compact=True, **({"dy_planes": dyp} if dyp is not None else {}))
-            elif dyp is not None:
-                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split,
-                                   dy_planes=dyp)
-            elif ctx.w_split is not None:
-                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, w_split=ctx.w_split)
             else:
-                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc)
+                kw = {}
+                bnb = ctx.bnb
+                if bnb is not None:
+                    K, B, H, W, Ci = x.shape
+                    part = torch.empty((K, be.conv_stats_parts(B * H * W), 2, Ci), dtype=torch.float32,
+                                       device=dy.device)
+                    kw["bnb"] = bnb.args(part)
+                if dyp is not None:
+                    kw["dy_planes"] = dyp
+                if ctx.w_split is not None:
+                    kw["w_split"] = ctx.w_split
+                dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, **kw)
+                if bnb is not None:
+                    bnb.part, bnb.key = part, (dx.data_ptr(), dx._version)
             if dx.shape[-1] > ctx.ci:
                 dx = dx[..., : ctx.ci]
         elif acc is not None:
@@ -346,6 +385,7 @@ class _BN(torch.autograd.Function):
         r3 = residual.reshape(K, -1, C) if residual is not None else None
         mask = None
         yp = None
+        bnb = None
         if be is ref:
             y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
         else:  # native: 1-bit ReLU mask so the backward need not re-read y
@@ -362,6 +402,10 @@ class _BN(torch.autograd.Function):
                 yp = out[-1]
             if stats is not None:
                 stats.part = None
+            if (wm and BN_BWD_PARTS and x.dtype == torch.float32 and x3.is_contiguous()
+                    and (mask is not None or not relu)):
+                vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+                bnb = BNBwdLink(x3, mask, mean, rstd, vr)
         # (y itself is only read by the backward when there is no ReLU mask)
         ctx.save_for_backward(x3, y if mask is None else None, mean, rstd, gamma)
         ctx.relu_mask = mask
@@ -369,9 +413,12 @@ class _BN(torch.autograd.Function):
         ctx.link = link
         ctx.stats = stats
         ctx.ggamma, ctx.gbeta, ctx.shape = ggamma, gbeta, x.shape
+        ctx.bnb = bnb
         yo = y.reshape(x.shape)
         if yp is not None:
             _tag_planes(yo, yp.view((K, 2) + tuple(x.shape[1:])), planes == 2)
+        if bnb is not None:
+            yo._dls_bnb = bnb
         return yo
 
     @staticmethod
@@ -389,8 +436,16 @@ class _BN(torch.autograd.Function):
             _require_fp32(dy, "batch_norm backward")
             # the producing conv reads dX as split planes: write only those
             dxm = 2 if (ctx.stats is not None and ctx.stats.dy_planes_ok and PLANES) else 0
+            # partial sums from the consuming conv's dgrad epilogue, if dy is exactly its output
+            pre = None
+            bnb = ctx.bnb
+            if bnb is not None:
+                if bnb.part is not None and bnb.key == (dy3.data_ptr(), dy3._version):
+                    pre = bnb.part
+                bn_bwd_parts_count["used" if pre is not None else "fallback"] += 1
+                bnb.part = bnb.key = None
             out = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
-                            ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask, dx_planes=dxm)
+                            ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask, dx_planes=dxm, pre_part=pre)
             dx, dpre = out[0], out[1]
             if dxm:
                 dxo = dx.reshape(ctx.shape)

@@ -269,13 +269,24 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
     return y
 
 
-def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None, acc_compact=False):
+def bn_bwd_parts_ok(dx_shape, stride: int, dtype) -> bool:
+    """A dgrad of this shape can write the BN-backward partials of its dX (conv_dgrad(bnb=)):
+    fp32, stride 1, 8-channel columns, one launch (no batch chunks)."""
+    K, B, H, W, Ci = dx_shape
+    return dtype == F32 and stride == 1 and Ci % 8 == 0 and B * H * W * Ci * 4 < WINDOW
+
+
+def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None, acc_compact=False,
+               bnb=None):
     """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
     residual branch of a ResNet block, so autograd never materialises the sum separately).
     `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient).
     `acc_compact` (fp32, stride > 1): `acc` holds only the stride grid (pixels (s·i, s·j)) as a
     dense [K, B, ceil(H/s), ceil(W/s), Ci] tensor — a 1x1 stride-s shortcut's input gradient —
-    added by the parity class (0, 0) launch alone."""
+    added by the parity class (0, 0) launch alone.
+    `bnb` (bn_bwd_parts_ok shapes): (part [K, conv_stats_parts(B·H·W), 2, Ci] fp32 out, x, mask,
+    mean, rstd, valid_rows) of the BatchNorm whose dY this dX is — the epilogue writes that BN's
+    backward partial sums Σĝ, Σĝ·x̂ (bn_bwd(pre_part=)); mask / valid_rows may be None."""
     K, B, OH, OW, Co = dy.shape
     Kw, Co2, KH, KW, Ci = w.shape
     H, W = int(in_hw[0]), int(in_hw[1])
@@ -284,7 +295,20 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
         assert stride > 1 and acc is not None and _f32(dy), "compact acc: fp32 strided dgrad only"
         assert acc.shape == (K, B, (H + stride - 1) // stride, (W + stride - 1) // stride, Ci), acc.shape
         assert acc.dtype == dy.dtype and acc.is_contiguous()
+    bnb_args = (NULL,) * 6
+    if bnb is not None:
+        part, bx, bmask, bmean, brstd, bvalid = bnb
+        assert bn_bwd_parts_ok((K, B, H, W, Ci), stride, dy.dtype) and not acc_compact
+        assert part.shape == (K, conv_stats_parts(B * H * W), 2, Ci) and part.dtype == F32 and part.is_contiguous()
+        assert bx.is_contiguous() and bx.numel() == K * B * H * W * Ci and bx.dtype == F32
+        assert bmean.shape == (K, Ci) and brstd.shape == (K, Ci) and bmean.is_contiguous() and brstd.is_contiguous()
+        if bmask is not None:
+            assert bmask.dtype == torch.uint8 and bmask.is_contiguous() and bmask.numel() == K * B * H * W * Ci // 8
+        if bvalid is not None:
+            assert bvalid.dtype == torch.int32 and bvalid.shape == (K,) and bvalid.is_contiguous()
+        bnb_args = (_p(part), _p(bx), _p(bmask), _p(bmean), _p(brstd), _p(bvalid))
     if B * per_sample >= WINDOW and dy_planes is None:
+        assert bnb is None
         if acc_compact:  # (chunked launches take the full-size acc)
             full = torch.zeros((K, B, H, W, Ci), dtype=dy.dtype, device=dy.device)
             full[:, :, ::stride, ::stride] = acc
@@ -321,7 +345,7 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
         planes_launches["dgrad"] += 1
     _C.conv_dgrad(dyp, _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
                   nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy_cs, ws_p, ws_cs, ws_plane, dy_lo,
-                  int(bool(acc_compact)))
+                  int(bool(acc_compact)), *bnb_args)
     return dx
 
 
@@ -547,11 +571,13 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
 
 
 def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None,
-           dx_planes: int = 0):
+           dx_planes: int = 0, pre_part=None):
     """`dx_out`: a channel slice of a wider gradient buffer (same strides as `x`) that dX is ADDED
     into (DenseNet block-buffer gradient); otherwise dX is returned contiguous. `dx_planes`
     (fp32, contiguous, no dx_out): 1 = also write dX's split planes, 2 = only the planes (dX is
-    their fp32-typed alias); the planes [K, 2, R, C] are then returned as a third value."""
+    their fp32-typed alias); the planes [K, 2, R, C] are then returned as a third value.
+    `pre_part`: [K, parts, 2, C] Σĝ / Σĝ·x̂ partials written by the dgrad that produced dy
+    (conv_dgrad(bnb=)) — the reduction pass over dy and x is skipped."""
     K, R, C = x.shape
     x, ldx = _pix_stride(x)
     assert x.stride(0) == R * ldx
@@ -580,9 +606,12 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     dg_cs = ggamma.stride(0) if ggamma is not None else 0
     assert dy.dtype == x.dtype == gamma.dtype
+    if pre_part is not None:
+        assert pre_part.dtype == F32 and pre_part.is_contiguous() and pre_part.shape == (K, (R + 31) // 32, 2, C)
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
               _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx,
-              int(dx_out is not None), _p(dxp), int(dx_planes != 2))
+              int(dx_out is not None), _p(dxp), int(dx_planes != 2), _p(pre_part),
+              0 if pre_part is None else pre_part.shape[1])
     if dx_planes:
         return dx, dpre, dxp
     return dx, dpre
@@ -1062,7 +1091,14 @@ def stochastic_qdq(x, seg_ids, nseg, seeds, levels):
     ld = out.stride(0)
     sd = _seeds_dev(seeds)
     _C.seg_minmax(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, _s())
-    _C.stochastic_qdq(_p(out), _p(seg), _p(mn), _p(mx), K, P, ld, nseg, _p(sd), levels, _s())
+    # QSGD code (ops.quant.qsgd_range): the kernel's affine form with range [−‖x‖, ‖x‖] and codes
+    # 0..2s (scale (2‖x‖)/(2s) = ‖x‖/s exactly)
+    from .quant import qsgd_range
+
+    lo, _, qmax = qsgd_range(mn, mx, levels)
+    lo = lo.contiguous()
+    hi = (-lo).contiguous()
+    _C.stochastic_qdq(_p(out), _p(seg), _p(lo), _p(hi), K, P, ld, nseg, _p(sd), qmax, _s())
     return out
 
 

@@ -7,9 +7,14 @@ wire size per row in bytes, so accounting follows the reference rule
 (`message.py:52-62`: Σ element_size·numel of the tensors actually sent):
 
 * stochastic quantisation (FedPAQ / fed_obd_sq; reference `StochasticQuant*Endpoint`,
-  levels=255): per tensor (min, scale) as 2×fp32 + one uint8 per element, unbiased
-  stochastic rounding E[Q(x)] = x. Wire = P + 8·n_tensors bytes ("1 B/param",
-  `analyze_log.py:263-272`).
+  `stochastic_quantization(quantization_level=255)`): QSGD form — per tensor the
+  norm ‖x‖ (max-abs), then sign(x)·ξ·‖x‖/s with ξ the unbiased stochastic rounding of
+  s·|x|/‖x‖ to an integer in [0, s], s = (255 − 1)/2 = 127: 255 signed levels, so sign and level
+  share one uint8 (code q = s + sign·ξ). Because rounding to adjacent levels with E[Q(x)] = x
+  fixes the distribution, this equals the affine code lo = −‖x‖, scale = ‖x‖/s,
+  q = floor((x − lo)/scale + u) ∈ [0, 2s] — the form the kernels evaluate. Wire = P + 4·n_tensors
+  bytes (one fp32 norm per tensor; "1 B/param", `analyze_log.py:263-272`). The norm choice
+  (max-abs rather than L2) is not pinned by any reference fixture (external package).
 * NNADQ (FedOBD; reference `NNADQ*Endpoint(weight)`): deterministic per-tensor
   quantisation with an adaptively chosen bit-width b ∈ [1, 8]: the smallest b whose
   relative RMS error estimate Δ_b/√12/rms(x) ≤ √weight (Δ_b = range/(2^b−1)). Wire =
@@ -40,24 +45,38 @@ def _seg_minmax(x: torch.Tensor, seg_ids: torch.Tensor, nseg: int):
     return mn, mx
 
 
+def qsgd_range(mn: torch.Tensor, mx: torch.Tensor, levels: int = 255):
+    """(lo, scale, max code) of the QSGD code with `levels` signed levels from per-tensor
+    min / max: ‖x‖ = max(|min|, |max|), lo = −‖x‖, scale = ‖x‖/s, codes 0..2s (s = (levels−1)/2).
+    Empty segments (min = +inf) get norm 0."""
+    s = (levels - 1) // 2
+    norm = torch.maximum(mn.abs(), mx.abs())
+    norm = torch.where(torch.isfinite(norm), norm, torch.zeros_like(norm))
+    # tensor / tensor: true division on every device (a Python-scalar divisor becomes a
+    # reciprocal multiply on the GPU, one ulp off the CPU oracle)
+    scale = (norm / torch.full_like(norm, float(s))).clamp(min=1e-30)
+    return -norm, scale, 2 * s
+
+
 def stochastic_quantize(x: torch.Tensor, seg_ids: torch.Tensor, seg_sizes: torch.Tensor, seeds: list[int],
                         levels: int = 255):
-    """Returns (dequantised x [K,P], wire_bytes [K] int). seeds: per-row (per-client) seeds."""
+    """QSGD stochastic quantisation (see module doc). Returns (dequantised x [K,P], wire_bytes
+    [K] int). seeds: per-row (per-client) seeds."""
     be = backend.get(x)
     nseg = int(seg_sizes.numel())  # + 1 trailing slot for inter-tensor padding
     if be is not ref:
         dq = be.stochastic_qdq(x, seg_ids, nseg + 1, seeds, levels)
     else:
         mn, mx = _seg_minmax(x, seg_ids, nseg + 1)
-        scale = ((mx - mn) / levels).clamp(min=1e-30)
+        lo_s, scale, qmax = qsgd_range(mn, mx, levels)
         sid = seg_ids.long()
-        lo = mn[:, sid]
+        lo = lo_s[:, sid]
         sc = scale[:, sid]
         u = uniform_rows(seeds, x.shape[1], x.device)
-        q = torch.floor((x.float() - lo) / sc + u).clamp(0, levels)
+        q = torch.floor((x.float() - lo) / sc + u).clamp(0, qmax)
         dq = lo + q * sc
     P_valid = int(seg_sizes.sum().item())
-    wire = P_valid * 1 + 8 * nseg
+    wire = P_valid * 1 + 4 * nseg
     return dq, [wire] * x.shape[0]
 
 

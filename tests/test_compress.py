@@ -34,7 +34,13 @@ def test_stochastic_payload_roundtrip_and_bytes():
     torch.testing.assert_close(p.decode(), dq_ref, rtol=0, atol=0)
     n = lay.num_params
     assert p.codes.numel() == 4 * n  # one byte per real element, padding not sent
-    assert p.row_bytes() == [n + 8 * len(lay.entries)] * 4 == wire_ref
+    assert p.row_bytes() == [n + 4 * len(lay.entries)] * 4 == wire_ref
+    # QSGD code: 255 signed levels of the per-tensor max-abs norm, unbiased
+    dq = p.decode()
+    for e in lay.entries:
+        seg = x[:, e.offset : e.offset + e.numel]
+        step = seg.abs().amax(1, keepdim=True) / 127
+        assert ((dq[:, e.offset : e.offset + e.numel] - seg).abs() <= step * 1.0001 + 1e-30).all()
 
 
 def test_nnadq_payload_roundtrip_bits_and_mask():

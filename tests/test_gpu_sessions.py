@@ -151,6 +151,26 @@ def test_resnet18_bitwise_reproducible_and_planes(hip, tmp_path, monkeypatch):
     assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
 
 
+def test_resnet18_bn_bwd_partials_from_dgrad(hip, tmp_path, monkeypatch):
+    """BN backward partial sums taken from the consuming conv's dgrad epilogue
+    (Fn.BNBwdLink): used by most of ResNet-18's BatchNorms, the run stays bitwise reproducible,
+    and it agrees with BN's own reduction pass to fp32 noise."""
+    from distributed_learning_simulator_amd.ops import functional as Fn
+
+    ov = {"round": 1, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
+          "learning_rate": 0.01}
+    Fn.bn_bwd_parts_count.update(used=0, fallback=0)
+    a, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    used, fb = Fn.bn_bwd_parts_count["used"], Fn.bn_bwd_parts_count["fallback"]
+    # per step: bn1 of all 8 blocks + the stem BN + bn2 of the 4 blocks followed by a stride-1 block
+    assert used > 0 and fb == 0, Fn.bn_bwd_parts_count
+    b, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    assert torch.equal(a.server.global_parameter, b.server.global_parameter)
+    monkeypatch.setattr(Fn, "BN_BWD_PARTS", False)
+    c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
+    assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
+
+
 def test_transformer_imdb_bitwise_reproducible_and_matches_cpu(hip, tmp_path):
     """The reference's imdb Transformer (d_model 100, 5 heads: dh 20 on the MFMA attention, with
     attention-probability dropout): two GPU runs are bitwise equal (deterministic LN / bias /
