@@ -1,0 +1,77 @@
+"""BatchNorm pass bandwidth on the ResNet-18 layer shapes, in the forms the training step runs:
+forward with epilogue statistics (coefficients + apply writing split planes and the ReLU bit mask,
+with / without residual) and backward with dgrad partials (coefficients + apply writing dX's
+planes, with / without the residual gradient). Prints one JSON line per (layer, pass): ms and
+effective TB/s over the bytes the apply pass must move.
+
+    python bench/bn_bench.py [--K 25] [--iters 20]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_learning_simulator_amd.ops import hip  # noqa: E402
+
+LAYERS = {"l1": (1024, 64), "l2": (256, 128), "l3": (64, 256), "l4": (16, 512)}  # pixels/sample, C
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters / 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=25)
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    dev = "cuda"
+    K = args.K
+    for name, (pix, C) in LAYERS.items():
+        R = args.B * pix
+        x = torch.randn(K, R, C, device=dev)
+        res = torch.randn(K, R, C, device=dev)
+        g = torch.rand(K, C, device=dev) + 0.5
+        b = torch.randn(K, C, device=dev)
+        vr = torch.full((K,), R, dtype=torch.int32, device=dev)
+        parts = (R + 31) // 32
+        pre = torch.zeros(K, parts, 2, C, device=dev)
+        pre[:, :, 1] = 1.0
+        n = K * R * C
+        for tag, r, planes in (("fwd_planes2", None, 2), ("fwd_res_planes1", res, 1)):
+            t = timeit(lambda: hip.bn_fwd(x, g, b, vr, True, r, with_mask=True, pre_stats=pre, planes=planes),
+                       args.iters)
+            nbytes = n * (4 + 4 + 1 / 8 + (4 if r is not None else 0) + (4 if planes == 1 else 0))
+            print(json.dumps({"layer": name, "pass": tag, "K": K, "ms": round(t * 1e3, 4),
+                              "TB/s": round(nbytes / t / 1e12, 3)}), flush=True)
+        y, mean, rstd, mask = hip.bn_fwd(x, g, b, vr, True, None, with_mask=True, pre_stats=pre)
+        dy = torch.randn(K, R, C, device=dev)
+        gg = torch.zeros(K, C, device=dev)
+        gb = torch.zeros(K, C, device=dev)
+        for tag, dpre in (("bwd_planes2", False), ("bwd_dpre_planes2", True)):
+            t = timeit(lambda: hip.bn_bwd(dy, x, y, mean, rstd, g, vr, True, gg, gb, dpre, relu_mask=mask,
+                                          dx_planes=2, pre_part=pre), args.iters)
+            nbytes = n * (4 + 4 + 1 / 8 + 4 + (4 if dpre else 0))
+            print(json.dumps({"layer": name, "pass": tag, "K": K, "ms": round(t * 1e3, 4),
+                              "TB/s": round(nbytes / t / 1e12, 3)}), flush=True)
+        t = timeit(lambda: hip.bn_bwd(dy, x, y, mean, rstd, g, vr, True, gg, gb, False, relu_mask=mask,
+                                      dx_planes=2), args.iters)
+        print(json.dumps({"layer": name, "pass": "bwd_own_reduce_planes2", "K": K, "ms": round(t * 1e3, 4)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
