@@ -422,12 +422,14 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
                 const BNBwdPartials* bnb) {
   ConvNTParams p{};
   if (bnb) {  // (the epilogue's partial rows are the dX rows of a single stride-1 launch)
-    if (!f32 || stride != 1 || Ci % 8 != 0) {
-      fprintf(stderr, "conv_dgrad: BN-backward partials need an fp32 stride-1 dgrad with Ci %% 8 == 0\n");
+    if (!f32 || stride != 1 || Ci % 4 != 0 || (bnb->mask && Ci % 8 != 0) || (bnb->xld && bnb->xld % 4 != 0)) {
+      fprintf(stderr, "conv_dgrad: BN-backward partials need an fp32 stride-1 dgrad with Ci %% 4 == 0\n");
       abort();
     }
     p.bnb = bnb->part;
     p.bnb_x = bnb->x;
+    p.bnb_xld = bnb->xld ? bnb->xld : Ci;
+    p.bnb_y = bnb->y;
     p.bnb_mask = bnb->mask;
     p.bnb_mean = bnb->mean;
     p.bnb_rstd = bnb->rstd;

@@ -30,6 +30,7 @@
 #include "gemm_common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -289,10 +290,20 @@ bool conv_nt_pl_supported(const ConvNTParams& p) {
 // 256x64 tile (l1 fwd / dgrad 253 / 238 TFLOP/s vs 168 / 165 for 128x128); N >= 512 the 256x256
 // tile (l4 354 / 297 vs 333 / 278); otherwise 128x128 at 2 blocks per CU (l3 331 / 291 vs 309 /
 // 249 for 256x128)
+// Small cohorts (a rank's share of a multi-GPU round: 100 clients / 8 ranks / 2 streams ≈ 6 per
+// launch) leave the 256x256 grid far below the 256 CUs: DLS_PL_MIN_WG = the grid below which
+// N >= 512 falls back to 128x128 (default 0: off)
+static int pl_min_wg() {
+  static const int v = [] {
+    const char* e = getenv("DLS_PL_MIN_WG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
-  (void)K;
   if (p.N <= 64) return 2;
-  if (p.N >= 512) return 3;
+  if (p.N >= 512) return (long)K * cdiv(p.M, 256) * cdiv(p.N, 256) < pl_min_wg() ? 1 : 3;
   return 1;
 }
 
@@ -576,7 +587,10 @@ __global__ void __launch_bounds__(256) tn_fold_kernel(const float* __restrict__ 
 struct TnPlTile {
   int bm, bn;
 };
-constexpr TnPlTile kTnPlTiles[] = {{128, 128}, {64, 128}, {128, 128}, {64, 128}, {256, 128}, {128, 256}};
+// 0-5: 64x64 wave tiles; 6-9: 128x64 / 64x128 wave tiles (half the LDS fragment reads per MFMA:
+// the hi / lo planes double the operand traffic of a plain bf16 tile)
+constexpr TnPlTile kTnPlTiles[] = {{128, 128}, {64, 128}, {128, 128}, {64, 128}, {256, 128},
+                                   {128, 256}, {256, 128}, {128, 256}, {128, 128}, {64, 256}};
 constexpr int kTnPlVariants = sizeof(kTnPlTiles) / sizeof(kTnPlTiles[0]);
 
 int tn_pl_default_variant(int K, int Co, int R) {
@@ -588,11 +602,20 @@ int tn_pl_default_variant(int K, int Co, int R) {
 // split-K factor from PER-CLIENT quantities only (as if KREF clients shared the launch): a
 // client's weight gradient — summation order included — is then the same whatever cohort size,
 // stream or rank trains it (1-rank ≡ N-rank, bitwise)
-constexpr int KREF = 32;
+// (DLS_TN_KREF overrides KREF: a smaller reference splits narrow layers further, which fills the
+// chip at small per-rank cohorts)
+static int tn_kref() {
+  static const int v = [] {
+    const char* e = getenv("DLS_TN_KREF");
+    const int k = e ? atoi(e) : 0;
+    return k > 0 ? k : 32;
+  }();
+  return v;
+}
 void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
   (void)K;
   const TnPlTile t = kTnPlTiles[variant];
-  const long tiles = (long)KREF * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  const long tiles = (long)tn_kref() * cdiv(Co, t.bm) * cdiv(R, t.bn);
   splitk = 1;
   const int target = 512;  // ≥ 2 blocks per CU
   if (tiles < target) {
@@ -649,6 +672,10 @@ bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s) {
     case 3: hipLaunchKernelGGL((conv_tn_pl_kernel<64, 128, 2, 2, 3, true>), dim3(grid), dim3(256), 0, s, p); break;
     case 4: hipLaunchKernelGGL((conv_tn_pl_kernel<256, 128, 4, 2, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
     case 5: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 256, 2, 4, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
+    case 6: hipLaunchKernelGGL((conv_tn_pl_kernel<256, 128, 2, 2, 2, false>), dim3(grid), dim3(256), 0, s, p); break;
+    case 7: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 256, 2, 2, 2, false>), dim3(grid), dim3(256), 0, s, p); break;
+    case 8: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 128, 1, 2, 2, false>), dim3(grid), dim3(128), 0, s, p); break;
+    case 9: hipLaunchKernelGGL((conv_tn_pl_kernel<64, 256, 1, 2, 2, false>), dim3(grid), dim3(128), 0, s, p); break;
     default: return false;
   }
   if (p.splitk > 1) tn_fold(p.part, p.dw, p.dw_cs, K, p.splitk, (long)p.Co * p.R, s);

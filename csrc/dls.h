@@ -81,12 +81,16 @@ struct ConvNTParams {
   // operands HBM → LDS by LDS-DMA and spends no VALU on the split.
   long x_lo;
   // optional BN-backward partials (fp32 stride-1 dgrad whose dX is the dY of a BatchNorm with
-  // input bnb_x [K][M][N], statistics bnb_mean / bnb_rstd [K][N] and 1-bit ReLU mask bnb_mask
-  // [K][M][N/8] or none): per 32-row group g and column n, bnb[client][g][0][n] = Σ ĝ and
-  // bnb[client][g][1][n] = Σ ĝ·x̂ over rows < bnb_valid[client] (ĝ = dX·relu', x̂ = (x − μ)·rstd)
-  // — the [K][parts][2N] layout bn_bwd(pre_part) consumes, so BN skips its reduction pass over dY
+  // input bnb_x [K][M][N] at row stride bnb_xld (0 = N; a channel prefix of DenseNet's block
+  // buffer), statistics bnb_mean / bnb_rstd [K][N] and ReLU gate: the 1-bit mask bnb_mask
+  // [K][M][N/8], else the fp32 output bnb_y (dX layout, > 0), else none): per 32-row group g and
+  // column n, bnb[client][g][0][n] = Σ ĝ and bnb[client][g][1][n] = Σ ĝ·x̂ over rows <
+  // bnb_valid[client] (ĝ = dX·relu', x̂ = (x − μ)·rstd) — the [K][parts][2N] layout
+  // bn_bwd(pre_part) consumes, so BN skips its reduction pass over dY
   float* bnb;
   const float* bnb_x;
+  long bnb_xld;
+  const float* bnb_y;
   const uint8_t* bnb_mask;
   const float* bnb_mean;
   const float* bnb_rstd;
@@ -97,6 +101,8 @@ struct ConvNTParams {
 struct BNBwdPartials {
   float* part;
   const float* x;
+  long xld;
+  const float* y;
   const uint8_t* mask;
   const float* mean;
   const float* rstd;
@@ -167,7 +173,7 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
                 int ld_dy = 0, long dy_cs = 0, const bf16_t* wsplit = nullptr, long ws_cs = 0, long ws_plane = 0,
                 long x_lo = 0, int acc_compact = 0,  // x_lo: dy is the hi plane of pre-split planes (ConvNTParams::x_lo)
-                const BNBwdPartials* bnb = nullptr);  // (fp32, stride 1, Ci % 8 == 0)
+                const BNBwdPartials* bnb = nullptr);  // (fp32, stride 1, Ci % 4 == 0)
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)

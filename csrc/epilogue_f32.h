@@ -126,9 +126,15 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
         }
         *reinterpret_cast<float4*>(dst) = v;
         if (bnb && m < bnb_rows) {  // ĝ = dX·relu', x̂ = (x − μ)·rstd of the BN whose dY this is
-          const float4 xv = *reinterpret_cast<const float4*>(p.bnb_x + (long)client * p.y_cs + row * p.ldy + n);
-          const uint32_t mb =
-              p.bnb_mask ? (p.bnb_mask[((long)client * p.M + m) * (p.N >> 3) + (n >> 3)] >> (n & 4)) : 0xFu;
+          const float4 xv =
+              *reinterpret_cast<const float4*>(p.bnb_x + ((long)client * p.M + row) * p.bnb_xld + n);
+          uint32_t mb = 0xFu;
+          if (p.bnb_mask) {
+            mb = p.bnb_mask[((long)client * p.M + m) * (p.N >> 3) + (n >> 3)] >> (n & 4);
+          } else if (p.bnb_y) {
+            const float4 yv = *reinterpret_cast<const float4*>(p.bnb_y + (long)client * p.y_cs + row * p.ldy + n);
+            mb = (yv.x > 0.f ? 1u : 0u) | (yv.y > 0.f ? 2u : 0u) | (yv.z > 0.f ? 4u : 0u) | (yv.w > 0.f ? 8u : 0u);
+          }
           const float g0 = (mb & 1u) ? v.x : 0.f, g1 = (mb & 2u) ? v.y : 0.f;
           const float g2 = (mb & 4u) ? v.z : 0.f, g3 = (mb & 8u) ? v.w : 0.f;
           bs0.x += g0;

@@ -70,9 +70,9 @@ class BNStats:
 
 # DLS_BN_BWD_PARTS=0: BatchNorm backward always runs its own reduction pass (A/B switch)
 BN_BWD_PARTS = os.environ.get("DLS_BN_BWD_PARTS", "1") != "0"
-# BN backward passes that used a dgrad's partials ("used") / ran their own pass despite a link
-# ("fallback"): for tests and reports
-bn_bwd_parts_count = {"used": 0, "fallback": 0}
+# BN backward passes that used a dgrad's partials ("used"), whose consumer wrote none (a strided
+# or absent conv: "none"), or whose dY was not that dgrad's output ("fallback"): tests, reports
+bn_bwd_parts_count = {"used": 0, "none": 0, "fallback": 0}
 
 
 class BNBwdLink:
@@ -91,7 +91,7 @@ class BNBwdLink:
         self.key = None
 
     def args(self, part):
-        return (part, self.x, self.mask, self.mean, self.rstd, self.valid)
+        return (part, self.x, self.mask, self.mean, self.rstd, self.valid, None)
 
 
 # Split-plane operands (csrc/conv_pl.hip). A tensor produced together with its bf16 (hi, lo)
@@ -442,7 +442,7 @@ class _BN(torch.autograd.Function):
             if bnb is not None:
                 if bnb.part is not None and bnb.key == (dy3.data_ptr(), dy3._version):
                     pre = bnb.part
-                bn_bwd_parts_count["used" if pre is not None else "fallback"] += 1
+                bn_bwd_parts_count["used" if pre is not None else "none" if bnb.part is None else "fallback"] += 1
                 bnb.part = bnb.key = None
             out = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
                             ctx.ggamma, ctx.gbeta, ctx.has_res, relu_mask=ctx.relu_mask, dx_planes=dxm, pre_part=pre)
@@ -793,6 +793,7 @@ class _DenseBlock(torch.autograd.Function):
         K, B, H, W, Ct = F.shape
         g, c0 = ctx.growth, ctx.c0
         dF = dF_out.contiguous().clone() if native else dF_out.float().clone()
+        vr32 = ctx.valid_rows.to(torch.int32).contiguous() if ctx.valid_rows is not None else None
         for i in range(len(ctx.layers) - 1, -1, -1):
             lp = ctx.layers[i]
             y, mean, rstd, mask = ctx.saved[i]
@@ -803,9 +804,17 @@ class _DenseBlock(torch.autograd.Function):
             if native:
                 if lp.gw is not None:
                     be.conv_wgrad(d_out, yv, lp.gw, 1, 1)
-                dy = be.conv_dgrad(d_out, lp.w, (H, W), 1, 1)
+                # the dgrad's epilogue writes this BN's backward partial sums (Fn.BNBwdLink): x is
+                # the block buffer's channel prefix, the ReLU gate the bit mask or y
+                part = None
+                kw = {}
+                if BN_BWD_PARTS and F.dtype == torch.float32 and be.bn_bwd_parts_ok((K, B, H, W, ci), 1, F.dtype):
+                    part = torch.empty((K, be.conv_stats_parts(B * H * W), 2, ci), dtype=torch.float32,
+                                       device=F.device)
+                    kw["bnb"] = (part, xi, mask, mean, rstd, vr32, y if mask is None else None)
+                dy = be.conv_dgrad(d_out, lp.w, (H, W), 1, 1, **kw)
                 be.bn_bwd(dy.view(K, -1, ci), xi, y, mean, rstd, lp.gamma, ctx.valid_rows, True, lp.ggamma, lp.gbeta,
-                          False, relu_mask=mask, dx_out=dF[..., :ci].reshape(K, -1, ci))
+                          False, relu_mask=mask, dx_out=dF[..., :ci].reshape(K, -1, ci), pre_part=part)
             else:
                 d_out = d_out.contiguous()
                 if lp.gw is not None:

@@ -271,9 +271,9 @@ def conv_fwd(x, w, stride: int, pad: int, bias=None, relu=False, out=None, stats
 
 def bn_bwd_parts_ok(dx_shape, stride: int, dtype) -> bool:
     """A dgrad of this shape can write the BN-backward partials of its dX (conv_dgrad(bnb=)):
-    fp32, stride 1, 8-channel columns, one launch (no batch chunks)."""
+    fp32, stride 1, 4-channel columns, one launch (no batch chunks)."""
     K, B, H, W, Ci = dx_shape
-    return dtype == F32 and stride == 1 and Ci % 8 == 0 and B * H * W * Ci * 4 < WINDOW
+    return dtype == F32 and stride == 1 and Ci % 4 == 0 and B * H * W * Ci * 4 < WINDOW
 
 
 def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None, acc_compact=False,
@@ -285,8 +285,10 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
     dense [K, B, ceil(H/s), ceil(W/s), Ci] tensor — a 1x1 stride-s shortcut's input gradient —
     added by the parity class (0, 0) launch alone.
     `bnb` (bn_bwd_parts_ok shapes): (part [K, conv_stats_parts(B·H·W), 2, Ci] fp32 out, x, mask,
-    mean, rstd, valid_rows) of the BatchNorm whose dY this dX is — the epilogue writes that BN's
-    backward partial sums Σĝ, Σĝ·x̂ (bn_bwd(pre_part=)); mask / valid_rows may be None."""
+    mean, rstd, valid_rows, y) of the BatchNorm whose dY this dX is — the epilogue writes that BN's
+    backward partial sums Σĝ, Σĝ·x̂ (bn_bwd(pre_part=)). x [K, R, Ci] may be a channel prefix of a
+    wider buffer (row stride ld); the ReLU gate is the bit mask, else y > 0 (y contiguous), else
+    none; mask / valid_rows / y may be None."""
     K, B, OH, OW, Co = dy.shape
     Kw, Co2, KH, KW, Ci = w.shape
     H, W = int(in_hw[0]), int(in_hw[1])
@@ -295,18 +297,22 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
         assert stride > 1 and acc is not None and _f32(dy), "compact acc: fp32 strided dgrad only"
         assert acc.shape == (K, B, (H + stride - 1) // stride, (W + stride - 1) // stride, Ci), acc.shape
         assert acc.dtype == dy.dtype and acc.is_contiguous()
-    bnb_args = (NULL,) * 6
+    bnb_args = (NULL, NULL, 0, NULL, NULL, NULL, NULL, NULL)
     if bnb is not None:
-        part, bx, bmask, bmean, brstd, bvalid = bnb
+        part, bx, bmask, bmean, brstd, bvalid, by = bnb
+        R = B * H * W
         assert bn_bwd_parts_ok((K, B, H, W, Ci), stride, dy.dtype) and not acc_compact
-        assert part.shape == (K, conv_stats_parts(B * H * W), 2, Ci) and part.dtype == F32 and part.is_contiguous()
-        assert bx.is_contiguous() and bx.numel() == K * B * H * W * Ci and bx.dtype == F32
+        assert part.shape == (K, conv_stats_parts(R), 2, Ci) and part.dtype == F32 and part.is_contiguous()
+        bx, bxld = _pix_stride(bx.reshape(K, R, -1) if bx.is_contiguous() else bx)
+        assert bx.dtype == F32 and bx.shape[-1] == Ci and bx.stride(0) == R * bxld and bxld % 4 == 0
         assert bmean.shape == (K, Ci) and brstd.shape == (K, Ci) and bmean.is_contiguous() and brstd.is_contiguous()
         if bmask is not None:
-            assert bmask.dtype == torch.uint8 and bmask.is_contiguous() and bmask.numel() == K * B * H * W * Ci // 8
+            assert bmask.dtype == torch.uint8 and bmask.is_contiguous() and bmask.numel() == K * R * Ci // 8
+        if by is not None:
+            assert by.dtype == F32 and by.is_contiguous() and by.numel() == K * R * Ci
         if bvalid is not None:
             assert bvalid.dtype == torch.int32 and bvalid.shape == (K,) and bvalid.is_contiguous()
-        bnb_args = (_p(part), _p(bx), _p(bmask), _p(bmean), _p(brstd), _p(bvalid))
+        bnb_args = (_p(part), _p(bx), bxld, _p(by), _p(bmask), _p(bmean), _p(brstd), _p(bvalid))
     if B * per_sample >= WINDOW and dy_planes is None:
         assert bnb is None
         if acc_compact:  # (chunked launches take the full-size acc)

@@ -159,11 +159,13 @@ def test_resnet18_bn_bwd_partials_from_dgrad(hip, tmp_path, monkeypatch):
 
     ov = {"round": 1, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
           "learning_rate": 0.01}
-    Fn.bn_bwd_parts_count.update(used=0, fallback=0)
+    Fn.bn_bwd_parts_count.update(used=0, none=0, fallback=0)
     a, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
-    used, fb = Fn.bn_bwd_parts_count["used"], Fn.bn_bwd_parts_count["fallback"]
-    # per step: bn1 of all 8 blocks + the stem BN + bn2 of the 4 blocks followed by a stride-1 block
-    assert used > 0 and fb == 0, Fn.bn_bwd_parts_count
+    c = Fn.bn_bwd_parts_count
+    # per step 13 BNs take their partials from a stride-1 dgrad (the stem BN, bn1 of all 8 blocks,
+    # bn2 of the 4 blocks followed by a stride-1 block); 7 have no such consumer (3 downsample
+    # shortcut BNs, bn2 before a stride-2 block or the pooling head)
+    assert c["used"] > 0 and c["fallback"] == 0 and c["used"] * 7 == c["none"] * 13, c
     b, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
     assert torch.equal(a.server.global_parameter, b.server.global_parameter)
     monkeypatch.setattr(Fn, "BN_BWD_PARTS", False)

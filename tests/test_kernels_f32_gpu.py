@@ -92,7 +92,7 @@ def test_conv_f32_every_variant(hip, case):
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
-                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
         _close(dx, dx_ref)
     for v in range(hip._C.conv_tn_f32_num_variants()):
         gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
@@ -698,37 +698,46 @@ def test_wgrad_halo(hip, case):
     (2, 2, 8, 32, 48, 3, False, True, True),
     (2, 41, 8, 64, 64, 3, True, True, False),
     (2, 3, 8, 64, 128, 1, True, False, True),
+    # DenseNet block backward: x a channel prefix of the block buffer (Ci % 8 == 4: no bit mask,
+    # the ReLU gate is y > 0; Ci % 8 == 0: bit mask), growth-12 dY, no planes
+    (2, 3, 8, 36, 12, 3, False, True, False, 48),
+    (2, 2, 8, 48, 12, 3, False, True, False, 36),
 ])
 def test_dgrad_epilogue_bn_bwd_parts(hip, case):
     """Stride-1 fp32 dgrad whose dX is a BatchNorm's dY writes that BN's backward partial sums
     (Σĝ, Σĝ·x̂ per 32 rows, ĝ = dX·relu', valid rows only) in its epilogue: dX is bitwise the same
     as without them, the partial totals match fp64 sums, and bn_bwd(pre_part=) matches bn_bwd's own
     reduction pass (dX, dγ, dβ)."""
-    K, B, H, Ci, Co, k, planes, relu, with_acc = case
+    K, B, H, Ci, Co, k, planes, relu, with_acc = case[:9]
+    wide = case[9] if len(case) > 9 else 0
     torch.manual_seed(B * 7 + Ci)
     pad = k // 2
-    xb = _f(K, B, H, H, Ci) * 1.5 + 0.3  # the BN's input (the producing conv's output)
+    R = B * H * H
+    # the BN's input (the producing conv's output), possibly a channel prefix of a wider buffer
+    xbuf = _f(K, B, H, H, Ci + wide) * 1.5 + 0.3
+    xb = xbuf[..., :Ci]
+    x3 = xb.reshape(K, R, Ci)
     g = torch.rand(K, Ci, device=DEV) + 0.5
     b = _f(K, Ci)
     valid = torch.tensor([B, max(1, B - 2), 1][:K], dtype=torch.int32, device=DEV)
     vr = (valid * H * H).to(torch.int32)
-    R = B * H * H
-    y, mean, rstd, mask = hip.bn_fwd(xb.reshape(K, R, Ci), g, b, vr, relu, None, with_mask=True)
+    y, mean, rstd, mask = hip.bn_fwd(x3, g, b, vr, relu, None, with_mask=True)
     if not relu:
         mask = None
+    ygate = y if (relu and mask is None) else None
     w = _f(K, Co, k, k, Ci, scale=0.2)
     dy = _f(K, B, H, H, Co)
     acc = _f(K, B, H, H, Ci) if with_acc else None
     kw = {"w_split": _wsplit(hip, w), "dy_planes": hip.split_planes(dy)} if planes else {}
     base = hip.conv_dgrad(dy, w, (H, H), 1, pad, acc=acc, **kw)
     part = torch.full((K, hip.conv_stats_parts(R), 2, Ci), float("nan"), device=DEV)
-    dx = hip.conv_dgrad(dy, w, (H, H), 1, pad, acc=acc, bnb=(part, xb, mask, mean, rstd, vr), **kw)
+    dx = hip.conv_dgrad(dy, w, (H, H), 1, pad, acc=acc, bnb=(part, x3, mask, mean, rstd, vr, ygate), **kw)
     assert torch.equal(dx, base)
     assert torch.isfinite(part).all()  # every partial slot written
     gd = _d(dx).reshape(K, R, Ci)
-    if mask is not None:
+    if relu:
         gd = gd * (_d(y) > 0).double()
-    xh = (_d(xb).reshape(K, R, Ci) - _d(mean)[:, None]) * _d(rstd)[:, None]
+    xh = (_d(x3) - _d(mean)[:, None]) * _d(rstd)[:, None]
     for kk in range(K):
         rows = int(vr[kk])
         _close(part[kk, :, 0].double().sum(0), gd[kk, :rows].sum(0), 1e-5)
@@ -737,8 +746,10 @@ def test_dgrad_epilogue_bn_bwd_parts(hip, case):
     for pre in (None, part):
         gg = torch.zeros(K, Ci, device=DEV)
         gb = torch.zeros(K, Ci, device=DEV)
-        o = hip.bn_bwd(dx.reshape(K, R, Ci), xb.reshape(K, R, Ci), y, mean, rstd, g, vr, relu, gg, gb, True,
-                       relu_mask=mask, pre_part=pre)
-        outs.append((o[0], o[1], gg, gb))
+        # (a strided x — DenseNet's block buffer — adds dX into a buffer of the same strides)
+        dxo = torch.zeros(K, B, H, H, Ci + wide, device=DEV)[..., :Ci].reshape(K, R, Ci) if wide else None
+        o = hip.bn_bwd(dx.reshape(K, R, Ci), x3, y, mean, rstd, g, vr, relu, gg, gb, True,
+                       relu_mask=mask, pre_part=pre, dx_out=dxo)
+        outs.append((o[0].contiguous(), o[1], gg, gb))
     for a, c in zip(outs[0], outs[1]):
         _close(c, a.double(), 1e-5)
