@@ -587,10 +587,11 @@ __global__ void __launch_bounds__(256) tn_fold_kernel(const float* __restrict__ 
 struct TnPlTile {
   int bm, bn;
 };
-// 0-5: 64x64 wave tiles; 6-9: 128x64 / 64x128 wave tiles (half the LDS fragment reads per MFMA:
-// the hi / lo planes double the operand traffic of a plain bf16 tile)
-constexpr TnPlTile kTnPlTiles[] = {{128, 128}, {64, 128}, {128, 128}, {64, 128}, {256, 128},
-                                   {128, 256}, {256, 128}, {128, 256}, {128, 128}, {64, 256}};
+// (all 64x64 wave tiles: 128x64 / 64x128 wave tiles — half the LDS fragment reads per MFMA, one
+// wave per SIMD — measured slower on every ResNet-18 layer at 50 clients: l3 243-271 vs 328,
+// l4 253-285 vs 318 TFLOP/s, profiles/r3_kernel_bench_tn_wave_tiles_K50.jsonl)
+// 6: 256x256, 8 waves of 128x64 (the NT 256x256 shape: two waves per SIMD, 128 KB)
+constexpr TnPlTile kTnPlTiles[] = {{128, 128}, {64, 128}, {128, 128}, {64, 128}, {256, 128}, {128, 256}, {256, 256}};
 constexpr int kTnPlVariants = sizeof(kTnPlTiles) / sizeof(kTnPlTiles[0]);
 
 int tn_pl_default_variant(int K, int Co, int R) {
@@ -672,10 +673,7 @@ bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s) {
     case 3: hipLaunchKernelGGL((conv_tn_pl_kernel<64, 128, 2, 2, 3, true>), dim3(grid), dim3(256), 0, s, p); break;
     case 4: hipLaunchKernelGGL((conv_tn_pl_kernel<256, 128, 4, 2, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
     case 5: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 256, 2, 4, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
-    case 6: hipLaunchKernelGGL((conv_tn_pl_kernel<256, 128, 2, 2, 2, false>), dim3(grid), dim3(256), 0, s, p); break;
-    case 7: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 256, 2, 2, 2, false>), dim3(grid), dim3(256), 0, s, p); break;
-    case 8: hipLaunchKernelGGL((conv_tn_pl_kernel<128, 128, 1, 2, 2, false>), dim3(grid), dim3(128), 0, s, p); break;
-    case 9: hipLaunchKernelGGL((conv_tn_pl_kernel<64, 256, 1, 2, 2, false>), dim3(grid), dim3(128), 0, s, p); break;
+    case 6: hipLaunchKernelGGL((conv_tn_pl_kernel<256, 256, 2, 4, 2, false>), dim3(grid), dim3(512), 0, s, p); break;
     default: return false;
   }
   if (p.splitk > 1) tn_fold(p.part, p.dw, p.dw_cs, K, p.splitk, (long)p.Co * p.R, s);

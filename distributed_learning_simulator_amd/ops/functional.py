@@ -49,6 +49,11 @@ EPILOGUE_BN_STATS = os.environ.get("DLS_BN_EPILOGUE_STATS", "1") != "0"
 # DLS_DENSE_STATS_CACHE=1: DenseNet blocks compute each channel's batch statistics once (see
 # _DenseBlock.forward)
 DENSE_STATS_CACHE = os.environ.get("DLS_DENSE_STATS_CACHE", "0") == "1"
+# DLS_DENSE_BN_PARTS=1: DenseNet block backward takes each BN's partial sums from the growth conv's
+# dgrad epilogue (off by default: the 100-client DenseNet-40 round measured 14.57 s with it vs
+# 14.36 s without — the strided x / y-gate reads in the non-plane dgrad's epilogue cost more than
+# the reduction pass they replace)
+DENSE_BN_PARTS = os.environ.get("DLS_DENSE_BN_PARTS", "0") == "1"
 
 
 class BNStats:
@@ -808,7 +813,8 @@ class _DenseBlock(torch.autograd.Function):
                 # the block buffer's channel prefix, the ReLU gate the bit mask or y
                 part = None
                 kw = {}
-                if BN_BWD_PARTS and F.dtype == torch.float32 and be.bn_bwd_parts_ok((K, B, H, W, ci), 1, F.dtype):
+                if (BN_BWD_PARTS and DENSE_BN_PARTS and F.dtype == torch.float32
+                        and be.bn_bwd_parts_ok((K, B, H, W, ci), 1, F.dtype)):
                     part = torch.empty((K, be.conv_stats_parts(B * H * W), 2, ci), dtype=torch.float32,
                                        device=F.device)
                     kw["bnb"] = (part, xi, mask, mean, rstd, vr32, y if mask is None else None)
