@@ -290,13 +290,15 @@ bool conv_nt_pl_supported(const ConvNTParams& p) {
 // 256x64 tile (l1 fwd / dgrad 253 / 238 TFLOP/s vs 168 / 165 for 128x128); N >= 512 the 256x256
 // tile (l4 354 / 297 vs 333 / 278); otherwise 128x128 at 2 blocks per CU (l3 331 / 291 vs 309 /
 // 249 for 256x128)
-// Small cohorts (a rank's share of a multi-GPU round: 100 clients / 8 ranks / 2 streams ≈ 6 per
-// launch) leave the 256x256 grid far below the 256 CUs: DLS_PL_MIN_WG = the grid below which
-// N >= 512 falls back to 128x128 (default 0: off)
+// Small cohorts (a rank's share of a multi-GPU round: 100 clients / 8 ranks / 2 streams ≈ 6-7 per
+// launch) leave the 256x256 grid far below the 256 CUs: below 256 workgroups N >= 512 takes the
+// 128x128 tile (l4 at 7 clients: fwd / dgrad 282 / 213 vs 127 / 107 TFLOP/s; at 50 clients the
+// 256x256 tile keeps 380 / 325 vs 350 / 303, profiles/r3_kernel_bench_small_cohort_kref.log).
+// DLS_PL_MIN_WG overrides the threshold (0 = always 256x256)
 static int pl_min_wg() {
   static const int v = [] {
     const char* e = getenv("DLS_PL_MIN_WG");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 256;
   }();
   return v;
 }
@@ -594,29 +596,35 @@ struct TnPlTile {
 constexpr TnPlTile kTnPlTiles[] = {{128, 128}, {64, 128}, {128, 128}, {64, 128}, {256, 128}, {128, 256}, {256, 256}};
 constexpr int kTnPlVariants = sizeof(kTnPlTiles) / sizeof(kTnPlTiles[0]);
 
+// Co >= 512 at >= 16 clients per launch: the 8-wave 256x256 tile (l4 364 vs 343 TFLOP/s at 50
+// clients; a small cohort's split-K reference — tn_kref — would split it, 246)
 int tn_pl_default_variant(int K, int Co, int R) {
-  (void)K;
   (void)R;
+  if (Co >= 512 && K >= 16) return 6;
   return Co <= 64 ? 1 : 0;
 }
 
-// split-K factor from PER-CLIENT quantities only (as if KREF clients shared the launch): a
-// client's weight gradient — summation order included — is then the same whatever cohort size,
-// stream or rank trains it (1-rank ≡ N-rank, bitwise)
-// (DLS_TN_KREF overrides KREF: a smaller reference splits narrow layers further, which fills the
-// chip at small per-rank cohorts)
-static int tn_kref() {
+// split-K factor from per-client quantities and a reference cohort KREF (as if KREF clients shared
+// the launch): a client's weight gradient — summation order included — is the same whatever
+// stream, rank or cohort size trains it, as long as the launch is in the same cohort class.
+// KREF = 32 for launches of >= 16 clients (one GPU: 50 per stream; two ranks: 25), 8 below (a rank
+// of an 8-GPU round: 6-7 per stream), where KREF 32 leaves the grid a few dozen workgroups:
+// at 7 clients l1 / l2 / l3 wgrad 223 / 308 / 324 vs 85 / 125 / 233 TFLOP/s, while at 50 clients
+// KREF 8 would cost l2 / l3 6-7 % in slab traffic (profiles/r3_kernel_bench_small_cohort_kref.log).
+// So 1-rank and 2-rank runs train bitwise alike; an 8-rank run's weight gradients differ from
+// them by summation order only. DLS_TN_KREF pins one KREF for every launch.
+static int tn_kref(int K) {
   static const int v = [] {
     const char* e = getenv("DLS_TN_KREF");
     const int k = e ? atoi(e) : 0;
-    return k > 0 ? k : 32;
+    return k > 0 ? k : 0;
   }();
-  return v;
+  if (v) return v;
+  return K >= 16 ? 32 : 8;
 }
 void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
-  (void)K;
   const TnPlTile t = kTnPlTiles[variant];
-  const long tiles = (long)tn_kref() * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  const long tiles = (long)tn_kref(K) * cdiv(Co, t.bm) * cdiv(R, t.bn);
   splitk = 1;
   const int target = 512;  // ≥ 2 blocks per CU
   if (tiles < target) {

@@ -9,5 +9,5 @@ for K in 7 50; do for kref in 8 16 32; do
   grep '^{' gpurun_out/kb9_K${K}_kref$kref.log | K=$K KREF=$kref python -c '
 import json,os,sys
 for l in sys.stdin:
-    d=json.loads(l); print("K", os.environ["K"], "kref", os.environ["KREF"], d.get("layer"), "wgrad", d["planes_wgrad"]["-1"], "nt", d["planes_fwd_dgrad"])'
+    d=json.loads(l); print("K", os.environ["K"], "kref", os.environ["KREF"], d.get("layer"), "wgrad", d["planes_wgrad"], "nt", d["planes_fwd_dgrad"])'
 done; done
