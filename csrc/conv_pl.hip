@@ -612,19 +612,20 @@ int tn_pl_default_variant(int K, int Co, int R) {
 // at 7 clients l1 / l2 / l3 wgrad 223 / 308 / 324 vs 85 / 125 / 233 TFLOP/s, while at 50 clients
 // KREF 8 would cost l2 / l3 6-7 % in slab traffic (profiles/r3_kernel_bench_small_cohort_kref.log).
 // So 1-rank and 2-rank runs train bitwise alike; an 8-rank run's weight gradients differ from
-// them by summation order only. DLS_TN_KREF pins one KREF for every launch.
-static int tn_kref(int K) {
+// them by summation order only. Co <= 64 (5 tiles per client: l1) takes 8 at any cohort size (236
+// vs 216 TFLOP/s at 50 clients). DLS_TN_KREF pins one KREF for every launch.
+static int tn_kref(int K, int Co) {
   static const int v = [] {
     const char* e = getenv("DLS_TN_KREF");
     const int k = e ? atoi(e) : 0;
     return k > 0 ? k : 0;
   }();
   if (v) return v;
-  return K >= 16 ? 32 : 8;
+  return (K >= 16 && Co > 64) ? 32 : 8;
 }
 void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
   const TnPlTile t = kTnPlTiles[variant];
-  const long tiles = (long)tn_kref(K) * cdiv(Co, t.bm) * cdiv(R, t.bn);
+  const long tiles = (long)tn_kref(K, Co) * cdiv(Co, t.bm) * cdiv(R, t.bn);
   splitk = 1;
   const int target = 512;  // ≥ 2 blocks per CU
   if (tiles < target) {
