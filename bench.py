@@ -56,6 +56,10 @@ def vs_baseline(args, value: float, n_gpus: int, fp32: bool):
                    and not args.emulate_world and (args.model == "ResNet18" or args.workload != "fedavg_resnet18"))
     if ref is None or not fp32 or not default_cfg:
         return None
+    if args.workload == "signsgd_resnet50":
+        # the eager baseline was measured at 10 % shards (8 vote steps per round): a round of
+        # `shard_scale` holds ~shard_scale / 0.1 times as many vote steps
+        ref = ref * 0.1 / float(args.shard_scale)
     return value / (ref * n_gpus)
 
 
