@@ -324,8 +324,10 @@ void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long
                    hipStream_t s, float scale = 1.f);
 // deterministic form: keys [n] = client·V + token sorted (stable), order [n] their row indices;
 // dtable rows of absent tokens are left untouched (zero them first)
+// part (optional, embedding_bwd_part_floats): the chunked two-pass form (skewed token counts)
 void embedding_bwd_sorted(const int* keys, const int* order, const void* dy, float* dtable, long n, int D, int V,
-                          long t_cs, int f32, hipStream_t s, float scale = 1.f);
+                          long t_cs, int f32, hipStream_t s, float scale = 1.f, float* part = nullptr);
+long embedding_bwd_part_floats(long n, int D);
 // masked mean over the sequence axis of x [S][L][D] (valid length per sequence)
 void seq_mean_fwd(const void* x, const int* len, void* y, long S, int L, int D, int f32, hipStream_t s);
 void seq_mean_bwd(const void* dy, const int* len, void* dx, long S, int L, int D, int f32, hipStream_t s);

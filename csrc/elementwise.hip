@@ -669,6 +669,108 @@ __global__ void __launch_bounds__(256) embedding_bwd_sorted_kernel(const int* __
   }
 }
 
+// Chunked form for skewed token counts (padding tokens: thousands of rows of one key per client,
+// which the per-segment wave above sums serially). The sorted rows are cut into fixed chunks of
+// EMB_CH rows, one wave each (A): a key run that starts and ends inside the chunk writes its
+// table row; a run that started in an earlier chunk leaves its in-chunk sum in part[c][0], one
+// that starts here and continues leaves it in part[c][1]. Then (B) the chunk where a continuing
+// run starts adds the following chunks' part[·][0] in chunk order and writes the row. Fixed
+// chunking and order: bitwise-reproducible, no atomics, no host sync.
+constexpr int EMB_CH = 64;
+
+__device__ __forceinline__ bool emb_run_starts(const int* keys, long rs, long cs, int key) {
+  return rs > cs || rs == 0 || keys[rs - 1] != key;
+}
+__device__ __forceinline__ bool emb_run_ends(const int* keys, long re, long ce, long n, int key) {
+  return re < ce || re >= n || keys[re] != key;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) embedding_bwd_chunk_kernel(const int* __restrict__ keys,
+                                                                  const int* __restrict__ order,
+                                                                  const T* __restrict__ dy,
+                                                                  float* __restrict__ dtable,
+                                                                  float* __restrict__ part, long n, int D, int V,
+                                                                  long t_cs, float scale) {
+  const long c = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long cs = c * EMB_CH;
+  if (cs >= n) return;
+  const long ce = min(n, cs + EMB_CH);
+  for (int d0 = 0; d0 < D; d0 += 64 * 4) {
+    long rs = cs;
+    while (rs < ce) {
+      const int key = keys[rs];
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      long re = rs;
+      for (; re < ce && keys[re] == key; ++re) {
+        const T* row = dy + (long)order[re] * D;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int d = d0 + j * 64 + lane;
+          if (d < D) acc[j] += ldf(row + d);
+        }
+      }
+      const bool st = emb_run_starts(keys, rs, cs, key), en = emb_run_ends(keys, re, ce, n, key);
+      float* out;
+      float sc = 1.f;
+      if (st && en) {
+        const int k = key / V, tok = key - k * V;
+        out = dtable + (long)k * t_cs + (long)tok * D;
+        sc = scale;
+      } else {
+        out = part + (c * 2 + (st ? 1 : 0)) * (long)D;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = d0 + j * 64 + lane;
+        if (d < D) out[d] = acc[j] * sc;
+      }
+      rs = re;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) embedding_bwd_join_kernel(const int* __restrict__ keys,
+                                                                 const float* __restrict__ part,
+                                                                 float* __restrict__ dtable, long n, int D, int V,
+                                                                 long t_cs, float scale) {
+  const long c = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long cs = c * EMB_CH;
+  if (cs >= n) return;
+  const long ce = min(n, cs + EMB_CH);
+  const int key = keys[ce - 1];  // the chunk's last run
+  long rs = ce - 1;
+  while (rs > cs && keys[rs - 1] == key) --rs;
+  if (!emb_run_starts(keys, rs, cs, key) || emb_run_ends(keys, ce, ce, n, key)) return;
+  const int k = key / V, tok = key - k * V;
+  float* out = dtable + (long)k * t_cs + (long)tok * D;
+  for (int d0 = 0; d0 < D; d0 += 64 * 4) {
+    float acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = d0 + j * 64 + lane;
+      acc[j] = d < D ? part[(c * 2 + 1) * (long)D + d] : 0.f;
+    }
+    for (long c2 = c + 1;; ++c2) {  // chunks the run continues into, in order
+      const long cs2 = c2 * EMB_CH, ce2 = min(n, cs2 + EMB_CH);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = d0 + j * 64 + lane;
+        if (d < D) acc[j] += part[(c2 * 2) * (long)D + d];
+      }
+      if (ce2 >= n || keys[ce2] != key || keys[ce2 - 1] != key) break;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = d0 + j * 64 + lane;
+      if (d < D) out[d] = acc[j] * scale;
+    }
+  }
+}
+
 // masked mean over the sequence: y[s, :] = Σ_{t < len[s]} x[s, t, :] / max(len[s], 1)
 template <typename T>
 __global__ void seq_mean_fwd_kernel(const T* __restrict__ x, const int* __restrict__ len, T* __restrict__ y, int L,
@@ -875,10 +977,19 @@ void embedding_bwd(const int* tokens, const void* dy, float* dtable, int K, long
 }
 
 void embedding_bwd_sorted(const int* keys, const int* order, const void* dy, float* dtable, long n, int D, int V,
-                          long t_cs, int f32, hipStream_t s, float scale) {
+                          long t_cs, int f32, hipStream_t s, float scale, float* part) {
+  if (part) {  // chunked (part: [cdiv(n, EMB_CH)][2][D] fp32 scratch)
+    const long nch = cdiv(n, (long)EMB_CH);
+    DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_chunk_kernel<TT>, dim3(cdiv(nch, 4L)), dim3(256), 0, s, keys,
+                                       order, CP(dy), dtable, part, n, D, V, t_cs, scale));
+    DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_join_kernel<TT>, dim3(cdiv(nch, 4L)), dim3(256), 0, s, keys,
+                                       part, dtable, n, D, V, t_cs, scale));
+    return;
+  }
   DISPATCH_T(f32, hipLaunchKernelGGL(embedding_bwd_sorted_kernel<TT>, dim3(cdiv(n, 4)), dim3(256), 0, s, keys, order,
                                      CP(dy), dtable, n, D, V, t_cs, scale));
 }
+long embedding_bwd_part_floats(long n, int D) { return cdiv(n, (long)EMB_CH) * 2 * D; }
 
 void seq_mean_fwd(const void* x, const int* len, void* y, long S, int L, int D, int f32, hipStream_t s) {
   const long total = S * D;

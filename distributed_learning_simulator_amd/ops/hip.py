@@ -747,12 +747,16 @@ def embedding_bwd(dy, tokens, gtable, scale: float = 1.0):
     D = dy.shape[-1]
     gtable.zero_()
     if deterministic:
-        # rows grouped by (client, token) with a stable sort; each group summed in sequence order
+        # rows grouped by (client, token) with a stable sort; each group summed in sequence order,
+        # in fixed 64-row chunks joined in chunk order (a padding token's thousands of rows per
+        # client are summed by many waves, not one)
         V = gtable.shape[1]
         keys = (tok.view(K, -1) + torch.arange(K, device=tok.device, dtype=torch.int32)[:, None] * V).reshape(-1)
         sk, order = torch.sort(keys, stable=True)
+        n = keys.numel()
+        part = torch.empty(_C.embedding_bwd_part_floats(n, D), dtype=torch.float32, device=dy.device)
         _C.embedding_bwd_sorted(_p(sk.contiguous()), _p(order.to(torch.int32).contiguous()), _p(dy.contiguous()),
-                                _p(gtable), keys.numel(), D, V, gtable.stride(0), _f32(dy), _s(), float(scale))
+                                _p(gtable), n, D, V, gtable.stride(0), _f32(dy), _s(), float(scale), _p(part))
         return
     _C.embedding_bwd(_p(tok), _p(dy.contiguous()), _p(gtable), K, tok.numel() // K, D, gtable.stride(0), _f32(dy), _s(),
                      float(scale))
