@@ -9,6 +9,7 @@ DenseNet-40 (k=12) 1,059,298 (CIFAR-10); Transformer layer (d=100, ff=2048) 452,
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -86,6 +87,8 @@ class LeNet5Net(Module):
 
 
 # ------------------------------------------------------------------------- ResNets
+_BLOCK_OUT_PLANES = os.environ.get("DLS_BLOCK_OUT_PLANES", "1") != "0"
+
 def _residual_link(block, x, ctx):
     """Blocks in training route the shortcut's gradient of the block input through conv1's dgrad
     epilogue (Fn.ResidualLink) instead of a separate autograd add over the block input: the
@@ -116,14 +119,16 @@ class BasicBlock(Module):
         if stride != 1 or cin != cout:
             self.down = self.child("downsample", Seq(Conv2d(cin, cout, 1, stride, 0), BatchNorm(cout)))
 
-    def forward(self, x, ctx):
+    def forward(self, x, ctx, out_planes: int = 1):
+        """`out_planes`: what reads the block output (ResNetNet.forward) — 1: the next block's convs
+        (planes) and its identity shortcut (fp32); 2: convs only (a downsample block follows);
+        0: the pooling head only (fp32)."""
         link = _residual_link(self, x, ctx)
-        # split planes (fp32 GEMMs, Fn.batch_norm): bn1's output feeds conv2 only; the block
-        # output feeds the next block's convs and its shortcut
+        # split planes (fp32 GEMMs, Fn.batch_norm): bn1's output feeds conv2 only
         out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link, planes=2)
         sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
         return conv_bn(self.conv2, self.bn2, out, ctx, residual=sc, relu=True,
-                       link=link if self.down is None else None, planes=1)
+                       link=link if self.down is None else None, planes=out_planes)
 
 
 class Bottleneck(Module):
@@ -143,13 +148,14 @@ class Bottleneck(Module):
         if stride != 1 or cin != cout:
             self.down = self.child("downsample", Seq(Conv2d(cin, cout, 1, stride, 0), BatchNorm(cout)))
 
-    def forward(self, x, ctx):
+    def forward(self, x, ctx, out_planes: int = 1):
+        """`out_planes`: as BasicBlock.forward."""
         link = _residual_link(self, x, ctx)
         out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link, planes=2)
         out = conv_bn(self.conv2, self.bn2, out, ctx, planes=2)
         sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
         return conv_bn(self.conv3, self.bn3, out, ctx, residual=sc, relu=True,
-                       link=link if self.down is None else None, planes=1)
+                       link=link if self.down is None else None, planes=out_planes)
 
 
 class ResNetNet(Module):
@@ -181,8 +187,16 @@ class ResNetNet(Module):
         x = conv_bn(self.conv1, self.bn1, x, ctx, planes=0 if not self.cifar_stem else 1)
         if not self.cifar_stem:
             x = self.maxpool.forward(x, ctx)
-        for s in self.stages:
-            x = s.forward(x, ctx)
+        # each block output is written in the form(s) its readers take: split planes only when a
+        # downsample block follows (its convs read planes; its shortcut is a conv too), fp32 only
+        # before the pooling head, both otherwise (planes for the convs, fp32 for the identity
+        # shortcut's residual add)
+        # (DLS_BLOCK_OUT_PLANES=0: every block output in both forms, the A/B switch)
+        blocks = [b for s in self.stages for b in s.children]
+        for i, b in enumerate(blocks):
+            nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+            op = 0 if nxt is None else 2 if nxt.down is not None else 1
+            x = b.forward(x, ctx, out_planes=op if _BLOCK_OUT_PLANES else 1)
         x = Fn.global_avg_pool(x)
         return self.fc.forward(x, ctx)
 
