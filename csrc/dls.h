@@ -234,7 +234,8 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
             const float* pre_part = nullptr,  // [K][pre_nparts][2C] Σĝ / Σĝx̂ partials from the dgrad
             int pre_nparts = 0);              // epilogue that produced dy (ConvNTParams::bnb): no reduction pass
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
-            long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s);
+            long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s,
+            bf16_t* yp = nullptr);  // yp (fp32): y's split planes [K][2][rows][C] as well
 void ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, const void* gamma, long g_cs, int K,
             long rows_per_client, int C, void* dx, float* dgamma, float* dbeta, long dg_cs, float* ws, int f32,
             hipStream_t s);

@@ -503,11 +503,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
 int vw(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : 1; }
 
 // ------------------------------------------------------------------ LayerNorm
+// yp (fp32 only): also write y's split planes ([K][2][rpc][C]: hi, then lo rpc·C later) for the
+// split-plane linears that read it (ops.functional planes)
 template <typename T>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ gamma,
                                                      const T* __restrict__ beta, T* __restrict__ y,
                                                      float* __restrict__ mean, float* __restrict__ rstd, long g_cs,
-                                                     long nrows, long rpc, int C, float eps, int rep) {
+                                                     long nrows, long rpc, int C, float eps, int rep,
+                                                     bf16_t* __restrict__ yp) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
@@ -525,7 +528,17 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ x, co
   const float rs = rsqrtf(fmaxf(sq / C - mu * mu, 0.f) + eps);
   const T* g = gamma + (long)(k / rep) * g_cs;
   const T* b = beta + (long)(k / rep) * g_cs;
-  for (int c = lane; c < C; c += 64) stf(y + row * C + c, (ldf(xr + c) - mu) * rs * ldf(g + c) + ldf(b + c));
+  bf16_t* hp = yp ? yp + (row + (long)k * rpc) * C : nullptr;  // (row = k·rpc + r: hi at (2k·rpc + r)·C)
+  for (int c = lane; c < C; c += 64) {
+    const float o = (ldf(xr + c) - mu) * rs * ldf(g + c) + ldf(b + c);
+    stf(y + row * C + c, o);
+    if (hp) {
+      bf16_t h, l;
+      split2(rt<T>(o), h, l);
+      hp[c] = h;
+      hp[rpc * C + c] = l;
+    }
+  }
   if (lane == 0) {
     mean[row] = mu;
     rstd[row] = rs;
@@ -758,10 +771,10 @@ void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, in
 }
 
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
-            long rpc, int C, float eps, int rep, int f32, hipStream_t s) {
+            long rpc, int C, float eps, int rep, int f32, hipStream_t s, bf16_t* yp) {
   const long nrows = (long)K * rpc;
   DISPATCH_T(f32, hipLaunchKernelGGL(ln_fwd_kernel<TT>, dim3(cdiv(nrows, 4)), dim3(256), 0, s, CP(x), CP(gamma),
-                                     CP(beta), MP(y), mean, rstd, g_cs, nrows, rpc, C, eps, rep));
+                                     CP(beta), MP(y), mean, rstd, g_cs, nrows, rpc, C, eps, rep, f32 ? yp : nullptr));
 }
 
 static int ln_rows_per_wave(long rpc) { return rpc >= 4096 ? 64 : 16; }

@@ -213,9 +213,13 @@ class LayerNorm(Module):
     def own_params(self):
         return [self.gamma, self.beta]
 
-    def forward(self, x, ctx):
+    def forward(self, x, ctx, planes: bool = False):
+        """`planes`: the output's readers include split-plane linears (Fn.layer_norm); effective
+        while the weights' planes are live (as BatchNorm.forward)."""
         P = ctx.P
-        return Fn.layer_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta))
+        planes = planes and getattr(P, "split", None) is not None and self.c % 32 == 0
+        return Fn.layer_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta),
+                             planes=planes)
 
 
 class Embedding(Module):

@@ -346,11 +346,13 @@ class TransformerEncoderLayer(Module):
         # residual adds, the FFN ReLU and the dropout masks (forward and backward) ride in the
         # GEMM epilogues
         sa = ctx.dropout_seeds() if p else None  # (the attention's site first: same order as unfused)
+        # the LayerNorm outputs feed linear1 / the next layer's in_proj (split planes: the LDS-DMA
+        # plane GEMM) and the residual adds (fp32)
         x = self.norm1.forward(self.self_attn.forward(x, ctx, key_valid, residual=x, attn_drop=p, attn_seeds=sa,
-                                                      **drop()), ctx)
+                                                      **drop()), ctx, planes=True)
         h = self.linear1.forward(x, ctx, relu=True, premasked=True, **drop())
         y = self.linear2.forward(h, ctx, gate_input=True, residual=x, gate_scale=1.0 / (1.0 - p), **drop())
-        return self.norm2.forward(y, ctx)
+        return self.norm2.forward(y, ctx, planes=True)
 
 
 class TransformerClassifier(Module):

@@ -104,6 +104,8 @@ class BNBwdLink:
 # layout); `_dls_planes_only` marks a tensor whose fp32 bytes ARE those planes (the producer
 # wrote nothing else) — only a planes-reading GEMM may consume it. DLS_PLANES=0 disables.
 PLANES = os.environ.get("DLS_PLANES", "1") != "0"
+# DLS_LN_PLANES=0: LayerNorm outputs carry no split planes (A/B of the Transformer's plane linears)
+LN_PLANES = os.environ.get("DLS_LN_PLANES", "1") != "0"
 
 
 def _planes_of(t):
@@ -286,12 +288,14 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False,
-                drop_p=0.0, drop_seeds=None, gate_scale=1.0, w_split=None):
+                drop_p=0.0, drop_seeds=None, gate_scale=1.0, w_split=None, x_planes=None):
         be = _be(x)
         if be is ref or x.dtype != torch.float32:
             w_split = None
         ws = {"w_split": w_split} if w_split is not None else {}
-        y = be.linear_fwd(x, w, b, relu=relu, acc=residual, drop_p=drop_p, drop_seeds=drop_seeds, **ws)
+        # x's split planes (a LayerNorm output, Fn.layer_norm planes): the plane GEMM reads them
+        xp = {"x_planes": x_planes} if (x_planes is not None and w_split is not None) else {}
+        y = be.linear_fwd(x, w, b, relu=relu, acc=residual, drop_p=drop_p, drop_seeds=drop_seeds, **ws, **xp)
         ctx.ws = ws
         mask_dy = relu and not premasked
         ctx.save_for_backward(x, w, y if mask_dy else None, drop_seeds if drop_p else None)
@@ -323,7 +327,7 @@ class _Linear(torch.autograd.Function):
                     ctx.gb.copy_(db)
             else:
                 be.linear_wgrad(dy, x, ctx.gw, ctx.gb)
-        return dx, None, None, None, None, None, dres, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, dres, None, None, None, None, None, None, None, None
 
 
 def linear(x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, gate_input=False,
@@ -333,10 +337,11 @@ def linear(x, token, w, b, gw, gb, residual=None, relu=False, premasked=False, g
     pre-split bf16 planes (BoundParams.ws) for the fp32 GEMMs."""
     assert not (relu and residual is not None), "ReLU and residual epilogues are not combined"
     shp = x.shape
+    xp = _planes_of(x)  # (the reshape below is a new tensor object: carry the planes explicitly)
     x3 = x.reshape(shp[0], -1, shp[-1])
     r3 = residual.reshape(shp[0], x3.shape[1], -1).contiguous() if residual is not None else None
     y = _Linear.apply(x3, token, w, b, gw, gb, r3, relu, premasked, gate_input, drop_p, drop_seeds, gate_scale,
-                      w_split)
+                      w_split, xp)
     return y.reshape(*shp[:-1], y.shape[-1])
 
 
@@ -478,11 +483,18 @@ def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False
 # ------------------------------------------------------------------------ layernorm
 class _LN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, token, gamma, beta, ggamma, gbeta):
+    def forward(ctx, x, token, gamma, beta, ggamma, gbeta, planes=False):
         be = _be(x)
-        y, mean, rstd = be.ln_fwd(x, gamma, beta)
+        yp = None
+        if (planes and PLANES and LN_PLANES and be is not ref and x.dtype == torch.float32
+                and be.planes_fit(x[0].numel())):
+            y, mean, rstd, yp = be.ln_fwd(x, gamma, beta, planes=True)
+        else:
+            y, mean, rstd = be.ln_fwd(x, gamma, beta)
         ctx.save_for_backward(x, mean, rstd, gamma)
         ctx.ggamma, ctx.gbeta = ggamma, gbeta
+        if yp is not None:
+            _tag_planes(y, yp, False)
         return y
 
     @staticmethod
@@ -493,11 +505,13 @@ class _LN(torch.autograd.Function):
         if ctx.ggamma is not None:
             ctx.ggamma.copy_(dgamma)
             ctx.gbeta.copy_(dbeta)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def layer_norm(x, token, gamma, beta, ggamma, gbeta):
-    return _LN.apply(x, token, gamma, beta, ggamma, gbeta)
+def layer_norm(x, token, gamma, beta, ggamma, gbeta, planes: bool = False):
+    """`planes` (fp32 native): the output also carries its split planes (`_dls_planes`) for the
+    split-plane linears that read it (Fn.linear)."""
+    return _LN.apply(x, token, gamma, beta, ggamma, gbeta, planes)
 
 
 # -------------------------------------------------------------------------- pooling

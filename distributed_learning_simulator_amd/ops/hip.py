@@ -447,10 +447,12 @@ def bias_grad(dy, gb):
 
 
 # --------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_seeds=None, w_split=None):
+def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_seeds=None, w_split=None,
+               x_planes=None):
     """y = x Wᵀ + b, optionally ReLU'd, dropped out (`drop_p`, per-client-row `drop_seeds`
     [K] int32: the epilogue mask of `dropout_apply`) and/or + `acc` (a residual branch), in the
-    epilogue."""
+    epilogue. `x_planes` [K, 2, N, Fi] (fp32, with `w_split`): x's split planes — the LDS-DMA
+    plane GEMM (csrc/conv_pl.hip) when the shape allows (planes_ok)."""
     K, N, Fi = x.shape
     x = x.contiguous()
     f32 = _f32(x)
@@ -462,9 +464,13 @@ def linear_fwd(x, w, b=None, relu=False, acc=None, drop_p: float = 0.0, drop_see
     if acc is not None:
         assert acc.shape == y.shape and acc.dtype == x.dtype and acc.is_contiguous()
     ws_p, ws_cs, ws_plane = _wsplit_args(w_split if f32 else None, w)
-    _C.conv_nt(_p(x), _p(w), _p(y), _p(b), N * Fi, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
+    xp, x_cs, x_lo = _p(x), N * Fi, 0
+    if x_planes is not None and f32 and ws_p and planes_ok(Fi, Fo):
+        xp, x_cs, x_lo = _planes_args(x_planes.reshape((K, 2) + tuple(x.shape[1:])), x)
+        planes_launches["linear_fwd"] += 1
+    _C.conv_nt(xp, _p(w), _p(y), _p(b), x_cs, N * Fo, w_cs, b_cs, 1, N, 1, Fi, N, 1, 1, 1, 1, 0, 1, N, Fo, Fi, rep,
                int(relu), K, 0, nt_f32_variant if f32 else nt_variant, _p(acc), NULL, f32, _s(), 0, 0, NULL, NULL,
-               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, ws_p, ws_cs, ws_plane, 0)
+               _p(_drop_seeds(drop_seeds, K, drop_p)), float(drop_p), 0.0, ws_p, ws_cs, ws_plane, x_lo)
     return y
 
 
@@ -624,7 +630,9 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
 
 
 # ------------------------------------------------------------------------ layernorm
-def ln_fwd(x, gamma, beta, eps=1e-5):
+def ln_fwd(x, gamma, beta, eps=1e-5, planes: bool = False):
+    """`planes` (fp32): also write y's split planes [K, 2, *x.shape[1:]] (returned fourth) for
+    the split-plane linears that read y."""
     K = x.shape[0]
     C = x.shape[-1]
     x = x.contiguous()
@@ -634,7 +642,10 @@ def ln_fwd(x, gamma, beta, eps=1e-5):
     mean = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
     rstd = torch.empty_like(mean)
     assert gamma.dtype == x.dtype
-    _C.ln_fwd(_p(x), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), g_cs, K, rpc, C, eps, rep, _f32(x), _s())
+    yp = torch.empty((K, 2) + tuple(x.shape[1:]), dtype=BF16, device=x.device) if planes and x.dtype == F32 else None
+    _C.ln_fwd(_p(x), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), g_cs, K, rpc, C, eps, rep, _f32(x), _s(), _p(yp))
+    if planes:
+        return y, mean, rstd, yp
     return y, mean, rstd
 
 

@@ -772,3 +772,24 @@ def test_embedding_bwd_skewed_tokens_deterministic(hip, D):
     hip.embedding_bwd(dy, tok, g2, 0.5)
     assert torch.equal(g1, g2)
     _close(g1, ref.embedding_bwd(_d(dy), tok.cpu(), V, 0.5), 1e-5)
+
+
+def test_layernorm_planes_feed_plane_linear(hip):
+    """LayerNorm writing its output's split planes (hi = bf16(y), lo = bf16(y − hi)) bitwise equal
+    to split_planes(y); a linear reading them runs the LDS-DMA plane GEMM within 1e-5 of fp64."""
+    torch.manual_seed(3)
+    K, B, L, D, Fo = 2, 3, 40, 512, 1536
+    x = _f(K, B, L, D) * 2 + 0.5
+    g = torch.rand(K, D, device=DEV) + 0.5
+    b = _f(K, D)
+    y, mean, rstd, yp = hip.ln_fwd(x, g, b, planes=True)
+    y0, _, _ = hip.ln_fwd(x, g, b)
+    assert torch.equal(y, y0)
+    assert torch.equal(yp, hip.split_planes(y))
+    w = _f(K, Fo, D, scale=0.05)
+    bias = _f(K, Fo)
+    ws = _wsplit(hip, w)
+    before = hip.planes_launches["linear_fwd"]
+    out = hip.linear_fwd(y.reshape(K, B * L, D), w, bias, w_split=ws, x_planes=yp.reshape(K, 2, B * L, D))
+    assert hip.planes_launches["linear_fwd"] == before + 1
+    _close(out, torch.einsum("knd,kod->kno", _d(y).reshape(K, B * L, D), _d(w)) + _d(bias)[:, None])
