@@ -43,6 +43,25 @@ def test_stochastic_payload_roundtrip_and_bytes():
         assert ((dq[:, e.offset : e.offset + e.numel] - seg).abs() <= step * 1.0001 + 1e-30).all()
 
 
+def test_qsgd_code_unbiased_signed_levels():
+    """QSGD form: codes are 255 signed levels of the per-tensor max-abs norm — the
+    extremes ±‖x‖ are exact, zero is a level, signs are kept — and E[Q(x)] = x over seeds."""
+    lay = _layout()
+    x = _rows(lay, K=2, seed=3)
+    seg, sizes = lay.segment_ids(), lay.segment_sizes()
+    reps = torch.stack([quant.stochastic_quantize(x, seg, sizes, fl.row_seeds(s, [0, 1]))[0] for s in range(200)])
+    for e in lay.entries:
+        sl = slice(e.offset, e.offset + e.numel)
+        xs, q = x[:, sl], reps[:, :, sl]
+        norm = xs.abs().amax(1, keepdim=True)
+        levels = q / (norm / 127)
+        assert torch.allclose(levels, levels.round(), atol=1e-3)  # on the grid
+        assert levels.abs().max() <= 127 + 1e-3
+        assert ((q == 0) | (torch.sign(q) == torch.sign(xs))).all()  # sign kept (or rounded to 0)
+        err = (q.mean(0) - xs).abs().max() / norm.max()
+        assert err < 0.003, err  # unbiased: the mean of 200 draws sits well inside one level (norm / 127)
+
+
 def test_nnadq_payload_roundtrip_bits_and_mask():
     lay = _layout()
     meta = compress.LayoutMeta.of(lay, "cpu")
