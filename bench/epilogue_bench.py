@@ -1,0 +1,98 @@
+"""Epilogue cost of the fp32 plane / halo convolutions on the ResNet-18 stride-1 layers.
+
+A conv's dgrad in a ResNet block does more than store dX: it adds the residual link's gradient
+(`acc`) and writes the consuming BatchNorm's backward partials (`bnb`: reads the BN input x and
+its ReLU bit mask). The forward writes the BN statistics partials (`stats`). This times each
+epilogue form next to the plain one on the same GEMM, interleaved in one process, so the
+epilogue's share of the kernel is visible (TFLOP/s of the GEMM, ms per call):
+
+    python bench/epilogue_bench.py [--K 50] [--iters 10] [--rounds 3]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+# (name, H, C, Co, k): stride-1 convs of ResNet-18 / CIFAR whose dgrad carries epilogue work
+LAYERS = [("l1", 32, 64, 64, 3), ("l2", 16, 128, 128, 3), ("l3", 8, 256, 256, 3), ("l4", 4, 512, 512, 3)]
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=50)
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    from distributed_learning_simulator_amd.ops import build
+
+    build.build()
+    from distributed_learning_simulator_amd.ops import hip
+
+    K, B, dev = args.K, args.B, "cuda"
+    for name, H, C, Co, k in LAYERS:
+        if args.only and name not in args.only.split(","):
+            continue
+        torch.manual_seed(0)
+        pad = k // 2
+        R = B * H * H
+        x = torch.randn(K, B, H, H, C, device=dev)
+        dy = torch.randn(K, B, H, H, Co, device=dev)
+        w = torch.randn(K, Co, k, k, C, device=dev) * 0.05
+        n = Co * k * k * C
+        wpl = torch.empty((K, 2, n), dtype=torch.bfloat16, device=dev)
+        hip.split_rows(w.reshape(K, n).contiguous(), wpl)
+        ws = wpl[:, 0].unflatten(1, (Co, k, k, C))
+        xp, dyp = hip.split_planes(x), hip.split_planes(dy)
+        # the BN whose dY the dgrad's dX is: input xb [K, R, C], ReLU bit mask, mean / rstd
+        xb = torch.randn(K, R, C, device=dev)
+        mask = torch.randint(0, 256, (K, R * C // 8), dtype=torch.uint8, device=dev)
+        mean = torch.randn(K, C, device=dev) * 0.1
+        rstd = torch.rand(K, C, device=dev) + 0.5
+        acc = torch.randn(K, B, H, H, C, device=dev)
+        part_b = torch.empty((K, hip.conv_stats_parts(R), 2, C), device=dev)
+        part_f = torch.empty((K, hip.conv_stats_parts(R), 2, Co), device=dev)
+        bnb = (part_b, xb, mask, mean, rstd, None, None)
+        flops = 2.0 * K * R * Co * C * k * k
+        cases = {
+            "fwd": lambda: hip.conv_fwd(x, w, 1, pad, w_split=ws, x_planes=xp),
+            "fwd_stats": lambda: hip.conv_fwd(x, w, 1, pad, w_split=ws, x_planes=xp, stats=part_f),
+            "dgrad": lambda: hip.conv_dgrad(dy, w, (H, H), 1, pad, w_split=ws, dy_planes=dyp),
+            "dgrad_acc": lambda: hip.conv_dgrad(dy, w, (H, H), 1, pad, w_split=ws, dy_planes=dyp, acc=acc),
+            "dgrad_bnb": lambda: hip.conv_dgrad(dy, w, (H, H), 1, pad, w_split=ws, dy_planes=dyp, bnb=bnb),
+            "dgrad_acc_bnb": lambda: hip.conv_dgrad(dy, w, (H, H), 1, pad, w_split=ws, dy_planes=dyp, acc=acc,
+                                                    bnb=bnb),
+        }
+        best = {c: float("inf") for c in cases}
+        for _ in range(args.rounds):
+            for c, fn in cases.items():
+                best[c] = min(best[c], timeit(fn, args.iters))
+        row = {"layer": name, "K": K, "B": B, "H": H, "C": C, "Co": Co}
+        for c, t in best.items():
+            row[f"{c}_ms"] = round(t * 1e3, 4)
+            row[f"{c}_tflops"] = round(flops / t / 1e12, 1)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -66,7 +66,11 @@ class FedAVGAlgorithm(AggregationAlgorithm):
                 self._w_block = bw if self._w_block is None else self._w_block + bw
                 self._block_ids = msg.extra["block_ids"]
         self._w_total += w.sum()
-        self._reported += len(msg.client_ids)
+        # clients that carry weight: counted on the host when the sizes are host tensors; a
+        # device-resident size vector is not read back (no sync per message), so there every
+        # message's clients count and the 'no reported client' warning means 'no upload'
+        ds = msg.dataset_sizes
+        self._reported += int((ds != 0).sum()) if not ds.is_cuda else len(msg.client_ids)
         self._dataset_size += float(msg.dataset_sizes.sum().item()) if not msg.dataset_sizes.is_cuda else 0.0
 
     @property
@@ -150,7 +154,7 @@ class FedAVGAlgorithm(AggregationAlgorithm):
             else:
                 new = torch.where(wt > 0, acc / wt.clamp(min=1e-300), old)
             if self._reported == 0:  # (host-side count: no device read)
-                get_logger().warning("round without any reported client: global model unchanged")
+                get_logger().warning("round without any weighted client upload: global model unchanged")
         self.last_fp64 = new  # pre-cast fp64 result (golden tests)
         new = new.to(old_dtype)
         if self.config is not None and self.config.debug:

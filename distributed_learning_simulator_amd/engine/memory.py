@@ -19,10 +19,18 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 
 import torch
 
 from ..utils.logging import get_logger
+
+# Device-wide operations that must not overlap a HIP-graph capture running on another thread of
+# this process (concurrent training tasks, training.train(config, practitioners)): the capture
+# itself with the allocator trims around it, device-wide synchronisation and the activation
+# probe (whose peak-memory counters are device-global). Re-entrant; uncontended in a
+# one-session process.
+DEVICE_LOCK = threading.RLock()
 
 
 def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
@@ -98,7 +106,8 @@ def plan_capacity(wanted: int, layout, model, dc, hyper, device, compute_dtype,
     if device.type != "cuda" or wanted <= 1:
         return max(1, wanted)
     state = state_bytes_per_client(layout, compute_dtype, hyper.optimizer_name)
-    act = probe_activation_bytes(model, dc, hyper, device, compute_dtype)
+    with DEVICE_LOCK:
+        act = probe_activation_bytes(model, dc, hyper, device, compute_dtype)
     per_client = state + int(act * 1.15)  # allocator slack
     free, _total = torch.cuda.mem_get_info(device)
     cap = max(1, min(wanted, int(math.floor(fraction * free / max(per_client, 1)))))

@@ -34,6 +34,7 @@ from ..ops import fl
 from ..ops import functional as Fn
 from ..utils.tracing import trace
 from .hooks import ExecutorHookPoint, HookRegistry, StopExecutingException
+from .memory import DEVICE_LOCK
 from .params import BoundParams, CohortBuffers
 
 
@@ -450,8 +451,9 @@ class CohortTrainer:
                 old = self._graphs.pop(next(iter(self._graphs)))
                 old.graph = None
                 del old
-                torch.cuda.synchronize(self.device)
-                torch.cuda.empty_cache()
+                with DEVICE_LOCK:
+                    torch.cuda.synchronize(self.device)
+                    torch.cuda.empty_cache()
             sg = self._graphs[key] = _StepGraph(K, B, self.device)
         streams = self._streams(len(parts))
 
@@ -483,24 +485,27 @@ class CohortTrainer:
                     run_parts()
                     sg.eager_steps += 1
                 else:
-                    # the eager step's cached blocks go back to the driver so the graph's private
-                    # pool can take them (else activation memory is held twice)
-                    torch.cuda.synchronize(self.device)
-                    torch.cuda.empty_cache()
-                    g = torch.cuda.CUDAGraph()
-                    # no cyclic GC while capturing: a collected cycle holding an older session's
-                    # graph or tensors would free device memory inside the capture (HIP aborts);
-                    # torch.cuda.graph collects once on entry
-                    gc_was_enabled = gc.isenabled()
-                    gc.disable()
-                    try:
-                        # thread-local capture: RCCL's watchdog thread keeps polling its events
-                        # while this rank captures (global mode would fail those calls)
-                        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                            run_parts()
-                    finally:
-                        if gc_was_enabled:
-                            gc.enable()
+                    # one capture at a time per process, and no device-wide synchronisation of
+                    # another task thread inside it (engine.memory.DEVICE_LOCK)
+                    with DEVICE_LOCK:
+                        # the eager step's cached blocks go back to the driver so the graph's
+                        # private pool can take them (else activation memory is held twice)
+                        torch.cuda.synchronize(self.device)
+                        torch.cuda.empty_cache()
+                        g = torch.cuda.CUDAGraph()
+                        # no cyclic GC while capturing: a collected cycle holding an older
+                        # session's graph or tensors would free device memory inside the capture
+                        # (HIP aborts); torch.cuda.graph collects once on entry
+                        gc_was_enabled = gc.isenabled()
+                        gc.disable()
+                        try:
+                            # thread-local capture: RCCL's watchdog thread (and other task threads'
+                            # launches on their own streams) keep running while this one captures
+                            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                                run_parts()
+                        finally:
+                            if gc_was_enabled:
+                                gc.enable()
                     sg.graph = g
                     g.replay()
                 if s + 1 == schedule.epoch_end[e]:

@@ -165,8 +165,14 @@ class _Conv(torch.autograd.Function):
         else:
             y = be.conv_fwd(x, w, stride, pad, bias=b)
         ctx.w_split = w_split
+        # the consuming BN will hand the backward dY as planes only: a dY without them (a tensor
+        # rebuilt on the way, which drops the _dls_planes attributes) must fail, not be read as fp32
+        ctx.expect_dy_planes = stats is not None and stats.dy_planes_ok
+        ctx.x_planes_only = bool(getattr(x, "_dls_planes_only", False))
         bnb = getattr(x, "_dls_bnb", None) if BN_BWD_PARTS else None
-        if bnb is not None and not (be is not ref and donor is None and x.shape[-1] == ci
+        # (the dgrad writes the partials only in one launch: a dY or dX window past 2 GiB runs
+        # batch-chunked, e.g. a 64 -> 256 1x1 conv whose output alone crosses it)
+        if bnb is not None and not (be is not ref and donor is None and x.shape[-1] == ci and not big
                                     and be.bn_bwd_parts_ok(x.shape, stride, x.dtype)):
             bnb = None
         ctx.bnb = bnb
@@ -203,6 +209,8 @@ class _Conv(torch.autograd.Function):
         if dyp is not None and ctx.xp is None:
             raise RuntimeError("conv2d backward: dY planes without the input's planes")
         if dyp is None:
+            if ctx.expect_dy_planes:
+                raise RuntimeError("conv2d backward: the BN wrote dY as planes only, but they did not arrive")
             _require_fp32(dy, "conv2d backward")
         donor = ctx.donor
         compact = (donor is not None and not donor.receiver_done and be is not ref and dy.dtype == torch.float32
@@ -247,7 +255,7 @@ class _Conv(torch.autograd.Function):
             elif dyp is not None:
                 be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad, dy_planes=dyp, x_planes=ctx.xp)
             else:
-                if ctx.xp is not None and getattr(x, "_dls_planes_only", False):
+                if ctx.x_planes_only:
                     raise RuntimeError("conv2d backward: fp32 dY with a planes-only input")
                 be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad)
                 if ctx.gb is not None:

@@ -10,6 +10,7 @@ from __future__ import annotations
 import collections
 import importlib
 import os
+import threading
 
 import torch
 
@@ -54,7 +55,7 @@ def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-_keepalive: collections.deque = collections.deque(maxlen=48)  # > pointer args of any one launch
+_tls = threading.local()  # per thread: concurrent training tasks build launches in parallel
 
 
 def _p(t) -> int:
@@ -62,10 +63,14 @@ def _p(t) -> int:
     consumes the pointer: an inline temporary (`_p(x.to(...))`) would otherwise be freed
     while the argument list is still being built and a second temporary in the same call
     could be allocated at the same address. After the launch, the caching allocator's
-    stream ordering makes reuse safe."""
+    stream ordering makes reuse safe. (The keep-alive ring is per thread, so another task
+    thread's launches cannot push this launch's temporaries out early.)"""
     if t is None:
         return 0
-    _keepalive.append(t)
+    ring = getattr(_tls, "keepalive", None)
+    if ring is None:
+        ring = _tls.keepalive = collections.deque(maxlen=48)  # > pointer args of any one launch
+    ring.append(t)
     return t.data_ptr()
 
 
@@ -865,9 +870,8 @@ def attn_fwd_packed(qkv, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds
     kv = _key_valid(key_valid, qkv)
     o = torch.empty((K, B, L, D), dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty((K, B, H, L), dtype=torch.float32, device=qkv.device)
-    base = qkv.data_ptr()
+    base = _p(qkv)
     es = qkv.element_size()
-    _keepalive.append(qkv)
     sp, dp_ = _attn_drop(drop_p, drop_seeds, K, qkv)
     ok = _C.attn_fwd(base, base + D * es, base + 2 * D * es, _p(kv), _p(o), _p(lse), K * B * H, H, L, DH,
                      _f32(qkv), _s(), D3, D, sp, B * H, dp_)
@@ -884,9 +888,7 @@ def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None, drop_p: float = 0.0
     kv = _key_valid(key_valid, qkv)
     dqkv = torch.empty_like(qkv)
     delta = torch.empty((K, B, H, L), dtype=torch.float32, device=qkv.device)
-    b, g, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
-    _keepalive.append(qkv)
-    _keepalive.append(dqkv)
+    b, g, es = _p(qkv), _p(dqkv), qkv.element_size()
     sp, dp_ = _attn_drop(drop_p, drop_seeds, K, qkv)
     ok = _C.attn_bwd(_p(do), b, b + D * es, b + 2 * D * es, _p(o), _p(lse.contiguous()), _p(kv), g, g + D * es,
                      g + 2 * D * es, _p(delta), K * B * H, H, L, DH, _f32(qkv), _s(), D3, D, sp, B * H, dp_)

@@ -27,7 +27,7 @@ import time
 import torch
 
 from .data.datasets import create_dataset_collection, get_spec
-from .engine.memory import plan_capacity
+from .engine.memory import DEVICE_LOCK, plan_capacity
 from .engine.trainer import CohortTrainer, HyperParameter
 from .method import CentralizedAlgorithmFactory
 from .models.zoo import build_model, stored_image_channels
@@ -144,7 +144,8 @@ class Session:
 
     def sync(self) -> None:
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            with DEVICE_LOCK:  # (not inside another task thread's graph capture)
+                torch.cuda.synchronize(self.device)
 
     # ---------------------------------------------------------------------- run
     def run(self) -> dict:
@@ -180,7 +181,8 @@ class Session:
                 for m in self.metrics:
                     f.write(json.dumps(m) + "\n")
         result = {"performance": server.performance_stat, "metrics": self.metrics,
-                  "bytes_up": self.bytes_up_total, "bytes_down": self.bytes_down_total, "seconds": total}
+                  "bytes_up": self.bytes_up_total, "bytes_down": self.bytes_down_total, "seconds": total,
+                  "save_dir": cfg.save_dir}
         algo = server.algorithm
         if algo is not None and hasattr(algo, "shapley_values"):
             result["sv"] = algo.shapley_values

@@ -9,7 +9,10 @@ from worker ids to practitioner ids.
 
 Here one call = one `Session` per rank. Under torchrun (WORLD_SIZE>1) every rank calls
 `train` and rank 0's result is returned. Concurrent tasks run in background threads of the
-calling process (each with its own Session and a single-rank communicator).
+calling process, each with its own Session, single-rank communicator, HIP stream and
+`save_dir/task_<id>` output directory; HIP-graph captures and device-wide synchronisation are
+serialised across those threads (engine.memory.DEVICE_LOCK). Tested against serial runs in
+tests/test_concurrent.py (the reference's `test/test_concurrent.py:11-46`).
 """
 
 from __future__ import annotations
@@ -45,6 +48,19 @@ def _run(config, practitioners=None, comm: Comm | None = None) -> dict:
     return session.run()
 
 
+def _run_task(config, practitioners, comm: Comm) -> dict:
+    """A concurrent task's thread: its own HIP stream, so its kernels, allocator traffic and
+    waits never serialise against another task's (kernel workspaces are keyed by stream, and
+    graph captures are serialised process-wide by engine.memory.DEVICE_LOCK)."""
+    if comm.device.type == "cuda":
+        import torch
+
+        torch.cuda.set_device(comm.device)
+        with torch.cuda.stream(torch.cuda.Stream(comm.device)):
+            return _run(config, practitioners, comm)
+    return _run(config, practitioners, comm)
+
+
 def train(config, practitioners=None) -> dict | int | None:
     config = copy.deepcopy(config)
     _check_limits()
@@ -62,8 +78,11 @@ def train(config, practitioners=None) -> dict | int | None:
         if _pool is None:
             _pool = ThreadPoolExecutor(max_workers=int(os.environ.get("DLS_MAX_CONCURRENT_TASKS", "8")))
     task_id = uuid.uuid4().int
+    # each task writes under its own directory (the reference names a task's executors
+    # "worker <id> of <task>", executor.py:60-67): concurrent tasks of one config never share files
+    config.save_dir = os.path.join(config.save_dir or "session", f"task_{task_id:032x}")
     comm = Comm(0, 1, init_distributed().device)
-    fut: Future = _pool.submit(_run, config, list(practitioners), comm)
+    fut: Future = _pool.submit(_run_task, config, list(practitioners), comm)
     _tasks[task_id] = {"future": fut, "practitioner_ids": sorted(p.id for p in practitioners), "config": config}
     return task_id
 
