@@ -12,6 +12,9 @@ The other BASELINE.json configs are selectable with `--workload` (same JSON cont
                       second_phase_epoch 10): block dropout 0.3 + NNADQ 1e-4
   signsgd_resnet50    config 4: sign-SGD, 128 clients, ResNet-50, ImageNet-shaped (batch 128; one
                       round = one local epoch of 1-bit majority-vote steps over a scaled ImageNet shard)
+  signsgd_densenet40  the reference's own `conf/sign_sgd/cifar10.yaml` (DenseNet-40, 10 workers, batch 64,
+                      SGD 0.1 cosine): one round = `--epoch` epochs of vote steps (the config's 100 epochs
+                      in one round is 7.9k steps; vote steps/s is the comparable figure)
   gtg_resnet18        config 5: GTG-Shapley, 32 clients, ResNet-18, 5 local epochs, full test split
   fedavg_mlp_mnist    config 1: FedAvg, 4 clients, MLP, MNIST-shaped (the CPU plumbing check)
 
@@ -70,7 +73,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="fedavg_resnet18",
                     choices=["fedavg_resnet18", "fedavg_densenet40", "fedobd_transformer", "fedobd_imdb",
-                             "signsgd_resnet50", "gtg_resnet18", "fedavg_mlp_mnist"])
+                             "signsgd_resnet50", "signsgd_densenet40", "gtg_resnet18", "fedavg_mlp_mnist"])
     ap.add_argument("--algo", default="fed_avg", choices=["fed_avg", "fed_obd"])
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--clients", type=int, default=100)
@@ -321,6 +324,25 @@ def workload_config(args, rounds: int) -> dict:
                 "config_extra": {"d_model": 512, "nhead": 8, "layers": 6, "ffn": 2048},
                 "metric": "FL rounds/sec (FedOBD stage 1, 100 clients / 50 per round, Transformer-base, AG-News-shaped)",
                 "data": "synthetic (AG-News-shaped token sequences, max_len 128, iid shards, random-init weights)"}
+    if args.workload == "signsgd_densenet40":
+        # conf/sign_sgd/cifar10.yaml verbatim but for `epoch` (--epoch; the config's 100 epochs make
+        # one 7.9k-step round): every step is one 1-bit majority vote over the 10 clients
+        cfg = {"distributed_algorithm": "sign_SGD", "dataset_name": "CIFAR10", "model_name": "densenet40",
+               "worker_number": 10, "epoch": args.epoch, "batch_size": 64, "optimizer_name": "SGD",
+               "learning_rate": 0.1, "learning_rate_scheduler_name": "CosineAnnealingLR",
+               "distribute_init_parameters": False}
+
+        def dn_extra(sess, s_per_round):
+            name = sess.dc.spec.name
+            B = sess.config.batch_size
+            n = max((p.dataset_size(name) + B - 1) // B for p in sess.practitioners.values()) * sess.config.epoch
+            return {"vote_steps_per_round": n, "ms_per_vote_step": s_per_round / n * 1e3,
+                    "vote_steps_per_s": n / s_per_round,
+                    "reference_round_s_estimate": 100 / sess.config.epoch * s_per_round}
+
+        return {"config": {**cfg, **common}, "samples_per_round": shard_samples, "extra": dn_extra,
+                "metric": "FL rounds/sec (sign-SGD, 10 clients, DenseNet-40, CIFAR-10-shaped)",
+                "data": "synthetic (CIFAR-10-shaped, iid shards, random-init weights)"}
     if args.workload == "signsgd_resnet50":
         scale = float(args.shard_scale)
         cfg = {"distributed_algorithm": "sign_SGD", "dataset_name": "ImageNet", "model_name": "Resnet50",

@@ -265,11 +265,7 @@ static int attn_rows(int L) {
 // padded to 64, 64) runs there unless DLS_ATTN_MFMA=0; the VALU kernels below are the fallback
 // (no dropout, no packed layouts)
 static bool use_mfma(int L, int DH) {
-  static const int mode = [] {
-    const char* e = getenv("DLS_ATTN_MFMA");
-    return e ? atoi(e) : 1;
-  }();
-  return mode != 0 && attn_mfma_supported(L, DH);
+  return native_option(g_opt_attn_mfma, "DLS_ATTN_MFMA", 1) != 0 && attn_mfma_supported(L, DH);
 }
 
 bool attn_packed_supported(int L, int DH) { return use_mfma(L, DH); }

@@ -409,11 +409,7 @@ int vw(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 // the other sub-cohort stream fills the GPU and per-CU efficiency matters more than grid fill
 // (rank 0's share of an 8-rank round, 2 streams: off 743 ms, NT rule 757, wgrad rule 765)
 int small_k_rules() {
-  static const int v = [] {
-    const char* e = getenv("DLS_F32_SMALLK");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
+  return native_option(g_opt_f32_smallk, "DLS_F32_SMALLK", 0);
 }
 
 // --------------------------------------------------------------------------- TN (wgrad)
@@ -780,8 +776,6 @@ int conv_tn_f32_num_variants() { return kTnF32Variants; }
 
 void conv_tn_f32(ConvTNParams p, int K, int variant, hipStream_t s) {
   if (p.dy_lo != 0) {  // pre-split dY / X planes: the LDS-DMA kernels of conv_pl.hip
-    // 3x3 stride 1: the halo wgrad (conv_wgrad_halo.hip) unless a tile variant was forced
-    if (variant < 0 && conv_wgrad_halo(p, K, s)) return;
     if (!conv_tn_pl(p, K, variant, s)) {
       fprintf(stderr, "conv_tn_f32: pre-split operands in an unsupported shape (C %d, Co %d)\n", p.C, p.Co);
       abort();

@@ -294,11 +294,7 @@ void launch_gl(ConvGLParams& p, int K, hipStream_t s) {
 
 // -1: shape heuristic; 0: never; 1: whenever the shape is supported (tests, A/B benchmarks)
 int gl_mode() {
-  static int mode = [] {
-    const char* e = getenv("DLS_CONV_GL");
-    return e ? atoi(e) : -1;
-  }();
-  return mode;
+  return native_option(g_opt_conv_gl, "DLS_CONV_GL", -1);
 }
 
 }  // namespace

@@ -257,7 +257,9 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   }
   hwait_vm<0>();
 
-  nt_f32_epilogue<TM, TN, NW>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
+  // (epilogue operand prefetch where the accumulators leave the VGPRs for it: the l1 shape, whose
+  // dgrads carry a residual gradient and BN partials over 64 channels)
+  nt_f32_epilogue<TM, TN, NW, (TM * TN <= 2 ? 2 : -1)>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
 }
 
 template <int IMG, int TH, int TW, int BN, int WM, int WN, int HB, int NBS>

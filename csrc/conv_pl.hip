@@ -296,11 +296,7 @@ bool conv_nt_pl_supported(const ConvNTParams& p) {
 // 256x256 tile keeps 380 / 325 vs 350 / 303, profiles/r3_kernel_bench_small_cohort_kref.log).
 // DLS_PL_MIN_WG overrides the threshold (0 = always 256x256)
 static int pl_min_wg() {
-  static const int v = [] {
-    const char* e = getenv("DLS_PL_MIN_WG");
-    return e ? atoi(e) : 256;
-  }();
-  return v;
+  return native_option(g_opt_pl_min_wg, "DLS_PL_MIN_WG", 256);
 }
 
 int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
@@ -615,12 +611,8 @@ int tn_pl_default_variant(int K, int Co, int R) {
 // them by summation order only. Co <= 64 (5 tiles per client: l1) takes 8 at any cohort size (236
 // vs 216 TFLOP/s at 50 clients). DLS_TN_KREF pins one KREF for every launch.
 static int tn_kref(int K, int Co) {
-  static const int v = [] {
-    const char* e = getenv("DLS_TN_KREF");
-    const int k = e ? atoi(e) : 0;
-    return k > 0 ? k : 0;
-  }();
-  if (v) return v;
+  const int v = native_option(g_opt_tn_kref, "DLS_TN_KREF", 0);
+  if (v > 0) return v;
   return (K >= 16 && Co > 64) ? 32 : 8;
 }
 void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {

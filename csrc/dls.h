@@ -6,6 +6,15 @@
 
 typedef uint16_t bf16_t;
 
+// Host-side launch knobs (A/B measurements, tests), one object instead of import-time globals:
+// each starts UNSET and then takes its environment variable (or the default) on first use;
+// set_native_option() — the Python RuntimeOptions (distributed_learning_simulator_amd/options.py)
+// — overrides it at any time between launches. Defined in elementwise.hip.
+constexpr int kOptUnset = -1000000;
+extern int g_opt_attn_mfma, g_opt_f32_smallk, g_opt_conv_gl, g_opt_pl_min_wg, g_opt_tn_kref, g_opt_bn_coef_groups;
+int native_option(int& slot, const char* env, int dflt);
+bool set_native_option(const char* name, int value);  // false: unknown name
+
 // Division by a runtime-constant divisor without the ~40-instruction integer divide:
 // q = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31 (host precomputes mul/shift).
 struct FastDiv {
@@ -202,12 +211,6 @@ void conv_tn_pl_set_variant(int v);
 int conv_tn_pl_splitk(int K, int Co, int R, int M, int variant);
 // dw[k][i] = Σ_s part[(s·K + k)·CoR + i] in split order (deterministic split-K fold)
 void tn_fold(const float* part, float* dw, long dw_cs, int K, int splitk, long CoR, hipStream_t s);
-// 3x3 stride-1 wgrad with LDS halo reuse on pre-split planes (conv_wgrad_halo.hip): false = the
-// shape is outside its contract (conv_tn_pl serves it)
-bool conv_wgrad_halo_supported(const ConvTNParams& p);
-bool conv_wgrad_halo(ConvTNParams p, int K, hipStream_t s);
-int conv_wgrad_halo_splitk(int Co, int C, int M);
-void conv_wgrad_halo_set_mode(int m);  // -1 shape rule, 0 never, 1 whenever supported
 int conv_tn_f32_num_variants();
 int conv_tn_f32_splitk(int K, int Co, int R, int M, int gco, int gc, int variant);
 

@@ -6,6 +6,8 @@
 
 #include "common.h"
 #include "dls.h"
+#include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -1028,4 +1030,32 @@ void synth_images(const int64_t* idx, long n, long npix, int C, int Cout, const 
   if (total == 0) return;
   hipLaunchKernelGGL(synth_images_kernel, dim3((unsigned)std::min<long>(cdiv(total, 256), 65536)), dim3(256), 0, s,
                      idx, n, npix, C, Cout, source, proto, salt, sqrt6, noise, out);
+}
+
+// ------------------------------------------------------------------ host launch knobs (dls.h)
+int g_opt_attn_mfma = kOptUnset, g_opt_f32_smallk = kOptUnset, g_opt_conv_gl = kOptUnset;
+int g_opt_pl_min_wg = kOptUnset, g_opt_tn_kref = kOptUnset, g_opt_bn_coef_groups = kOptUnset;
+
+int native_option(int& slot, const char* env, int dflt) {
+  if (slot == kOptUnset) {
+    const char* e = getenv(env);
+    slot = e ? atoi(e) : dflt;
+  }
+  return slot;
+}
+
+bool set_native_option(const char* name, int value) {
+  struct Entry {
+    const char* name;
+    int* slot;
+  };
+  const Entry table[] = {{"attn_mfma", &g_opt_attn_mfma},   {"f32_smallk", &g_opt_f32_smallk},
+                         {"conv_gl", &g_opt_conv_gl},       {"pl_min_wg", &g_opt_pl_min_wg},
+                         {"tn_kref", &g_opt_tn_kref},       {"bn_coef_groups", &g_opt_bn_coef_groups}};
+  for (const Entry& t : table)
+    if (strcmp(t.name, name) == 0) {
+      *t.slot = value;
+      return true;
+    }
+  return false;
 }

@@ -8,7 +8,11 @@
 
 // acc[TM][TN]: the wave's 32x32 accumulator tiles (v_mfma_f32_32x32x16 C layout); smem: ≥
 // NW·32·SW floats, free (the caller has retired every read of the main-loop images)
-template <int TM, int TN, int NW>
+// PF > 0: the global operands of the store loop (second gradient, BN input x, ReLU mask) are
+// fetched PF column quads ahead of use; PF < 0: the rolled loop, each quad's operands loaded at
+// its turn. The prefetch costs up to 9·PF VGPRs: a kernel opts in only where that keeps its
+// occupancy and spills nothing (-Rpass-analysis=kernel-resource-usage; conv_halo.hip).
+template <int TM, int TN, int NW, int PF = -1>
 __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&acc)[TM][TN], unsigned char* smem,
                                                 int client, int m0, int n0, int wm0, int wn0, int wid, int lane) {
   constexpr int SW = TN * 32 + 4;  // slab row (fp32), 16-B aligned
@@ -47,10 +51,12 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
       brs = *reinterpret_cast<const float4*>(p.bnb_rstd + (long)client * p.N + n);
     }
   }
-  constexpr int QPL = 4 * TN, NB = QPL < 4 ? QPL : 4;  // column quads per lane per row group, per batch
+  constexpr int QPL = 4 * TN;  // column quads per lane per 32-row group
   const float* bx_base = bnb ? p.bnb_x + (long)client * p.M * p.bnb_xld : nullptr;
   const unsigned char* bm_base = (bnb && p.bnb_mask) ? p.bnb_mask + (long)client * p.M * (p.N >> 3) : nullptr;
   const float* by_base = (bnb && p.bnb_y) ? p.bnb_y + (long)client * p.y_cs : nullptr;
+  // an invalid quad loads from its tensor's client base (always mapped) and is zeroed after: no
+  // branch around the load, so the loads of two quads issue back to back
   auto ld4 = [](const float* base, long off, bool ok) {
     const float4 v = *reinterpret_cast<const float4*>(ok ? base + off : base);
     return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -96,105 +102,186 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
         }
       }
     }
-    // 16-B column quads: lane l always owns columns cc = (l % Q)·4 of rows l / Q + t·(64 / Q).
-    // Every global operand of a batch of quads (second gradient, gate, BN input x and its ReLU
-    // mask) is fetched up front — an invalid quad loads from its tensor's client base (always
-    // mapped) and is zeroed after, so no branch or per-quad wait separates the loads — and the
-    // first batch is in flight while the accumulators go through the slab. (A rolled loop of
-    // dependent loads per quad serialised ≈4·TM L2/HBM round trips per wave after the main
-    // loop: the l1 dgrad with acc + BN partials ran at 28 % MFMA-busy vs 44 % forward.)
-    const int cc = (lane % Q) * 4, n = n0 + wn0 + cc;
-    float4 av[NB], gv[NB], xv[NB];
-    uint32_t mv[NB];
-    auto issue = [&](int t0) {
-#pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        const int m = m0 + wm0 + i * 32 + lane / Q + (t0 + t) * (64 / Q);
+    float4 bs0 = make_float4(0.f, 0.f, 0.f, 0.f), bs1 = bs0;
+    if constexpr (PF > 0) {
+      // 16-B column quads: lane l always owns columns cc = (l % Q)·4 of rows l / Q + t·(64 / Q). The
+      // global operands of a quad (second gradient, BN input x and its ReLU mask) are fetched PF
+      // quads ahead of their use — the first ones while the accumulators go through the slab — and
+      // always together: a rolled load → wait → store loop serialised ≈3 L2/HBM round trips per
+      // quad per wave (l1 dgrad with acc + BN partials: +34 % over the plain dgrad,
+      // bench/epilogue_bench.py). (All quads in flight pushed the halo kernels from 4 to 2 waves
+      // per SIMD.)
+      const int cc = (lane % Q) * 4, n = n0 + wn0 + cc;
+      constexpr int NS = PF > 0 ? PF : 1;  // operand slots
+      float4 av[NS], xv[NS];
+      uint32_t mv[NS];
+      auto issue = [&](int t) {  // (t: compile-time after unrolling; slot t % NS)
+        const int m = m0 + wm0 + i * 32 + lane / Q + t * (64 / Q);
         const bool ok = n < p.N && m < p.M;
         const long row = row_of(m);
-        if (accp) av[t] = ld4(accp, (p.acc_compact ? (long)m : row) * p.ldy + n, ok);
-        if (gatep) gv[t] = ld4(gatep, row * p.ldy + n, ok);
+        if (accp) av[t % NS] = ld4(accp, (p.acc_compact ? (long)m : row) * p.ldy + n, ok);
         if (bnb) {
           const bool okb = ok && m < bnb_rows;
-          xv[t] = ld4(bx_base, row * p.bnb_xld + n, okb);
+          xv[t % NS] = ld4(bx_base, row * p.bnb_xld + n, okb);
           if (bm_base) {
             const uint32_t mb = *(okb ? bm_base + (long)m * (p.N >> 3) + (n >> 3) : bm_base);
-            mv[t] = okb ? (mb >> (n & 4)) : 0u;
+            mv[t % NS] = okb ? (mb >> (n & 4)) : 0u;
           } else if (by_base) {
             const float4 yv = ld4(by_base, row * p.ldy + n, okb);
-            mv[t] = (yv.x > 0.f ? 1u : 0u) | (yv.y > 0.f ? 2u : 0u) | (yv.z > 0.f ? 4u : 0u) | (yv.w > 0.f ? 8u : 0u);
+            mv[t % NS] = (yv.x > 0.f ? 1u : 0u) | (yv.y > 0.f ? 2u : 0u) | (yv.z > 0.f ? 4u : 0u) | (yv.w > 0.f ? 8u : 0u);
           } else {
-            mv[t] = okb ? 0xFu : 0u;
+            mv[t % NS] = okb ? 0xFu : 0u;
           }
         }
+      };
+      if (vec_ok) {
+#pragma unroll
+        for (int t = 0; t < PF && t < QPL; ++t) issue(t);
       }
-    };
-    if (vec_ok) issue(0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
+      for (int j = 0; j < TN; ++j) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        float v = acc[i][j][e] + bvals[j];
-        if (p.relu) v = fmaxf(v, 0.f);
-        v *= oscale;
-        if (drop) {
-          const int rr = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-          if (!drop_keep(dseed, m0 + wm0 + i * 32 + rr, p.N, n0 + wn0 + j * 32 + (lane & 31), p.drop_p)) v = 0.f;
+        for (int e = 0; e < 16; ++e) {
+          float v = acc[i][j][e] + bvals[j];
+          if (p.relu) v = fmaxf(v, 0.f);
+          v *= oscale;
+          if (drop) {
+            const int rr = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            if (!drop_keep(dseed, m0 + wm0 + i * 32 + rr, p.N, n0 + wn0 + j * 32 + (lane & 31), p.drop_p)) v = 0.f;
+          }
+          slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = v;
         }
-        slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = v;
       }
-    }
-    __syncthreads();
-    float4 bs0 = make_float4(0.f, 0.f, 0.f, 0.f), bs1 = bs0;
-    if (vec_ok) {
+      // LDS barrier only: __syncthreads()'s fence would also drain the operand loads in flight
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      if (vec_ok) {
 #pragma unroll
-      for (int t0 = 0; t0 < QPL; t0 += NB) {
-        if (t0) issue(t0);
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          const int r = lane / Q + (t0 + t) * (64 / Q);
+        for (int t = 0; t < QPL; ++t) {
+          const int r = lane / Q + t * (64 / Q);
           const int m = m0 + wm0 + i * 32 + r;
+          const long row = row_of(m);
           float4 v = *reinterpret_cast<const float4*>(slab + r * SW + cc);
           if (gatep) {
-            v.x = gv[t].x > 0.f ? v.x : 0.f;
-            v.y = gv[t].y > 0.f ? v.y : 0.f;
-            v.z = gv[t].z > 0.f ? v.z : 0.f;
-            v.w = gv[t].w > 0.f ? v.w : 0.f;
+            const float4 gv = ld4(gatep, row * p.ldy + n, n < p.N && m < p.M);
+            v.x = gv.x > 0.f ? v.x : 0.f;
+            v.y = gv.y > 0.f ? v.y : 0.f;
+            v.z = gv.z > 0.f ? v.z : 0.f;
+            v.w = gv.w > 0.f ? v.w : 0.f;
           }
           if (accp) {
-            v.x += av[t].x;
-            v.y += av[t].y;
-            v.z += av[t].z;
-            v.w += av[t].w;
+            v.x += av[t % NS].x;
+            v.y += av[t % NS].y;
+            v.z += av[t % NS].z;
+            v.w += av[t % NS].w;
           }
-          if (n < p.N && m < p.M) *reinterpret_cast<float4*>(y + row_of(m) * p.ldy + n) = v;
+          if (n < p.N && m < p.M) *reinterpret_cast<float4*>(y + row * p.ldy + n) = v;
           if (bnb) {  // ĝ = dX·relu', x̂ = (x − μ)·rstd of the BN whose dY this is (none past bnb_rows)
-            const uint32_t mb = mv[t];
+            const uint32_t mb = mv[t % NS];
             const float g0 = (mb & 1u) ? v.x : 0.f, g1 = (mb & 2u) ? v.y : 0.f;
             const float g2 = (mb & 4u) ? v.z : 0.f, g3 = (mb & 8u) ? v.w : 0.f;
             bs0.x += g0;
             bs0.y += g1;
             bs0.z += g2;
             bs0.w += g3;
-            bs1.x = fmaf(g0, (xv[t].x - bmu.x) * brs.x, bs1.x);
-            bs1.y = fmaf(g1, (xv[t].y - bmu.y) * brs.y, bs1.y);
-            bs1.z = fmaf(g2, (xv[t].z - bmu.z) * brs.z, bs1.z);
-            bs1.w = fmaf(g3, (xv[t].w - bmu.w) * brs.w, bs1.w);
+            bs1.x = fmaf(g0, (xv[t % NS].x - bmu.x) * brs.x, bs1.x);
+            bs1.y = fmaf(g1, (xv[t % NS].y - bmu.y) * brs.y, bs1.y);
+            bs1.z = fmaf(g2, (xv[t % NS].z - bmu.z) * brs.z, bs1.z);
+            bs1.w = fmaf(g3, (xv[t % NS].w - bmu.w) * brs.w, bs1.w);
+          }
+          if (PF > 0 && t + PF < QPL) issue(t + PF);
+        }
+      } else {  // scalar columns (N or the row stride not a multiple of 4; no BN partials here)
+        for (int qd = lane; qd < 32 * TN * 8; qd += 64) {
+          const int r = qd / (TN * 8), c4 = (qd % (TN * 8)) * 4;
+          const int m = m0 + wm0 + i * 32 + r, nn = n0 + wn0 + c4;
+          if (m >= p.M || nn >= p.N) continue;
+          const long row = row_of(m);
+          const long arow = p.acc_compact ? (long)m : row;  // (compact acc: the class-grid row)
+          for (int t2 = 0; t2 < 4 && nn + t2 < p.N; ++t2) {
+            float o = slab[r * SW + c4 + t2];
+            if (gatep && !(gatep[row * p.ldy + nn + t2] > 0.f)) o = 0.f;
+            if (accp) o += accp[arow * p.ldy + nn + t2];
+            y[row * p.ldy + nn + t2] = o;
           }
         }
       }
-    } else {  // scalar columns (N or the row stride not a multiple of 4; no BN partials here)
+    } else {  // PF < 0: the rolled store loop (kernels without VGPRs to spare)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float v = acc[i][j][e] + bvals[j];
+          if (p.relu) v = fmaxf(v, 0.f);
+          v *= oscale;
+          if (drop) {
+            const int rr = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            if (!drop_keep(dseed, m0 + wm0 + i * 32 + rr, p.N, n0 + wn0 + j * 32 + (lane & 31), p.drop_p)) v = 0.f;
+          }
+          slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * SW + j * 32 + (lane & 31)] = v;
+        }
+      }
+      __syncthreads();
       for (int qd = lane; qd < 32 * TN * 8; qd += 64) {
-        const int r = qd / (TN * 8), c4 = (qd % (TN * 8)) * 4;
-        const int m = m0 + wm0 + i * 32 + r, nn = n0 + wn0 + c4;
-        if (m >= p.M || nn >= p.N) continue;
-        const long row = row_of(m);
+        const int r = qd / (TN * 8), cc = (qd % (TN * 8)) * 4;
+        const int m = m0 + wm0 + i * 32 + r, n = n0 + wn0 + cc;
+        if (m >= p.M || n >= p.N) continue;
+        long row = m;
+        if (p.out_s > 1) {
+          const uint32_t b = fdiv(m, p.fd_ohw);
+          const uint32_t rem = m - b * p.OH * p.OW;
+          const uint32_t oh = fdiv(rem, p.fd_ow);
+          const uint32_t ow = rem - oh * p.OW;
+          row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
+        }
+        float* dst = y + row * p.ldy + n;
+        const float* src = slab + r * SW + cc;
         const long arow = p.acc_compact ? (long)m : row;  // (compact acc: the class-grid row)
-        for (int t2 = 0; t2 < 4 && nn + t2 < p.N; ++t2) {
-          float o = slab[r * SW + c4 + t2];
-          if (gatep && !(gatep[row * p.ldy + nn + t2] > 0.f)) o = 0.f;
-          if (accp) o += accp[arow * p.ldy + nn + t2];
-          y[row * p.ldy + nn + t2] = o;
+        if (vec_ok && n + 4 <= p.N) {
+          float4 v = *reinterpret_cast<const float4*>(src);
+          if (gatep) {
+            const float4 gv = *reinterpret_cast<const float4*>(gatep + row * p.ldy + n);
+            v.x = gv.x > 0.f ? v.x : 0.f;
+            v.y = gv.y > 0.f ? v.y : 0.f;
+            v.z = gv.z > 0.f ? v.z : 0.f;
+            v.w = gv.w > 0.f ? v.w : 0.f;
+          }
+          if (accp) {
+            const float4 av = *reinterpret_cast<const float4*>(accp + arow * p.ldy + n);
+            v.x += av.x;
+            v.y += av.y;
+            v.z += av.z;
+            v.w += av.w;
+          }
+          *reinterpret_cast<float4*>(dst) = v;
+          if (bnb && m < bnb_rows) {  // ĝ = dX·relu', x̂ = (x − μ)·rstd of the BN whose dY this is
+            const float4 xv =
+                *reinterpret_cast<const float4*>(p.bnb_x + ((long)client * p.M + row) * p.bnb_xld + n);
+            uint32_t mb = 0xFu;
+            if (p.bnb_mask) {
+              mb = p.bnb_mask[((long)client * p.M + m) * (p.N >> 3) + (n >> 3)] >> (n & 4);
+            } else if (p.bnb_y) {
+              const float4 yv = *reinterpret_cast<const float4*>(p.bnb_y + (long)client * p.y_cs + row * p.ldy + n);
+              mb = (yv.x > 0.f ? 1u : 0u) | (yv.y > 0.f ? 2u : 0u) | (yv.z > 0.f ? 4u : 0u) | (yv.w > 0.f ? 8u : 0u);
+            }
+            const float g0 = (mb & 1u) ? v.x : 0.f, g1 = (mb & 2u) ? v.y : 0.f;
+            const float g2 = (mb & 4u) ? v.z : 0.f, g3 = (mb & 8u) ? v.w : 0.f;
+            bs0.x += g0;
+            bs0.y += g1;
+            bs0.z += g2;
+            bs0.w += g3;
+            bs1.x = fmaf(g0, (xv.x - bmu.x) * brs.x, bs1.x);
+            bs1.y = fmaf(g1, (xv.y - bmu.y) * brs.y, bs1.y);
+            bs1.z = fmaf(g2, (xv.z - bmu.z) * brs.z, bs1.z);
+            bs1.w = fmaf(g3, (xv.w - bmu.w) * brs.w, bs1.w);
+          }
+        } else {
+          for (int t2 = 0; t2 < 4 && n + t2 < p.N; ++t2) {
+            float o = src[t2];
+            if (gatep && !(gatep[row * p.ldy + n + t2] > 0.f)) o = 0.f;
+            if (accp) o += accp[arow * p.ldy + n + t2];
+            dst[t2] = o;
+          }
         }
       }
     }

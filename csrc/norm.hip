@@ -223,11 +223,7 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
 // the other sub-cohort stream's GEMM workgroups occupy them
 constexpr int COEF_GROUPS = 32;  // (upper bound: shared-memory sizing)
 static int coef_groups() {
-  static const int g = [] {
-    const char* e = getenv("DLS_BN_COEF_GROUPS");
-    return (e && atoi(e) == 32) ? 32 : 8;
-  }();
-  return g;
+  return native_option(g_opt_bn_coef_groups, "DLS_BN_COEF_GROUPS", 8) == 32 ? 32 : 8;
 }
 
 // First stage for the conv-epilogue statistics, which arrive as one partial per 32 GEMM rows

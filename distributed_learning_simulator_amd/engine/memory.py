@@ -18,7 +18,6 @@ wave; ResNet-50/ImageNet at batch 128 costs ≈20 GB of activations and runs in 
 from __future__ import annotations
 
 import math
-import os
 import threading
 
 import torch
@@ -40,7 +39,7 @@ def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:
         n += 4 * P
     if compute_dtype != torch.float32:
         n += torch.tensor([], dtype=compute_dtype).element_size() * P
-    elif optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "1") == "1":
+    elif optimizer.lower() != "adam":
         n += 4 * P  # pre-split (hi, lo) bf16 weight planes of the fp32 GEMMs (CohortBuffers.split)
     return n
 

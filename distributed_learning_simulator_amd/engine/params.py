@@ -19,7 +19,6 @@ Parameter order/naming follows PyTorch `state_dict` naming of the equivalent nn.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -151,12 +150,13 @@ class CohortBuffers:
         # fp32 compute on the GPU: every row's weights also as (bf16 hi, bf16 lo) planes, written
         # by the SGD kernel with θ. They are the B operand of the split-plane GEMMs
         # (csrc/conv_pl.hip: LDS-DMA loads, no split VALU), whose A operand — activation / dY
-        # planes — the BatchNorms write (ops.functional planes). DLS_WSPLIT=0 disables both
-        # (SGD only: the Adam kernel does not write planes)
+        # planes — the BatchNorms write (ops.functional planes). SGD only: the Adam kernel does
+        # not write planes. (Pre-split weights alone measured 0-5 % faster GEMMs but a slower
+        # round in round 2; with the activation planes they carry the LDS-DMA kernels.)
         self.split = (
             torch.zeros((capacity, 2, P), dtype=torch.bfloat16, device=device)
             if (compute_dtype == torch.float32 and torch.device(device).type == "cuda"
-                and optimizer.lower() != "adam" and os.environ.get("DLS_WSPLIT", "1") == "1") else None
+                and optimizer.lower() != "adam") else None
         )
 
     @property

@@ -24,7 +24,6 @@ from __future__ import annotations
 import contextlib
 import gc
 import math
-import os
 from dataclasses import dataclass
 
 import torch
@@ -34,6 +33,7 @@ from ..ops import fl
 from ..ops import functional as Fn
 from ..utils.tracing import trace
 from .hooks import ExecutorHookPoint, HookRegistry, StopExecutingException
+from ..options import OPTIONS
 from .memory import DEVICE_LOCK
 from .params import BoundParams, CohortBuffers
 
@@ -128,14 +128,14 @@ class CohortTrainer:
         self.layout = model.layout
         self.buffers = CohortBuffers(self.layout, capacity, self.device, compute_dtype, hyper.optimizer_name)
         self.debug = False  # `debug` config: per-step NaN/Inf scan (synchronises every step)
-        self.num_streams = int(os.environ.get("DLS_STREAMS", "2"))  # concurrent sub-cohorts on GPU
+        self.num_streams = int(OPTIONS.streams)  # concurrent sub-cohorts on GPU
         self._stream_pool: list = []
-        # HIP-graph replay of whole training steps (DLS_GRAPHS=0 disables): a ResNet-18 step is
+        # HIP-graph replay of whole training steps (OPTIONS.graphs): a ResNet-18 step is
         # ≈400 launches per sub-cohort, which at the 8-GPU per-rank load (13 clients) costs more
         # host time than the GPU needs to run them
-        self.use_graphs = os.environ.get("DLS_GRAPHS", "1") != "0"
+        self.use_graphs = bool(OPTIONS.graphs)
         self._graphs: dict = {}
-        self.max_graphs = int(os.environ.get("DLS_MAX_GRAPHS", "2"))
+        self.max_graphs = int(OPTIONS.max_graphs)
         # pre-split weight planes (buffers.split) are read by the convolutions only inside a
         # graphed training run: refreshed from θ when it starts and after epoch hooks, kept
         # current by the SGD kernel in between (no other θ writer runs there)

@@ -9,11 +9,11 @@ DenseNet-40 (k=12) 1,059,298 (CIFAR-10); Transformer layer (d=100, ff=2048) 452,
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 from ..engine.params import ParamLayout
+from ..options import OPTIONS
 from ..ops import functional as Fn
 from .layers import (AvgPool, BatchNorm, Conv2d, Embedding, conv_bn, Flatten, LayerNorm, Linear,
                      MaxPool, Module, ReLU, RunCtx, Seq)
@@ -87,7 +87,6 @@ class LeNet5Net(Module):
 
 
 # ------------------------------------------------------------------------- ResNets
-_BLOCK_OUT_PLANES = os.environ.get("DLS_BLOCK_OUT_PLANES", "1") != "0"
 
 def _residual_link(block, x, ctx):
     """Blocks in training route the shortcut's gradient of the block input through conv1's dgrad
@@ -191,12 +190,12 @@ class ResNetNet(Module):
         # downsample block follows (its convs read planes; its shortcut is a conv too), fp32 only
         # before the pooling head, both otherwise (planes for the convs, fp32 for the identity
         # shortcut's residual add)
-        # (DLS_BLOCK_OUT_PLANES=0: every block output in both forms, the A/B switch)
+        # (OPTIONS.block_out_planes = False: every block output in both forms, the A/B switch)
         blocks = [b for s in self.stages for b in s.children]
         for i, b in enumerate(blocks):
             nxt = blocks[i + 1] if i + 1 < len(blocks) else None
             op = 0 if nxt is None else 2 if nxt.down is not None else 1
-            x = b.forward(x, ctx, out_planes=op if _BLOCK_OUT_PLANES else 1)
+            x = b.forward(x, ctx, out_planes=op if OPTIONS.block_out_planes else 1)
         x = Fn.global_avg_pool(x)
         return self.fc.forward(x, ctx)
 

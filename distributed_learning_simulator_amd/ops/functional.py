@@ -10,10 +10,9 @@ even when the op's activation input does not need a gradient (e.g. the stem conv
 
 from __future__ import annotations
 
-import os
-
 import torch
 
+from ..options import OPTIONS
 from . import backend, ref
 
 
@@ -44,16 +43,8 @@ class ResidualLink:
         self.receiver_stride = 1  # stride of the receiving conv (set by its forward)
 
 
-# DLS_BN_EPILOGUE_STATS=0: BatchNorm computes its statistics in its own pass (A/B switch)
-EPILOGUE_BN_STATS = os.environ.get("DLS_BN_EPILOGUE_STATS", "1") != "0"
-# DLS_DENSE_STATS_CACHE=1: DenseNet blocks compute each channel's batch statistics once (see
-# _DenseBlock.forward)
-DENSE_STATS_CACHE = os.environ.get("DLS_DENSE_STATS_CACHE", "0") == "1"
-# DLS_DENSE_BN_PARTS=1: DenseNet block backward takes each BN's partial sums from the growth conv's
-# dgrad epilogue (off by default: the 100-client DenseNet-40 round measured 14.57 s with it vs
-# 14.36 s without — the strided x / y-gate reads in the non-plane dgrad's epilogue cost more than
-# the reduction pass they replace)
-DENSE_BN_PARTS = os.environ.get("DLS_DENSE_BN_PARTS", "0") == "1"
+# A/B switches (BN statistics from the conv epilogue, BN backward partials, split planes, ...)
+# live in options.OPTIONS and are read when an op runs
 
 
 class BNStats:
@@ -73,8 +64,6 @@ class BNStats:
         self.dy_planes_ok = False
 
 
-# DLS_BN_BWD_PARTS=0: BatchNorm backward always runs its own reduction pass (A/B switch)
-BN_BWD_PARTS = os.environ.get("DLS_BN_BWD_PARTS", "1") != "0"
 # BN backward passes that used a dgrad's partials ("used"), whose consumer wrote none (a strided
 # or absent conv: "none"), or whose dY was not that dgrad's output ("fallback"): tests, reports
 bn_bwd_parts_count = {"used": 0, "none": 0, "fallback": 0}
@@ -102,10 +91,8 @@ class BNBwdLink:
 # Split-plane operands (csrc/conv_pl.hip). A tensor produced together with its bf16 (hi, lo)
 # planes carries them as attribute `_dls_planes` ([K, 2, *shape[1:]], ops.hip.planes_buffer
 # layout); `_dls_planes_only` marks a tensor whose fp32 bytes ARE those planes (the producer
-# wrote nothing else) — only a planes-reading GEMM may consume it. DLS_PLANES=0 disables.
-PLANES = os.environ.get("DLS_PLANES", "1") != "0"
-# DLS_LN_PLANES=0: LayerNorm outputs carry no split planes (A/B of the Transformer's plane linears)
-LN_PLANES = os.environ.get("DLS_LN_PLANES", "1") != "0"
+# wrote nothing else) — only a planes-reading GEMM may consume it. OPTIONS.planes = False
+# disables them (OPTIONS.ln_planes: the LayerNorm ones).
 
 
 def _planes_of(t):
@@ -155,7 +142,7 @@ class _Conv(torch.autograd.Function):
         big = be is not ref and max(x[0].numel(), y_numel) * x.element_size() >= (1 << 31)
         if stats is not None:
             stats.dy_planes_ok = stats.dy_planes_ok and be.planes_fit(y_numel)
-        if stats is not None and be is not ref and x.dtype == torch.float32 and EPILOGUE_BN_STATS and not big:
+        if stats is not None and be is not ref and x.dtype == torch.float32 and OPTIONS.bn_epilogue_stats and not big:
             stats.part = torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
                                      device=x.device)
             y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid,
@@ -169,7 +156,7 @@ class _Conv(torch.autograd.Function):
         # rebuilt on the way, which drops the _dls_planes attributes) must fail, not be read as fp32
         ctx.expect_dy_planes = stats is not None and stats.dy_planes_ok
         ctx.x_planes_only = bool(getattr(x, "_dls_planes_only", False))
-        bnb = getattr(x, "_dls_bnb", None) if BN_BWD_PARTS else None
+        bnb = getattr(x, "_dls_bnb", None) if OPTIONS.bn_bwd_parts else None
         # (the dgrad writes the partials only in one launch: a dY or dX window past 2 GiB runs
         # batch-chunked, e.g. a 64 -> 256 1x1 conv whose output alone crosses it)
         if bnb is not None and not (be is not ref and donor is None and x.shape[-1] == ci and not big
@@ -408,7 +395,7 @@ class _BN(torch.autograd.Function):
             y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
         else:  # native: 1-bit ReLU mask so the backward need not re-read y
             pre = stats.part if stats is not None else None
-            planes = planes if (PLANES and x.dtype == torch.float32 and x.is_contiguous()
+            planes = planes if (OPTIONS.planes and x.dtype == torch.float32 and x.is_contiguous()
                                 and be.planes_fit(x[0].numel())) else 0
             # (inference passes — evaluation, GTG utilities — write no ReLU mask: no backward reads
             # it. Autograd is off inside Function.forward, so ask which inputs need a gradient)
@@ -420,7 +407,7 @@ class _BN(torch.autograd.Function):
                 yp = out[-1]
             if stats is not None:
                 stats.part = None
-            if (wm and BN_BWD_PARTS and x.dtype == torch.float32 and x3.is_contiguous()
+            if (wm and OPTIONS.bn_bwd_parts and x.dtype == torch.float32 and x3.is_contiguous()
                     and (mask is not None or not relu)):
                 vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
                 bnb = BNBwdLink(x3, mask, mean, rstd, vr)
@@ -453,7 +440,7 @@ class _BN(torch.autograd.Function):
         else:
             _require_fp32(dy, "batch_norm backward")
             # the producing conv reads dX as split planes: write only those
-            dxm = 2 if (ctx.stats is not None and ctx.stats.dy_planes_ok and PLANES) else 0
+            dxm = 2 if (ctx.stats is not None and ctx.stats.dy_planes_ok and OPTIONS.planes) else 0
             # partial sums from the consuming conv's dgrad epilogue, if dy is exactly its output
             pre = None
             bnb = ctx.bnb
@@ -494,7 +481,7 @@ class _LN(torch.autograd.Function):
     def forward(ctx, x, token, gamma, beta, ggamma, gbeta, planes=False):
         be = _be(x)
         yp = None
-        if (planes and PLANES and LN_PLANES and be is not ref and x.dtype == torch.float32
+        if (planes and OPTIONS.planes and OPTIONS.ln_planes and be is not ref and x.dtype == torch.float32
                 and be.planes_fit(x[0].numel())):
             y, mean, rstd, yp = be.ln_fwd(x, gamma, beta, planes=True)
         else:
@@ -771,10 +758,10 @@ class _DenseBlock(torch.autograd.Function):
         # channel (only γ/β differ), so they are computed ONCE per channel: the block input's in
         # one pass, each new slice's from its conv epilogue (Σ / Σ² partials) — instead of a
         # statistics pass over the whole growing prefix in every layer (O(L²) → O(L) bytes).
-        # (DLS_DENSE_STATS_CACHE=1; off by default: alternating A/B on the 100-client DenseNet-40
+        # (OPTIONS.dense_stats_cache; off by default: alternating A/B on the 100-client DenseNet-40
         # round gave 13.47 s with the cache vs 13.43 s without — the per-layer stack / cast / sum
         # launches cost what the skipped statistics passes save)
-        cache = native and x.dtype == torch.float32 and EPILOGUE_BN_STATS and DENSE_STATS_CACHE
+        cache = native and x.dtype == torch.float32 and OPTIONS.bn_epilogue_stats and OPTIONS.dense_stats_cache
         if cache:
             R = B * H * W
             S = torch.empty((K, 2, Ct), dtype=torch.float64, device=x.device)  # Σx, Σx² per channel
@@ -820,7 +807,6 @@ class _DenseBlock(torch.autograd.Function):
         K, B, H, W, Ct = F.shape
         g, c0 = ctx.growth, ctx.c0
         dF = dF_out.contiguous().clone() if native else dF_out.float().clone()
-        vr32 = ctx.valid_rows.to(torch.int32).contiguous() if ctx.valid_rows is not None else None
         for i in range(len(ctx.layers) - 1, -1, -1):
             lp = ctx.layers[i]
             y, mean, rstd, mask = ctx.saved[i]
@@ -831,18 +817,11 @@ class _DenseBlock(torch.autograd.Function):
             if native:
                 if lp.gw is not None:
                     be.conv_wgrad(d_out, yv, lp.gw, 1, 1)
-                # the dgrad's epilogue writes this BN's backward partial sums (Fn.BNBwdLink): x is
-                # the block buffer's channel prefix, the ReLU gate the bit mask or y
-                part = None
-                kw = {}
-                if (BN_BWD_PARTS and DENSE_BN_PARTS and F.dtype == torch.float32
-                        and be.bn_bwd_parts_ok((K, B, H, W, ci), 1, F.dtype)):
-                    part = torch.empty((K, be.conv_stats_parts(B * H * W), 2, ci), dtype=torch.float32,
-                                       device=F.device)
-                    kw["bnb"] = (part, xi, mask, mean, rstd, vr32, y if mask is None else None)
-                dy = be.conv_dgrad(d_out, lp.w, (H, W), 1, 1, **kw)
+                # (BN partials from this dgrad's epilogue measured slower here: 14.57 vs 14.36 s per
+                # 100-client round — the strided x / gate reads cost more than the pass they replace)
+                dy = be.conv_dgrad(d_out, lp.w, (H, W), 1, 1)
                 be.bn_bwd(dy.view(K, -1, ci), xi, y, mean, rstd, lp.gamma, ctx.valid_rows, True, lp.ggamma, lp.gbeta,
-                          False, relu_mask=mask, dx_out=dF[..., :ci].reshape(K, -1, ci), pre_part=part)
+                          False, relu_mask=mask, dx_out=dF[..., :ci].reshape(K, -1, ci))
             else:
                 d_out = d_out.contiguous()
                 if lp.gw is not None:

@@ -14,6 +14,7 @@ import threading
 
 import torch
 
+from ..options import OPTIONS
 from . import ref
 
 try:
@@ -124,17 +125,16 @@ def _workspace(numel: int, device) -> torch.Tensor:
 
 
 _ctr_cache: dict = {}
-# fused BN coefficients (csrc/norm.hip, last-arriver stage) instead of the separate coefficient
-# kernel. Off by default: measured SLOWER on MI355X — every workgroup's agent-scope release
-# (buffer_wbl2) writes back its XCD's dirty L2 lines: FedAvg ResNet-18 round 2.45 -> 2.91 s at
-# 100 clients, 462 -> 529 ms at the 8-rank per-rank load (DLS_BN_FUSED_COEF=1 to A/B)
-bn_fused_coef = os.environ.get("DLS_BN_FUSED_COEF", "0") == "1"
+# OPTIONS.bn_fused_coef: fused BN coefficients (csrc/norm.hip, last-arriver stage) instead of the
+# separate coefficient kernel. Off by default: measured SLOWER on MI355X — every workgroup's
+# agent-scope release (buffer_wbl2) writes back its XCD's dirty L2 lines: FedAvg ResNet-18 round
+# 2.45 -> 2.91 s at 100 clients, 462 -> 529 ms at the 8-rank per-rank load
 
 
 def _bn_counters(K: int, device):
     """Per-(device, stream) zeroed ticket counters of the fused BN coefficient stage; every
     launch leaves them zero again. Sized once, generously, so graph capture never allocates."""
-    if not bn_fused_coef:
+    if not OPTIONS.bn_fused_coef:
         return None
     key = (device, torch.cuda.current_stream().cuda_stream)
     t = _ctr_cache.get(key)
@@ -361,8 +361,7 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
 
 
 # fp32 weight gradients: split-K partial slabs folded in split order (bitwise-reproducible, no
-# atomics) — DLS_DETERMINISTIC=0 restores fp32 atomics into pre-zeroed rows (A/B)
-deterministic = os.environ.get("DLS_DETERMINISTIC", "1") != "0"
+# atomics) — OPTIONS.deterministic = False restores fp32 atomics into pre-zeroed rows (A/B)
 _part_cache: dict = {}
 
 
@@ -388,12 +387,9 @@ def _tn_launch(dy, x, gw, dy_cs, x_cs, B, H, W, C, OH, OW, KH, KW, stride, pad, 
         xp, x_cs, x_lo = _planes_args(x_planes, x)
         planes_launches["wgrad"] += 1
     splitk = _C.conv_tn_splitk(K, Co, R, M, C, tv, f32, ldy, ldx, int(planes))
-    if planes and tv < 0 and KH == 3 and KW == 3 and stride == 1 and pad == 1 and W in (8, 16, 32):
-        # the halo wgrad may serve it (csrc/conv_wgrad_halo.hip): slabs for either split
-        splitk = max(splitk, _C.conv_wgrad_halo_splitk(Co, C, M))
     part = NULL
     if splitk > 1:
-        if f32 and (deterministic or planes):
+        if f32 and (OPTIONS.deterministic or planes):
             part = _p(_tn_part(splitk * K * Co * R, gw.device))
         else:
             gw.zero_()
@@ -435,7 +431,7 @@ def conv_wgrad(dy, x, gw, stride: int, pad: int, dy_planes=None, x_planes=None):
 def _col_sum(x, out, K: int, rows: int, C: int):
     """out[k, c] = Σ_rows x[k, row, c] (fp32, into a strided gradient view): partials folded in
     order when deterministic, else fp32 atomics into the zeroed view."""
-    if deterministic:
+    if OPTIONS.deterministic:
         ws = _tn_part(_C.col_sum_workspace_floats(K, rows, C), x.device)
         _C.col_sum(_p(x), _p(out), out.stride(0), K, rows, C, _f32(x), _s(), _p(ws))
     else:
@@ -661,7 +657,7 @@ def ln_bwd(dy, x, mean, rstd, gamma):
     g_cs, rep = _client_view(gamma, K)
     rpc = x.numel() // (K * C)
     dx = torch.empty_like(x)
-    if deterministic:
+    if OPTIONS.deterministic:
         dgamma = torch.empty((K, C), dtype=torch.float32, device=x.device)
         dbeta = torch.empty((K, C), dtype=torch.float32, device=x.device)
         ws = _p(_tn_part(_C.ln_workspace_floats(K, rpc, C), x.device))
@@ -734,7 +730,7 @@ def ce_fwd_bwd(logits, labels, valid=None):
     loss = torch.empty(K, dtype=torch.float32, device=logits.device)
     correct = torch.empty(K, dtype=torch.float32, device=logits.device)
     dlogits = torch.empty_like(logits)
-    rowbuf = torch.empty((2, K, B), dtype=torch.float32, device=logits.device) if deterministic else None
+    rowbuf = torch.empty((2, K, B), dtype=torch.float32, device=logits.device) if OPTIONS.deterministic else None
     _C.ce_fwd_bwd(_p(logits), _p(lab), _p(v), _p(loss), _p(correct), _p(dlogits), K, B, NC, _f32(logits), _s(),
                   _p(rowbuf))
     return loss, correct, dlogits
@@ -762,7 +758,7 @@ def embedding_bwd(dy, tokens, gtable, scale: float = 1.0):
     tok = tokens.to(torch.int32).contiguous()
     D = dy.shape[-1]
     gtable.zero_()
-    if deterministic:
+    if OPTIONS.deterministic:
         # rows grouped by (client, token) with a stable sort; each group summed in sequence order,
         # in fixed 64-row chunks joined in chunk order (a padding token's thousands of rows per
         # client are summed by many waves, not one)

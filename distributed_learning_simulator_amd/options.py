@@ -1,0 +1,129 @@
+"""Runtime options of the engine and kernels: one object, read at call time.
+
+These are measurement / comparison switches (alternating A/B runs, tests), not part of the
+experiment config surface of the reference. They used to be import-time module constants
+(`DLS_*` environment variables read once when a module loaded), so a session could not change
+them and tests had to patch module globals. Now:
+
+* `OPTIONS` holds every switch; the code paths read `OPTIONS.<name>` when they run;
+* the environment variables of the same switches still seed the defaults (scripts/ab_env.sh);
+* a run can set them from its config (`runtime_options: {planes: false, streams: 1}` in the
+  YAML or `++<group>.runtime_options.streams=1` on the command line; Session applies them),
+  programmatically (`options.update(streams=1)`), or for a block (`with options.override(...)`);
+* the native launch knobs (tile rules of csrc/) are forwarded to the extension
+  (`set_native_option`) when set.
+
+Defaults are the measured-best settings; each field's comment says what the other setting does.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import dataclasses
+import os
+
+
+def _env_bool(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    return default if v is None else v not in ("0", "", "false", "False")
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return default if v is None or v == "" else int(v)
+
+
+@dataclasses.dataclass
+class RuntimeOptions:
+    # --- fp32 (split-bf16) activation operands
+    planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_PLANES", True))
+    """BatchNorms emit bf16 (hi, lo) planes for the LDS-DMA plane / halo GEMMs (off: every conv
+    splits its operand in registers)."""
+    ln_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_LN_PLANES", True))
+    """LayerNorm outputs carry planes for the Transformer's plane linears."""
+    block_out_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BLOCK_OUT_PLANES", True))
+    """ResNet block outputs written only in the forms their readers take (off: fp32 + planes)."""
+    # --- BatchNorm fusions
+    bn_epilogue_stats: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_EPILOGUE_STATS", True))
+    """BN forward statistics from the producing conv's epilogue (off: BN's own statistics pass)."""
+    bn_bwd_parts: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_BWD_PARTS", True))
+    """BN backward partial sums from the consuming conv's dgrad epilogue (off: own reduction)."""
+    dense_stats_cache: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_STATS_CACHE", False))
+    """DenseNet blocks compute each channel's statistics once (measured no faster: off)."""
+    bn_fused_coef: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_COEF", False))
+    """BN coefficients in a last-arriver stage of the statistics kernel (measured slower: off)."""
+    # --- reductions
+    deterministic: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DETERMINISTIC", True))
+    """Split-K weight gradients and column sums folded in a fixed order (off: fp32 atomics)."""
+    # --- step execution
+    streams: int = dataclasses.field(default_factory=lambda: _env_int("DLS_STREAMS", 2))
+    """Sub-cohort HIP streams trained concurrently on one GPU."""
+    graphs: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_GRAPHS", True))
+    """HIP-graph replay of whole training steps (off: eager steps)."""
+    max_graphs: int = dataclasses.field(default_factory=lambda: _env_int("DLS_MAX_GRAPHS", 2))
+    """Captured step graphs kept per trainer (each owns a private memory pool)."""
+    shared_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_SHARED_PLANES", False))
+    """Shared-model steps (sign-SGD / sync-SGD): every client reads the one shared row's weight
+    planes (rep = K) and its activations' planes (off: register-split GEMMs)."""
+    # --- native launch knobs (csrc/, forwarded to the extension; None = the kernel's own default)
+    native: dict = dataclasses.field(default_factory=dict)
+    """e.g. {"tn_kref": 8, "pl_min_wg": 0, "conv_gl": 0, "f32_smallk": 1, "attn_mfma": 0}."""
+
+
+OPTIONS = RuntimeOptions()
+_FIELDS = {f.name for f in dataclasses.fields(RuntimeOptions)}
+
+
+_NATIVE_UNSET = -1000000  # (csrc/dls.h kOptUnset: back to the environment / kernel default)
+
+
+def _push_native(native: dict) -> None:
+    if not native:
+        return
+    try:
+        from .ops import hip
+    except ImportError:  # no extension (CPU box): nothing to forward
+        return
+    for k, v in native.items():
+        hip._C.set_native_option(str(k), _NATIVE_UNSET if v is None else int(v))
+
+
+def update(**kw) -> dict:
+    """Set options; returns the previous values of the ones changed."""
+    old = {}
+    for k, v in kw.items():
+        if k not in _FIELDS:
+            raise KeyError(f"unknown runtime option {k!r}; known: {sorted(_FIELDS)}")
+        old[k] = getattr(OPTIONS, k)
+        if k == "native":
+            merged = dict(OPTIONS.native)
+            merged.update(v or {})
+            v = {n: x for n, x in merged.items() if x is not None}
+        else:
+            v = type(old[k])(v)
+        setattr(OPTIONS, k, v)
+    if "native" in kw:
+        _push_native(kw["native"] or {})
+    return old
+
+
+@contextlib.contextmanager
+def override(**kw):
+    """Temporarily set options (tests, A/B loops)."""
+    old = update(**kw)
+    try:
+        yield OPTIONS
+    finally:
+        native_prev = old.pop("native", None)
+        for k, v in old.items():
+            setattr(OPTIONS, k, v)
+        if native_prev is not None:  # knobs this block set go back to their previous value (or unset)
+            update(native={n: native_prev.get(n) for n in (kw["native"] or {})})
+
+
+def apply_config(config) -> None:
+    """A run's `runtime_options:` mapping (config extra key) → OPTIONS."""
+    extra = getattr(config, "extra", None) or {}
+    opts = extra.get("runtime_options")
+    if opts:
+        update(**dict(opts))

@@ -30,6 +30,7 @@ from .data.datasets import create_dataset_collection, get_spec
 from .engine.memory import DEVICE_LOCK, plan_capacity
 from .engine.trainer import CohortTrainer, HyperParameter
 from .method import CentralizedAlgorithmFactory
+from .options import apply_config as apply_options
 from .models.zoo import build_model, stored_image_channels
 from .parallel.comm import Comm, get_comm, init_distributed
 from .practitioner import create_practitioners
@@ -56,6 +57,7 @@ class Session:
     def __init__(self, config, practitioners=None, comm: Comm | None = None):
         self.config = copy.deepcopy(config)
         cfg = self.config
+        apply_options(cfg)  # the run's `runtime_options:` (A/B switches, options.py)
         if not CentralizedAlgorithmFactory.has_algorithm(cfg.distributed_algorithm):
             raise ValueError(f"unknown distributed_algorithm {cfg.distributed_algorithm!r}; registered: "
                              f"{sorted(CentralizedAlgorithmFactory.config)}")

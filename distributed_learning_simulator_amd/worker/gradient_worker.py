@@ -29,6 +29,7 @@ import torch
 from ..engine.trainer import TrainStats
 from ..message import FlatParameterMessage
 from ..ops import fl
+from ..options import OPTIONS
 from ..server.aggregation_server import AggregationServer
 from .aggregation_worker import AggregationWorker
 
@@ -94,12 +95,12 @@ class GradientWorker(AggregationWorker):
         wd = tr.hyper.weight_decay
         theta0 = b.theta[:1]
         nbytes = self._wire_bytes_per_client()
-        # DLS_SHARED_PLANES=1: the shared row's (hi, lo) weight planes feed the split-plane GEMMs
+        # OPTIONS.shared_planes: the shared row's (hi, lo) weight planes feed the split-plane GEMMs
         # of every client (rep = K; the SGD kernel keeps them current with θ). Off by default:
         # measured on sign-SGD ResNet-50 (224², batch 128) it lost to the register-staged split
         # kernels (29.4 s/round at 8 clients per wave vs 26.5 s), and the planes' activation
         # memory shrinks the wave (tests/test_gpu_sessions.py covers the path)
-        split = b.split[:1] if (b.split is not None and os.environ.get("DLS_SHARED_PLANES", "0") == "1") else None
+        split = b.split[:1] if (b.split is not None and OPTIONS.shared_planes) else None
         if split is not None:
             fl.split_rows(theta0, split)
         tr._split_live = split is not None

@@ -10,6 +10,7 @@ criterion: "accuracy trajectory matches the CPU oracle").
 import pytest
 import torch
 
+from distributed_learning_simulator_amd import options
 from distributed_learning_simulator_amd.config import load_config
 from distributed_learning_simulator_amd.ops import backend
 from distributed_learning_simulator_amd.parallel.comm import Comm
@@ -147,8 +148,6 @@ def test_resnet18_bitwise_reproducible_and_planes(hip, tmp_path, monkeypatch):
     bitwise-equal global models (split-K weight gradients folded in order, no atomics), and the
     split-plane GEMM path (csrc/conv_pl.hip, planes written by the BatchNorms) agrees with the
     register-staged split path to fp32 noise."""
-    from distributed_learning_simulator_amd.ops import functional as Fn
-
     from distributed_learning_simulator_amd.ops import hip as H
 
     ov = {"round": 1, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
@@ -159,8 +158,8 @@ def test_resnet18_bitwise_reproducible_and_planes(hip, tmp_path, monkeypatch):
     assert min(H.planes_launches[k] for k in ("fwd", "dgrad", "wgrad")) > 0, H.planes_launches
     b, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
     assert torch.equal(a.server.global_parameter, b.server.global_parameter)
-    monkeypatch.setattr(Fn, "PLANES", False)
-    c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
+    with options.override(planes=False):
+        c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
     assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
 
 
@@ -181,8 +180,8 @@ def test_resnet18_bn_bwd_partials_from_dgrad(hip, tmp_path, monkeypatch):
     assert c["used"] > 0 and c["fallback"] == 0 and c["used"] * 7 == c["none"] * 13, c
     b, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
     assert torch.equal(a.server.global_parameter, b.server.global_parameter)
-    monkeypatch.setattr(Fn, "BN_BWD_PARTS", False)
-    c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
+    with options.override(bn_bwd_parts=False):
+        c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
     assert _rel(a.server.global_parameter, c.server.global_parameter) < 1e-4
 
 
@@ -207,19 +206,19 @@ def test_sign_sgd_resnet18_planes_shared_weights(hip, tmp_path, monkeypatch):
     paths are vote flips where a client's gradient sits within rounding noise of zero: the
     planes path must disagree with the CPU fp32 oracle no more often than the plain fp32 GPU
     path (no planes) does."""
-    from distributed_learning_simulator_amd.ops import functional as Fn
+    from distributed_learning_simulator_amd import options
     from distributed_learning_simulator_amd.ops import hip as H
 
     # (5 clients: an even count makes 2-2 vote ties, which any last-bit gradient change breaks)
     ov = {"round": 1, "epoch": 1, "worker_number": 5, "model_name": "ResNet18", "dataset_name": "CIFAR10",
           "dataset_kwargs.scale": 0.004, "learning_rate": 0.001}
-    monkeypatch.setenv("DLS_SHARED_PLANES", "1")
     H.planes_launches.clear()
-    a, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    with options.override(shared_planes=True):
+        a, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "a", "cuda")
     assert min(H.planes_launches[k] for k in ("fwd", "dgrad", "wgrad")) > 0, H.planes_launches
     c, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "c", "cpu")
-    monkeypatch.setattr(Fn, "PLANES", False)
-    b, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    with options.override(shared_planes=True, planes=False):
+        b, _ = _run("sign_sgd/cifar10.yaml", ov, tmp_path / "b", "cuda")
     ga, gb, gc = (s.server.global_parameter.cpu() for s in (a, b, c))
 
     def flips(x, y):  # each step moves a weight by ±lr (0 on a tie): a flipped vote differs by ≥ lr

@@ -648,49 +648,6 @@ def test_dgrad_compact_shortcut_acc(hip, H, planes):
 
 
 @pytest.mark.parametrize("case", [
-    # K, B, H (= W), Ci, Co: every compiled (BMc, W) shape of the halo wgrad, split-K and not
-    (2, 2, 32, 64, 64),     # BMc 64, W 32
-    (2, 3, 16, 32, 128),    # BMc 128, W 16
-    (3, 4, 8, 64, 64),      # BMc 64, W 8
-    (2, 2, 8, 256, 256),    # BMc 128, W 8
-    (1, 64, 32, 32, 64),    # a full CIFAR batch: many split-K slabs
-])
-def test_wgrad_halo(hip, case):
-    """3x3 stride-1 weight gradient with LDS halo reuse (csrc/conv_wgrad_halo.hip): within 1e-5 of
-    the fp64 oracle, bitwise-reproducible run to run, and the default wgrad route for these shapes."""
-    K, B, H, Ci, Co = case
-    torch.manual_seed(11)
-    x = _f(K, B, H, H, Ci)
-    dy = _f(K, B, H, H, Co)
-    exp = ref.conv_wgrad(_d(dy), _d(x), (K, Co, 3, 3, Ci), 1, 1)
-    xp, dyp = hip.split_planes(x), hip.split_planes(dy)
-    try:
-        hip._C.conv_wgrad_halo_set_mode(2)  # 64 output channels per wave
-        g2 = torch.full((K, Co, 3, 3, Ci), 4.0, device=DEV)
-        hip.conv_wgrad(dy, x, g2, 1, 1, dy_planes=dyp, x_planes=xp)
-        _close(g2, exp)
-        hip._C.conv_wgrad_halo_set_mode(1)  # 32 per wave
-        ga = torch.full((K, Co, 3, 3, Ci), 5.0, device=DEV)
-        hip.conv_wgrad(dy, x, ga, 1, 1, dy_planes=dyp, x_planes=xp)
-        _close(ga, exp)
-        gb = torch.full_like(ga, -5.0)
-        hip.conv_wgrad(dy, x, gb, 1, 1, dy_planes=dyp, x_planes=xp)
-        assert torch.equal(ga, gb), "halo wgrad not reproducible"
-        hip._C.conv_wgrad_halo_set_mode(0)
-        gc = torch.full_like(ga, 7.0)
-        hip.conv_wgrad(dy, x, gc, 1, 1, dy_planes=dyp, x_planes=xp)
-        _close(gc, exp)
-        # (where both kernels pick the same pixel split, they sum every element in the same order
-        # — 16 pixels per MFMA triple, splits folded in order — and agree bitwise)
-        if hip._C.conv_wgrad_halo_splitk(Co, Ci, B * H * H) == hip._C.conv_tn_splitk(K, Co, 9 * Ci, B * H * H, Ci, -1,
-                                                                                    1, Co, Ci, 1):
-            assert torch.equal(ga, gc)
-        assert torch.equal(ga, g2)  # (same split and order: the wave tiling changes nothing)
-    finally:
-        hip._C.conv_wgrad_halo_set_mode(-1)
-
-
-@pytest.mark.parametrize("case", [
     # K, B, H (= W), Ci, Co, k, planes, relu, acc: conv_halo (3x3 planes), conv_pl (1x1 planes),
     # conv_f32 (no planes), a 41-sample batch (> FOLD partials: the fp64 fold stage), no ReLU
     (2, 3, 16, 64, 64, 3, True, True, True),

@@ -1,0 +1,41 @@
+"""Runtime options (options.py): one object read when the ops run, settable per run from the
+config, programmatically or for a block — not import-time module constants."""
+
+import pytest
+
+from distributed_learning_simulator_amd import options
+from distributed_learning_simulator_amd.config import config_from_dict
+from distributed_learning_simulator_amd.parallel.comm import Comm
+from distributed_learning_simulator_amd.session import Session
+
+
+def test_override_restores():
+    before = options.OPTIONS.streams, options.OPTIONS.planes
+    with options.override(streams=1, planes=False) as o:
+        assert o.streams == 1 and o.planes is False
+    assert (options.OPTIONS.streams, options.OPTIONS.planes) == before
+    with pytest.raises(KeyError):
+        options.update(no_such_switch=1)
+
+
+def test_session_applies_runtime_options(tmp_path):
+    """A run's `runtime_options:` mapping reaches the engine (trainer stream count) and the
+    model code (block-output planes switch) at session start."""
+    before = options.OPTIONS.streams, options.OPTIONS.block_out_planes
+    try:
+        cfg = config_from_dict({"distributed_algorithm": "fed_avg", "dataset_name": "MNIST", "model_name": "LeNet5",
+                                "worker_number": 2, "round": 1, "epoch": 1, "dataset_kwargs": {"scale": 0.01},
+                                "save_dir": str(tmp_path), "log_level": "WARNING",
+                                "runtime_options": {"streams": 3, "block_out_planes": False}})
+        sess = Session(cfg, comm=Comm())
+        assert sess.trainer.num_streams == 3
+        assert options.OPTIONS.block_out_planes is False
+    finally:
+        options.update(streams=before[0], block_out_planes=before[1])
+
+
+def test_env_seeds_defaults(monkeypatch):
+    monkeypatch.setenv("DLS_STREAMS", "4")
+    monkeypatch.setenv("DLS_PLANES", "0")
+    o = options.RuntimeOptions()
+    assert o.streams == 4 and o.planes is False
