@@ -74,7 +74,9 @@ def main() -> None:
     ap.add_argument("--workload", default="fedavg_resnet18",
                     choices=["fedavg_resnet18", "fedavg_densenet40", "fedobd_transformer", "fedobd_imdb",
                              "signsgd_resnet50", "signsgd_densenet40", "gtg_resnet18", "fedavg_mlp_mnist"])
-    ap.add_argument("--algo", default="fed_avg", choices=["fed_avg", "fed_obd"])
+    ap.add_argument("--algo", default="fed_avg", choices=["fed_avg", "fed_obd", "fed_obd_sq"],
+                    help="fedavg_resnet18: fed_avg or fed_obd; fedobd_*: fed_obd (NNADQ uploads, the default) or "
+                         "fed_obd_sq (stochastic 255-level quantisation, method/fed_obd/__init__.py)")
     ap.add_argument("--model", default="ResNet18")
     ap.add_argument("--clients", type=int, default=100)
     ap.add_argument("--epoch", type=int, default=5)
@@ -301,7 +303,9 @@ def workload_config(args, rounds: int) -> dict:
     if args.workload in ("fedobd_transformer", "fedobd_imdb"):
         # stage-1 rounds are the timed steps; stage 2 (second_phase_epoch epochs over all clients)
         # is run to the end afterwards and reported under "stage2"
-        obd = {"distributed_algorithm": "fed_obd", "worker_number": 100, "epoch": 5, "batch_size": 64,
+        sq = args.algo == "fed_obd_sq"
+        obd = {"distributed_algorithm": "fed_obd_sq" if sq else "fed_obd", "worker_number": 100, "epoch": 5,
+               "batch_size": 64,
                "optimizer_name": "SGD", "learning_rate": 0.01, "learning_rate_scheduler_name": "CosineAnnealingLR",
                "algorithm_kwargs": {"second_phase_epoch": 10, "dropout_rate": 0.3, "random_client_number": 50},
                "endpoint_kwargs": {"server": {"weight": 0.0001}, "worker": {"weight": 0.0001}},
@@ -321,8 +325,10 @@ def workload_config(args, rounds: int) -> dict:
                "model_kwargs": {"d_model": 512, "nhead": 8, "num_encoder_layer": 6, "dim_feedforward": 2048,
                                 "max_len": 128}}
         return {"config": cfg, "stage2": True, "samples_per_round": shard_samples, "seq_len": 128,
-                "config_extra": {"d_model": 512, "nhead": 8, "layers": 6, "ffn": 2048},
-                "metric": "FL rounds/sec (FedOBD stage 1, 100 clients / 50 per round, Transformer-base, AG-News-shaped)",
+                "config_extra": {"d_model": 512, "nhead": 8, "layers": 6, "ffn": 2048,
+                                 "upload_quantiser": "stochastic-255" if sq else "NNADQ"},
+                "metric": ("FL rounds/sec (FedOBD" + ("-SQ" if sq else "") +
+                           " stage 1, 100 clients / 50 per round, Transformer-base, AG-News-shaped)"),
                 "data": "synthetic (AG-News-shaped token sequences, max_len 128, iid shards, random-init weights)"}
     if args.workload == "signsgd_densenet40":
         # conf/sign_sgd/cifar10.yaml verbatim but for `epoch` (--epoch; the config's 100 epochs make

@@ -2,10 +2,11 @@
 CIFAR-10-shaped 10k test split, exactly as GTG-Shapley's batch metric function runs them
 (`method/shapley_value/__init__.py` batch_metric → Session.evaluate_tensors → CohortTrainer.evaluate).
 
-    python bench/eval_bench.py [--M 32] [--iters 3] [--max-images 8192]
+    python bench/eval_bench.py [--M 32] [--iters 3] [--max-images 8192 ...] [--streams 2 ...]
 
-Prints one JSON line: ms per M-model chunk, ms per model, images/s and the useful forward
-TFLOP/s (1.11 GFLOP per 32x32 ResNet-18 forward).
+Prints one JSON line per (max_images, streams) setting — timed in interleaved rounds, best of
+`--rounds` — with ms per M-model chunk, ms per model, images/s and the useful forward TFLOP/s
+(1.11 GFLOP per 32x32 ResNet-18 forward).
 """
 
 from __future__ import annotations
@@ -28,7 +29,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=32)
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--max-images", type=int, default=8192)
+    ap.add_argument("--max-images", type=int, nargs="+", default=[8192])
+    ap.add_argument("--streams", type=int, nargs="+", default=[2])
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--fused", type=int, nargs="+", default=[1],
+                    help="1: bn1 applied in conv2's halo loader (options.bn_fused_halo), 0: unfused")
     ap.add_argument("--n-test", type=int, default=10000)
     ap.add_argument("--no-planes", action="store_true", help="A/B: evaluate without weight planes")
     args = ap.parse_args()
@@ -50,21 +55,32 @@ def main():
     g = torch.Generator().manual_seed(0)
     rows = torch.stack([model.layout.init_flat(g) for _ in range(args.M)]).to(dev)
 
-    def run():
-        return tr.evaluate(rows, max_images=args.max_images)
+    from distributed_learning_simulator_amd import options
 
-    run()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.iters):
-        loss, corr, n = run()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.iters
-    imgs = args.M * n
-    print(json.dumps({"bench": "eval_resnet18_fp32", "M": args.M, "n_test": n, "planes": not args.no_planes,
-                      "max_images": args.max_images, "ms_per_chunk": dt * 1e3, "ms_per_model": dt * 1e3 / args.M,
-                      "images_per_s": imgs / dt, "fwd_tflops": imgs * FWD_GFLOP_RESNET18_CIFAR / dt / 1e3,
-                      "acc_mean": float((corr / n).mean())}), flush=True)
+    settings = [(mi, st, fu) for mi in args.max_images for st in args.streams for fu in args.fused]
+    best = {}
+    out = {}
+    for _ in range(args.rounds):
+        for mi, st, fu in settings:
+            tr.num_streams = st
+            options.update(bn_fused_halo=bool(fu))
+            tr.evaluate(rows, max_images=mi)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                loss, corr, n = tr.evaluate(rows, max_images=mi)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.iters
+            if dt < best.get((mi, st, fu), float("inf")):
+                best[(mi, st, fu)] = dt
+                out[(mi, st, fu)] = (n, float((corr / n).mean()))
+    for (mi, st, fu), dt in best.items():
+        n, acc = out[(mi, st, fu)]
+        imgs = args.M * n
+        print(json.dumps({"bench": "eval_resnet18_fp32", "M": args.M, "n_test": n, "planes": not args.no_planes,
+                          "max_images": mi, "streams": st, "bn_fused_halo": bool(fu), "ms_per_chunk": dt * 1e3, "ms_per_model": dt * 1e3 / args.M,
+                          "images_per_s": imgs / dt, "fwd_tflops": imgs * FWD_GFLOP_RESNET18_CIFAR / dt / 1e3,
+                          "acc_mean": acc}), flush=True)
 
 
 if __name__ == "__main__":

@@ -40,9 +40,15 @@ __device__ __forceinline__ void hwait_vm() {
 
 // HB: halo buffers (2: chunk c+1's halo in flight during chunk c; 1: loaded at the chunk start
 // behind a barrier — half the LDS, so two workgroups share a CU); NBS: weight-tile slots (3 or 2)
-template <int IMG, int TH, int TW, int BN, int WM, int WN, bool BKM, int MINW, int HB, int NBS>
+// BNF: the A operand is BatchNorm(+ReLU) of the raw fp32 input, applied while the halo is staged
+// (ConvNTParams::bn_x): each lane loads its 8 channels of a halo row into registers, applies the
+// per-channel (scale, shift) and ReLU, splits to hi / lo and writes the same 16-B LDS slots the
+// plane DMA would fill — bit-identical operands to BN-apply-then-planes, without the normalised
+// tensor ever reaching HBM. Forward (row-major B) with one halo buffer only.
+template <int IMG, int TH, int TW, int BN, int WM, int WN, bool BKM, int MINW, int HB, int NBS, bool BNF = false>
 __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTParams p) {
   static_assert((HB == 2 && NBS == 3) || (HB == 1 && (NBS == 2 || NBS == 3)), "pipeline shape");
+  static_assert(!BNF || (HB == 1 && !BKM), "fused BN input: forward, one halo buffer");
   constexpr int BM = IMG * TH * TW;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -94,7 +100,11 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
 
   // ---- halo loader: instruction i of wave w fills halo rows (i·NW + w)·16 + lane/4, physical
   // chunk lane & 3 ← logical chunk lc = (lane & 3) ^ key(row)
-  int h_off[HI];
+  int h_off[HI], h_ch[HI];  // (h_ch: BNF, the lane's first channel within a 32-channel chunk)
+  // (BNF) rows of samples past the BN's valid rows read as zero, like the padding; h_ctr: the halo
+  // row is one of this row block's own output pixels (written out when bn_yp is set)
+  bool h_bnok[HI], h_ctr[HI];
+  const int bn_rows = BNF ? (p.bn_valid ? p.bn_valid[client] : p.B * p.H * p.W) : 0;
 #pragma unroll
   for (int i = 0; i < HI; ++i) {
     const int hr = (i * NW + wid) * 16 + (lane >> 2);
@@ -102,8 +112,12 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
     const int hh = rem / PITCH, ww = rem - hh * PITCH;
     const int ih = h0 - p.pad + hh, iw = ww - p.pad_w;
     const int lc = (lane & 3) ^ (((hr >> 2) + (hr / PITCH) * KC) & 3);
+    const int pix = ((b0 + img) * p.H + ih) * p.W + iw;
     const bool ok = hr < HP && ww < HW2 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-    h_off[i] = ok ? (((b0 + img) * p.H + ih) * p.W + iw) * p.ldx + lc * 8 : -1;
+    h_off[i] = ok ? pix * p.ldx + lc * 8 : -1;
+    h_ch[i] = lc * 8;
+    h_bnok[i] = !BNF || pix < bn_rows;
+    h_ctr[i] = ok && hh >= 1 && hh <= TH && ww >= 1 && ww <= TW;
   }
   // ---- weight loader (as conv_pl.hip): row-major rows (i·NW + w)·16 + lane/4; k-major k-rows
   // (i·NW + w)·RPI + lane/CPR with the 32-element segment swizzle of the k-major image
@@ -127,17 +141,58 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   }
 
   const int nchunks = p.C / 32, nsteps = nchunks * 9;
+  const float* bxc = BNF ? p.bn_x + (long)client * p.bn_x_cs : nullptr;
+  const float* bcoef = BNF ? p.bn_coef + (long)client * p.C * 2 : nullptr;
+  const long bn_rc = (long)p.B * p.H * p.W * p.C;  // (elements of one plane of one client)
+  bf16_t* bn_yph = (BNF && p.bn_yp && n0 == 0) ? p.bn_yp + (long)client * 2 * bn_rc : nullptr;
+  uint8_t* bn_mk = (BNF && p.bn_mask && n0 == 0) ? p.bn_mask + (long)client * (bn_rc >> 3) : nullptr;
   auto issue_halo = [&](int c, int buf) {
     const bool live = c < nchunks;
     unsigned char* Hs = smem + H_OFF + buf * 2 * H_PL;
 #pragma unroll
     for (int i = 0; i < HI; ++i) {
       const bool ok = live && h_off[i] >= 0;
-      const uint32_t off = (uint32_t)(h_off[i] + c * 32) * 2u;
       unsigned char* d = Hs + (i * NW + wid) * 1024;
-      hdma16(ar, d, ok ? off : OOB_OFF);
-      hdma16(ar, d + H_PL, ok ? off + a_lo : OOB_OFF);
+      if constexpr (BNF) {
+        // lane's 8 channels: h_off = pixel·C + lc·8 (the DMA's element offset, ldx == C)
+        const bool inimg = ok;
+        const bool okv = ok && h_bnok[i];
+        const int e = (ok ? h_off[i] : 0) + c * 32;
+        const int ch = c * 32 + h_ch[i];
+        const float4 x0 = *reinterpret_cast<const float4*>(bxc + e);
+        const float4 x1 = *reinterpret_cast<const float4*>(bxc + e + 4);
+        const float4* cf = reinterpret_cast<const float4*>(bcoef + 2 * ch);  // (scale, shift) pairs
+        const float4 c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3];
+        float v[8] = {fmaf(x0.x, c0.x, c0.y), fmaf(x0.y, c0.z, c0.w), fmaf(x0.z, c1.x, c1.y), fmaf(x0.w, c1.z, c1.w),
+                      fmaf(x1.x, c2.x, c2.y), fmaf(x1.y, c2.z, c2.w), fmaf(x1.z, c3.x, c3.y), fmaf(x1.w, c3.z, c3.w)};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (p.bn_relu) v[j] = fmaxf(v[j], 0.f);
+          if (!okv) v[j] = 0.f;
+        }
+        uint32_t hi[4], lo[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) split_pair(v[2 * j], v[2 * j + 1], hi[j], lo[j]);
+        *reinterpret_cast<uint4*>(d + lane * 16) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+        *reinterpret_cast<uint4*>(d + H_PL + lane * 16) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+        if (bn_yph && inimg && h_ctr[i]) {  // this row block's own pixels: planes + ReLU bits out
+          *reinterpret_cast<uint4*>(bn_yph + e) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+          *reinterpret_cast<uint4*>(bn_yph + bn_rc + e) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+          if (bn_mk) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m |= (v[j] > 0.f ? 1u : 0u) << j;
+            bn_mk[e >> 3] = (uint8_t)m;
+          }
+        }
+      } else {
+        const uint32_t off = (uint32_t)(h_off[i] + c * 32) * 2u;
+        hdma16(ar, d, ok ? off : OOB_OFF);
+        hdma16(ar, d + H_PL, ok ? off + a_lo : OOB_OFF);
+      }
     }
+    // (the LDS writes of a register-staged halo must land before the barrier that publishes it)
+    if constexpr (BNF) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   };
   auto issue_w = [&](int s, int slot) {
     const bool live = s < nsteps;
@@ -274,6 +329,14 @@ void launch_halo(const ConvNTParams& p, int K, hipStream_t s) {
                        dim3(WM * WN * 64), 0, s, p);
 }
 
+template <int IMG, int TH, int TW, int BN, int WM, int WN, int NBS>
+void launch_halo_bnf(const ConvNTParams& p, int K, hipStream_t s) {
+  const int tilesM = IMG == 1 ? p.B * (p.OH / TH) : p.B / IMG;
+  const int grid = K * tilesM * cdiv(p.N, BN);
+  hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, false, 1, 1, NBS, true>), dim3(grid),
+                     dim3(WM * WN * 64), 0, s, p);
+}
+
 int g_halo_mode = -1;  // -1 shape rule, 0 never, 1 whenever supported (tests / A-B)
 int g_halo_variant = -1;
 
@@ -286,7 +349,8 @@ void conv_halo_set_variant(int v) { g_halo_variant = v; }
 static int halo_config(const ConvNTParams& p) {
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.pad_w != 1 || p.dil != 1) return -1;
   if (p.OH != p.H || p.OW != p.W || p.out_s > 1 || p.C % 32 || p.N % 8 || p.ldx % 8 || p.R != 9 * p.C) return -1;
-  if (p.x_lo == 0 || p.wsplit == nullptr) return -1;
+  if ((p.x_lo == 0 && p.bn_x == nullptr) || p.wsplit == nullptr) return -1;
+  if (p.bn_x != nullptr && (p.b_kmajor || p.ldx != p.C)) return -1;
   if (p.OW == 32 && p.OH % 8 == 0 && p.N <= 64) return 0;  // 1 × 8 × 32, BN 64
   if (p.OW == 16 && p.OH == 16) return 1;                   // 1 × 16 × 16, BN 128
   if (p.OW == 8 && p.OH == 8 && p.B % 2 == 0) return 2;     // 2 × 8 × 8, BN 128
@@ -308,6 +372,15 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
   // measured (kernel_bench --f32 --planes, 50 clients; fwd / dgrad TFLOP/s vs the implicit-GEMM
   // plane kernels): l1 v1 302 / 275 (259 / 247), l2 v1 441 / 396 (338 / 310), l3 v2 409 / 344
   // (361 / 321)
+  if (p.bn_x != nullptr) {  // fused BN input: the default one-halo-buffer shapes only
+    if (g_halo_variant >= 0 || cfg == 3) return false;
+    switch (cfg) {
+      case 0: launch_halo_bnf<1, 8, 32, 64, 4, 2, 3>(p, K, s); break;
+      case 1: launch_halo_bnf<1, 16, 16, 128, 4, 2, 2>(p, K, s); break;
+      default: launch_halo_bnf<2, 8, 8, 128, 4, 2, 2>(p, K, s); break;
+    }
+    return true;
+  }
   const int v = g_halo_variant >= 0 ? g_halo_variant : (cfg == 2 ? 2 : 1);
   switch (cfg * 3 + v) {
     case 0: launch_halo<1, 8, 32, 64, 4, 1, 2, 3>(p, K, s); break;    // 120 KB, 4 waves
@@ -325,4 +398,50 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
     default: return false;
   }
   return true;
+}
+
+bool conv_halo_bn_supported(int B, int H, int W, int C, int N) {
+  ConvNTParams p{};
+  p.bn_x = reinterpret_cast<const float*>(16);  // (shape check only)
+  p.wsplit = reinterpret_cast<const bf16_t*>(16);
+  p.B = B; p.H = H; p.W = W; p.C = C; p.OH = H; p.OW = W; p.KH = 3; p.KW = 3;
+  p.stride = 1; p.pad = 1; p.pad_w = 1; p.dil = 1; p.N = N; p.R = 9 * C; p.ldx = C; p.out_s = 1;
+  const int cfg = halo_config(p);
+  return g_halo_mode != 0 && g_halo_variant < 0 && cfg >= 0 && cfg != 3 && (long)B * H * W * C * 4 < (1L << 31);
+}
+
+bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, const int* valid_rows,
+                      const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y, long y_cs, int K, int B,
+                      int H, int W, int C, int N, float* stats, const int* stats_valid, hipStream_t s,
+                      bf16_t* yp, uint8_t* mask) {
+  ConvNTParams p{};
+  p.f32 = 1;
+  p.bn_yp = yp;
+  p.bn_mask = mask;
+  p.bn_x = x;
+  p.bn_x_cs = x_cs;
+  p.bn_coef = coef;
+  p.bn_relu = relu;
+  p.bn_valid = valid_rows;
+  p.wsplit = wsplit;
+  p.ws_cs = ws_cs;
+  p.ws_plane = ws_plane;
+  p.rep = rep;
+  p.y = reinterpret_cast<bf16_t*>(y);
+  p.y_cs = y_cs;
+  p.B = B; p.H = H; p.W = W; p.C = C; p.OH = H; p.OW = W; p.KH = 3; p.KW = 3;
+  p.stride = 1; p.pad = 1; p.pad_w = 1; p.dil = 1;
+  p.M = B * H * W; p.N = N; p.R = 9 * C;
+  p.wKH = 3; p.wKW = 3; p.kh_off = 2; p.kw_off = 2; p.kh_step = 1; p.kw_step = 1;
+  p.out_s = 1;
+  p.ldx = C; p.ldy = N;
+  p.fd_ohw = make_fastdiv((uint32_t)(H * W));
+  p.fd_ow = make_fastdiv((uint32_t)W);
+  p.fd_kwc = make_fastdiv((uint32_t)(3 * C));
+  p.fd_c = make_fastdiv((uint32_t)C);
+  p.stats = stats;
+  p.stats_valid = stats_valid;
+  const long wb = (ws_plane + (long)N * p.R) * 2;
+  if (wb >= (long)OOB_OFF || (long)p.M * C * 4 >= (1L << 31)) return false;
+  return conv_halo(p, K, s);
 }

@@ -104,6 +104,21 @@ struct ConvNTParams {
   const float* bnb_mean;
   const float* bnb_rstd;
   const int* bnb_valid;
+  // optional BatchNorm(+ReLU) applied to the A operand while it is staged (conv_halo.hip forward,
+  // fp32): the layer input is then bn_x, the RAW output of the previous conv [K][B][H][W][C] fp32
+  // (client stride bn_x_cs floats), and the GEMM reads relu?(bn_coef[k][c][0]·x + bn_coef[k][c][1])
+  // — the BN's (scale, shift) pairs — zero outside the image and past bn_valid[k] rows; no
+  // normalised activation is ever written
+  const float* bn_x;
+  long bn_x_cs;
+  const float* bn_coef;
+  int bn_relu;
+  const int* bn_valid;
+  // (training) the normalised activation's split planes [K][2][R][C] and ReLU bit mask [K][R][C/8],
+  // written by the first N tile of each row block from the values it stages — what the BN apply
+  // pass would have written for the conv's weight gradient and the BN's backward
+  bf16_t* bn_yp;
+  uint8_t* bn_mask;
 };
 
 // BN-backward partial request handed to conv_dgrad (see ConvNTParams::bnb)
@@ -200,6 +215,17 @@ int conv_nt_pl_variant();           // -1: shape heuristic (set by benchmarks)
 void conv_nt_pl_set_variant(int v);
 // 3x3 stride-1 split-plane conv with LDS halo reuse (conv_halo.hip): false = shape not covered
 bool conv_halo(const ConvNTParams& p, int K, hipStream_t s);
+// 3x3 / stride-1 / pad-1 fp32 forward whose input is a BatchNorm(+ReLU) of the raw tensor x,
+// applied in the halo loader (ConvNTParams::bn_*); false: shape outside the halo kernels (the
+// caller applies the BN and runs the plain conv)
+bool conv_halo_bn_supported(int B, int H, int W, int C, int N);
+// BN apply with precomputed (scale, shift) coefficients (bn_fwd coef_out) → split planes (+ ReLU bits)
+void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
+                   bf16_t* yp, uint8_t* rmask, hipStream_t s);
+bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, const int* valid_rows,
+                      const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y, long y_cs, int K, int B,
+                      int H, int W, int C, int N, float* stats, const int* stats_valid, hipStream_t s,
+                      bf16_t* yp = nullptr, uint8_t* mask = nullptr);
 void conv_halo_set_mode(int m);  // -1 shape rule, 0 never, 1 whenever supported
 void conv_halo_set_variant(int v);  // -1 default, 0..2 pipeline / tile variant (benchmarks)
 bool conv_tn_pl_supported(const ConvTNParams& p);
@@ -223,7 +249,7 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
             uint8_t* relu_mask, unsigned* counters, int f32, hipStream_t s,
             int ldx = 0, const float* pre_part = nullptr,
             int pre_nparts = 0, bf16_t* yp = nullptr,
-            int y_f32 = 1);  // yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused
+            int y_f32 = 1, float* coef_out = nullptr, int apply = 1);  // yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused
                                   // coefs); ldx: row stride of x / res (channel slice of a wider buffer), y
                                   // contiguous; pre_part: [K][pre_nparts][2C] Σx / Σx² partials from the
                                   // producing conv's epilogue (ConvNTParams::stats) — no statistics pass

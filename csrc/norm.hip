@@ -661,10 +661,12 @@ long bn_workspace_floats(int K, long R, int C) {
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
             uint8_t* rmask, unsigned* counters, int f32, hipStream_t s, int ldx, const float* pre_part,
-            int pre_nparts, bf16_t* yp, int y_f32) {
+            int pre_nparts, bf16_t* yp, int y_f32, float* coef_out, int apply) {
   if (ldx == 0) ldx = C;
-  // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums
-  float* coef = ws;
+  // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums. coef_out: the
+  // (scale, shift) pairs go there instead and outlive this call (apply = 0: the consumer conv
+  // applies them while staging its input, conv_halo_bn_fwd)
+  float* coef = coef_out ? coef_out : ws;
   const float* part = pre_part ? pre_part : ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
@@ -691,10 +693,27 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
                              (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
                              (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
     }
-    DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
-                                     valid_rows, coef, R, C, relu, rpb, rmask, ldx, f32 ? yp : nullptr,
-                                     f32 ? y_f32 : 1));
+    if (apply) {
+      DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
+                                       valid_rows, coef, R, C, relu, rpb, rmask, ldx, f32 ? yp : nullptr,
+                                       f32 ? y_f32 : 1));
+    }
   });
+}
+
+void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
+                   bf16_t* yp, uint8_t* rmask, hipStream_t s) {
+  // the apply pass of bn_fwd with coefficients computed earlier (bn_coef): planes (+ ReLU bits)
+  // only — what a deferred BN materialises when its consumer cannot apply it itself
+  const int rpb = rows_per_block(R, K);
+  dim3 grid(cdiv(R, rpb), K);
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL((bn_apply_kernel<float, 8>), grid, dim3(256), 0, s, x, (const float*)nullptr, (float*)nullptr,
+                       valid_rows, coef, R, C, relu, rpb, rmask, C, yp, 0);
+  } else {
+    hipLaunchKernelGGL((bn_apply_kernel<float, 1>), grid, dim3(256), 0, s, x, (const float*)nullptr, (float*)nullptr,
+                       valid_rows, coef, R, C, relu, rpb, (uint8_t*)nullptr, C, yp, 0);
+  }
 }
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,

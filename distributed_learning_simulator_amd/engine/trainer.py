@@ -531,7 +531,7 @@ class CohortTrainer:
     # ------------------------------------------------------------------ evaluate
     @torch.no_grad()
     def evaluate(self, theta_rows: torch.Tensor, dataset=None, batch_size: int | None = None,
-                 max_images: int = 8192, shard: tuple[int, int] = (0, 1), indices: torch.Tensor | None = None):
+                 max_images: int | None = None, shard: tuple[int, int] = (0, 1), indices: torch.Tensor | None = None):
         """Evaluate M models (theta_rows [M,P] fp32 or [P]) on `dataset` (default: the Test
         phase — `dc.test_indices` of the test split when a validation half was carved out).
         BN uses batch statistics of each eval batch (reference: running stats disabled).
@@ -550,6 +550,7 @@ class CohortTrainer:
             return self.graph.evaluate(self, theta_rows, shard)
         M = theta_rows.shape[0]
         B = batch_size or self.hyper.batch_size
+        max_images = int(max_images or OPTIONS.eval_max_images)
         n = ds.n if indices is None else int(indices.numel())
         nb = (n + B - 1) // B
         flat = torch.arange(nb * B, device=self.device) % n
@@ -570,26 +571,47 @@ class CohortTrainer:
             compute = compute.contiguous()
             split = torch.empty((M, 2, compute.shape[1]), dtype=torch.bfloat16, device=self.device)
             fl.split_rows(compute, split)
-        loss_tot = torch.zeros(M, dtype=torch.float32, device=self.device)
-        corr_tot = torch.zeros(M, dtype=torch.float32, device=self.device)
         g = max(1, min(nb, max_images // max(B * M, 1)))
-        for b0 in range(lo, hi, g):
-            b1 = min(hi, b0 + g)
-            gi = idx[b0:b1]
-            x = ds.gather(gi)
-            y = ds.gather_labels(gi)
-            c = counts[b0:b1]
-            if M > 1:
-                x = _repeat_leading(x, M)
-                y = y.repeat(M, 1)
-                c = c.repeat(M)
-            params = BoundParams(self.layout, compute, None, K=M * (b1 - b0), split=split)
-            ctx = RunCtx(params, c, training=False)
-            logits = self.model.forward(x, ctx)
-            loss, correct = Fn.cross_entropy(logits, y, c)
-            w = c.float()
-            loss_tot += (loss * w).view(M, -1).sum(1)
-            corr_tot += correct.view(M, -1).sum(1)
+        starts = list(range(lo, hi, g))
+        # launches alternate over the sub-cohort streams (their tails and the small BN / CE
+        # kernels overlap); each stream sums into its own accumulators, added in stream order
+        ns = max(1, min(self.num_streams if self.device.type == "cuda" else 1, len(starts)))
+        streams = self._streams(ns) if ns > 1 else [None]
+        if ns > 1:
+            cur = torch.cuda.current_stream(self.device)
+            for st in streams:
+                st.wait_stream(cur)
+        accs = []
+        for si in range(ns):
+            with (torch.cuda.stream(streams[si]) if ns > 1 else _nullctx()):
+                accs.append((torch.zeros(M, dtype=torch.float32, device=self.device),
+                             torch.zeros(M, dtype=torch.float32, device=self.device)))
+        for li, b0 in enumerate(starts):
+            si = li % ns
+            with (torch.cuda.stream(streams[si]) if ns > 1 else _nullctx()):
+                b1 = min(hi, b0 + g)
+                gi = idx[b0:b1]
+                x = ds.gather(gi)
+                y = ds.gather_labels(gi)
+                c = counts[b0:b1]
+                if M > 1:
+                    x = _repeat_leading(x, M)
+                    y = y.repeat(M, 1)
+                    c = c.repeat(M)
+                params = BoundParams(self.layout, compute, None, K=M * (b1 - b0), split=split)
+                ctx = RunCtx(params, c, training=False)
+                logits = self.model.forward(x, ctx)
+                loss, correct = Fn.cross_entropy(logits, y, c)
+                w = c.float()
+                accs[si][0].add_((loss * w).view(M, -1).sum(1))
+                accs[si][1].add_(correct.view(M, -1).sum(1))
+        if ns > 1:
+            for st in streams:
+                cur.wait_stream(st)
+        loss_tot, corr_tot = accs[0]
+        for la, ca in accs[1:]:
+            loss_tot = loss_tot + la
+            corr_tot = corr_tot + ca
         return loss_tot, corr_tot, n
 
 

@@ -123,8 +123,9 @@ class BasicBlock(Module):
         (planes) and its identity shortcut (fp32); 2: convs only (a downsample block follows);
         0: the pooling head only (fp32)."""
         link = _residual_link(self, x, ctx)
-        # split planes (fp32 GEMMs, Fn.batch_norm): bn1's output feeds conv2 only
-        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link, planes=2)
+        # bn1's output feeds conv2 only: its apply pass is deferred into conv2's halo loader where
+        # the shape allows (Fn.DeferredBN), planes only otherwise (fp32 GEMMs, Fn.batch_norm)
+        out = conv_bn(self.conv1, self.bn1, x, ctx, conv_link=link, planes=3)
         sc = x if self.down is None else _down(self.down, x, ctx, donor=link)
         return conv_bn(self.conv2, self.bn2, out, ctx, residual=sc, relu=True,
                        link=link if self.down is None else None, planes=out_planes)

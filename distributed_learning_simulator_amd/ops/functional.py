@@ -110,6 +110,30 @@ def _require_fp32(t, who: str):
         raise RuntimeError(f"{who}: a planes-only activation reached an op that reads fp32 values")
 
 
+class DeferredBN:
+    """A BatchNorm(+ReLU) output whose apply pass is deferred to its one consumer, a 3x3 stride-1
+    conv that applies it while staging its input (ops.hip.conv_halo_bn_fwd, csrc/conv_halo.hip
+    BNF): the normalised activation is never read back from HBM. The BN hands autograd the
+    planes-only alias of `yp` (batch_norm planes=3); in training the fused conv also writes the
+    planes and ReLU bits (its weight gradient and the BN backward read them). A consumer that
+    cannot fuse — or anything that needs the values first — calls `materialize()`, which runs
+    the ordinary apply pass into the same buffers. Bits are identical either way."""
+
+    __slots__ = ("x", "coef", "relu", "valid_rows", "yp", "mask", "write_out", "pending")
+
+    def __init__(self, x, coef, relu, valid_rows, yp, mask, write_out):
+        self.x, self.coef, self.relu, self.valid_rows = x, coef, relu, valid_rows
+        self.yp, self.mask, self.write_out = yp, mask, write_out
+        self.pending = True
+
+    def materialize(self):
+        if self.pending:
+            from . import hip
+
+            hip.bn_apply_only(self.x, self.coef, self.valid_rows, self.relu, self.yp, self.mask)
+            self.pending = False
+
+
 class _Conv(torch.autograd.Function):
     """Conv2d over the client dim. If the input carries more channels than the weight (image
     data stored zero-padded to 8 channels), the weight is zero-padded to match and only the
@@ -142,7 +166,28 @@ class _Conv(torch.autograd.Function):
         big = be is not ref and max(x[0].numel(), y_numel) * x.element_size() >= (1 << 31)
         if stats is not None:
             stats.dy_planes_ok = stats.dy_planes_ok and be.planes_fit(y_numel)
-        if stats is not None and be is not ref and x.dtype == torch.float32 and OPTIONS.bn_epilogue_stats and not big:
+        want_stats = stats is not None and be is not ref and x.dtype == torch.float32 and OPTIONS.bn_epilogue_stats \
+            and not big
+        y = None
+        defer = getattr(x, "_dls_bn_defer", None)
+        if defer is not None and defer.pending:
+            # a deferred BN input (DeferredBN): apply it in this conv's halo loader if it can
+            if (use_pl and stride == 1 and pad == 1 and KH == 3 and w.shape[3] == 3 and b is None
+                    and be.halo_bn_ok(x.shape, w)):
+                part = (torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
+                                    device=x.device) if want_stats else None)
+                y = be.conv_halo_bn_fwd(defer.x.view(x.shape), defer.coef, defer.relu, defer.valid_rows, w, w_split,
+                                        stats=part, stats_valid=stats.valid if want_stats else None,
+                                        yp=defer.yp if defer.write_out else None,
+                                        mask=defer.mask if defer.write_out else None)
+                if y is not None:
+                    defer.pending = False
+                    if want_stats:
+                        stats.part = part
+            defer.materialize()
+        if y is not None:
+            pass
+        elif want_stats:
             stats.part = torch.empty((K, be.conv_stats_parts(B * OH * OW), 2, w.shape[1]), dtype=torch.float32,
                                      device=x.device)
             y = be.conv_fwd(x, w, stride, pad, bias=b, stats=stats.part, stats_valid=stats.valid,
@@ -400,11 +445,23 @@ class _BN(torch.autograd.Function):
             # (inference passes — evaluation, GTG utilities — write no ReLU mask: no backward reads
             # it. Autograd is off inside Function.forward, so ask which inputs need a gradient)
             wm = any(ctx.needs_input_grad)
-            out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=wm, pre_stats=pre, planes=planes)
-            y, mean, rstd = out[:3]
-            mask = out[3] if wm else None
-            if planes:
-                yp = out[-1]
+            C8 = C % 8 == 0
+            if planes == 3 and not (OPTIONS.bn_fused_halo and residual is None and C8 and x3.is_contiguous()):
+                planes = 2  # (no deferral: apply now, planes only)
+            if planes == 3:
+                # deferred apply (DeferredBN): statistics + coefficients now; the consuming 3x3 conv
+                # applies them in its halo loader, or materialises the planes / ReLU bits first
+                coef, mean, rstd = be.bn_coef(x3, gamma, beta, valid_rows, pre_stats=pre)
+                y, yp = be.planes_buffer((K, x3.shape[1], C), x.device)
+                mask = torch.empty((K, x3.shape[1], C // 8), dtype=torch.uint8, device=x.device) if (wm and relu) else None
+                defer = DeferredBN(x3, coef, relu, valid_rows, yp, mask, write_out=wm)
+            else:
+                defer = None
+                out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=wm, pre_stats=pre, planes=planes)
+                y, mean, rstd = out[:3]
+                mask = out[3] if wm else None
+                if planes:
+                    yp = out[-1]
             if stats is not None:
                 stats.part = None
             if (wm and OPTIONS.bn_bwd_parts and x.dtype == torch.float32 and x3.is_contiguous()
@@ -421,7 +478,10 @@ class _BN(torch.autograd.Function):
         ctx.bnb = bnb
         yo = y.reshape(x.shape)
         if yp is not None:
-            _tag_planes(yo, yp.view((K, 2) + tuple(x.shape[1:])), planes == 2)
+            _tag_planes(yo, yp.view((K, 2) + tuple(x.shape[1:])), planes >= 2)
+        ctx.defer = None
+        if be is not ref and planes == 3:
+            yo._dls_bn_defer = ctx.defer = defer
         if bnb is not None:
             yo._dls_bnb = bnb
         return yo
@@ -431,6 +491,9 @@ class _BN(torch.autograd.Function):
         x3, y, mean, rstd, gamma = ctx.saved_tensors
         be = _be(dy)
         K, R, C = x3.shape
+        if ctx.defer is not None:  # (a consumer that never ran: the ReLU bits must exist now)
+            ctx.defer.materialize()
+            ctx.defer = None
         dy3 = dy.reshape(K, R, C).contiguous()
         if be is ref:
             dx, dgamma, dbeta, dpre = ref.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu)
@@ -471,7 +534,8 @@ def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False
                link: ResidualLink | None = None, stats: BNStats | None = None, planes: int = 0):
     """`planes` (fp32 native): 1 = the output also carries its split planes (`_dls_planes`) for
     the conv(s) that read it, 2 = the output is ONLY planes — for outputs read by nothing but
-    split-plane convs (e.g. a ResNet block's inner BN)."""
+    split-plane convs (e.g. a ResNet block's inner BN), 3 = as 2 with the apply pass deferred to
+    the ONE conv that reads it (DeferredBN: a 3x3 stride-1 halo conv applies it while staging)."""
     return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link, stats, planes)
 
 

@@ -578,9 +578,79 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
     assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
               eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx, _p(pre_stats),
-              0 if pre_stats is None else pre_stats.shape[1], _p(yp), int(planes != 2))
+              0 if pre_stats is None else pre_stats.shape[1], _p(yp), int(planes != 2), NULL, 1)
     out = (y, mean, rstd, mask) if with_mask else (y, mean, rstd)
     return out + (yp,) if planes else out
+
+
+def bn_coef(x, gamma, beta, valid_rows=None, eps=1e-5, pre_stats=None):
+    """BatchNorm statistics → per-(client, channel) (scale, shift) pairs [K, C, 2] fp32, with
+    nothing applied: the consumer conv applies them while staging its input (conv_halo_bn_fwd).
+    Same statistics / coefficient kernels (and bits) as bn_fwd."""
+    K, R, C = x.shape
+    assert x.dtype == F32 and x.is_contiguous()
+    g_cs, rep = _client_view(gamma, K)
+    mean = torch.empty((K, C), dtype=torch.float32, device=x.device)
+    rstd = torch.empty((K, C), dtype=torch.float32, device=x.device)
+    coef = torch.empty((K, C, 2), dtype=torch.float32, device=x.device)
+    ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    if pre_stats is not None:
+        assert pre_stats.dtype == torch.float32 and pre_stats.is_contiguous()
+        assert pre_stats.shape[0] == K and pre_stats.shape[2:] == (2, C), pre_stats.shape
+    _C.bn_fwd(_p(x), _p(gamma), _p(beta), NULL, NULL, _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, 0, eps, rep, _p(ws),
+              NULL, _p(_bn_counters(K, x.device)), 1, _s(), C, _p(pre_stats),
+              0 if pre_stats is None else pre_stats.shape[1], NULL, 1, _p(coef), 0)
+    return coef, mean, rstd
+
+
+def halo_bn_ok(shape, w) -> bool:
+    """conv_halo_bn_fwd serves a [K, B, H, W, C] fp32 input and a 3x3 weight of this shape."""
+    K, B, H, W, C = shape
+    return (w.dim() == 5 and w.shape[2] == 3 and w.shape[3] == 3 and w.shape[4] == C
+            and bool(_C.conv_halo_bn_supported(B, H, W, C, w.shape[1])))
+
+
+def bn_apply_only(x, coef, valid_rows, relu: bool, yp, mask=None):
+    """Materialise a deferred BN: relu?(coef-scaled x) → split planes yp [K, 2, R, C] (+ ReLU bits)."""
+    K, R, C = x.shape
+    assert x.dtype == F32 and x.is_contiguous() and coef.shape == (K, C, 2)
+    assert yp.shape == (K, 2, R, C) and yp.dtype == BF16 and yp.is_contiguous()
+    if mask is not None:
+        assert mask.shape == (K, R, C // 8) and C % 8 == 0
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    _C.bn_apply_only(_p(x), _p(coef), _p(vr), K, R, C, int(relu), _p(yp), _p(mask), _s())
+
+
+def conv_halo_bn_fwd(x, coef, relu: bool, valid_rows, w, w_split, stats=None, stats_valid=None, yp=None, mask=None):
+    """3x3 / stride-1 / pad-1 fp32 conv of relu?(BN(x)) with the BN applied in the halo loader
+    (csrc/conv_halo.hip BNF): x [K, B, H, W, C] is the RAW previous conv output, `coef` [K, C, 2]
+    its BN (scale, shift) pairs (bn_coef), `valid_rows` [K] the BN's valid rows (zero past them).
+    `yp` [K, 2, B·H·W, C] / `mask` [K, B·H·W, C/8] (training): the normalised activation's split
+    planes and ReLU bits are written as well (the conv's weight gradient and the BN's backward
+    read them). Returns y [K, B, H, W, N], or None where no halo kernel serves the shape."""
+    K, B, H, W, C = x.shape
+    Kw, N, KH, KW, Ci = w.shape
+    if not (x.dtype == F32 and x.is_contiguous() and KH == 3 and KW == 3 and Ci == C and w_split is not None):
+        return None
+    assert coef.shape == (K, C, 2) and coef.dtype == F32 and coef.is_contiguous()
+    w_cs, rep = _client_view(w, K)
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split, w)
+    y = torch.empty((K, B, H, W, N), dtype=F32, device=x.device)
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    if stats is not None:
+        assert stats.shape == (K, conv_stats_parts(B * H * W), 2, N) and stats.is_contiguous()
+        if stats_valid is not None:
+            stats_valid = stats_valid.to(torch.int32).contiguous()
+    if yp is not None:
+        assert yp.shape == (K, 2, B * H * W, C) and yp.dtype == BF16 and yp.is_contiguous()
+    if mask is not None:
+        assert mask.shape == (K, B * H * W, C // 8) and mask.dtype == torch.uint8 and mask.is_contiguous()
+    ok = _C.conv_halo_bn_fwd(_p(x), x.stride(0), _p(coef), int(relu), _p(vr), ws_p, ws_cs, ws_plane, rep, _p(y),
+                             y.stride(0), K, B, H, W, C, N, _p(stats), _p(stats_valid), _s(), _p(yp), _p(mask))
+    if ok:
+        planes_launches["fwd_bn_fused"] += 1
+    return y if ok else None
 
 
 def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None,

@@ -48,6 +48,9 @@ class RuntimeOptions:
     """BN forward statistics from the producing conv's epilogue (off: BN's own statistics pass)."""
     bn_bwd_parts: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_BWD_PARTS", True))
     """BN backward partial sums from the consuming conv's dgrad epilogue (off: own reduction)."""
+    bn_fused_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_HALO", True))
+    """Inference: a BN(+ReLU) whose only reader is a 3x3 stride-1 conv is applied in that conv's
+    halo loader (ops.functional.bn_relu_conv3x3_eval; off: BN apply pass + plane conv)."""
     dense_stats_cache: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_STATS_CACHE", False))
     """DenseNet blocks compute each channel's statistics once (measured no faster: off)."""
     bn_fused_coef: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_COEF", False))
@@ -62,6 +65,9 @@ class RuntimeOptions:
     """HIP-graph replay of whole training steps (off: eager steps)."""
     max_graphs: int = dataclasses.field(default_factory=lambda: _env_int("DLS_MAX_GRAPHS", 2))
     """Captured step graphs kept per trainer (each owns a private memory pool)."""
+    eval_max_images: int = dataclasses.field(default_factory=lambda: _env_int("DLS_EVAL_MAX_IMAGES", 8192))
+    """Images per evaluation launch (M models x batches): larger launches fill the GPU better and
+    cost activation memory."""
     shared_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_SHARED_PLANES", False))
     """Shared-model steps (sign-SGD / sync-SGD): every client reads the one shared row's weight
     planes (rep = K) and its activations' planes (off: register-split GEMMs)."""

@@ -227,3 +227,83 @@ def test_sign_sgd_resnet18_planes_shared_weights(hip, tmp_path, monkeypatch):
     fa, fb = flips(ga, gc), flips(gb, gc)
     assert fa <= 2 * fb + 1e-4, (fa, fb)
     assert fa < 1e-2, fa
+
+
+@pytest.mark.parametrize("cfg_name,overrides", [
+    ("fed_paq/cifar10.yaml", {"model_name": "LeNet5", "worker_number": 4, "algorithm_kwargs.random_client_number": 4}),
+    ("fed_obd/cifar10.yaml", {"model_name": "LeNet5", "worker_number": 4, "algorithm_kwargs.random_client_number": 4,
+                              "algorithm_kwargs.second_phase_epoch": 1}),
+    ("fed_obd_sq/cifar100.yaml", {"model_name": "LeNet5", "worker_number": 4,
+                                  "algorithm_kwargs.random_client_number": 4, "algorithm_kwargs.second_phase_epoch": 1}),
+])
+def test_quantised_upload_path_equals_cpu_given_uploads(hip, tmp_path, cfg_name, overrides):
+    """The 2e-2 GPU-vs-CPU bounds of the lossy methods (test_methods_match_cpu) come from the
+    clients' fp32 training drift alone: given the SAME uploads — every real upload of a GPU
+    session — the GPU quantiser writes the CPU oracle's wire bytes exactly, and the server's
+    dequantise-inside-the-fp64-accumulation kernel adds what the CPU oracle adds (to fp64
+    summation-order rounding, ≤ 1e-12 relative)."""
+    from distributed_learning_simulator_amd.ops import compress, fl
+    from distributed_learning_simulator_amd.topology import endpoints as E
+
+    nnadq = cfg_name.startswith("fed_obd/")
+    cls = E.NNADQClientEndpoint if nnadq else E.StochasticQuantClientEndpoint
+    q_orig, a_orig = cls.quantize, compress.QuantPayload.accumulate
+    twins = {}  # id(GPU payload) -> CPU oracle payload of the same upload rows
+    stats = {"uploads": 0, "accumulates": 0, "worst": 0.0}
+
+    def q_spy(self, msg, seed):
+        rows = msg.data.detach().cpu()
+        mask = msg.extra.get("segment_mask")
+        mask = None if mask is None else mask.cpu()
+        cids = list(msg.client_ids)
+        out = q_orig(self, msg, seed)
+        meta_c = compress.LayoutMeta.of(self.ctx.layout, "cpu")
+        if nnadq:
+            pc = compress.pack_nnadq(rows, meta_c, self.weight, mask)
+        else:
+            pc = compress.pack_stochastic(rows, meta_c, fl.row_seeds(seed, cids), mask, self.levels)
+        assert torch.equal(pc.codes, out.payload.codes.cpu()), "GPU wire bytes differ from the CPU oracle's"
+        assert torch.equal(pc.bits, out.payload.bits.cpu())
+        twins[id(out.payload)] = pc
+        stats["uploads"] += 1
+        return out
+
+    def a_spy(self, acc, w):
+        pc = twins.get(id(self))
+        if pc is None or not acc.is_cuda:
+            return a_orig(self, acc, w)
+        before = acc.detach().cpu().clone()
+        a_orig(self, acc, w)
+        exp = before.clone()
+        a_orig(pc, exp, w.detach().cpu().double())
+        got = acc.detach().cpu()
+        rel = ((got - exp).abs().max() / exp.abs().max().clamp(min=1e-300)).item()
+        stats["worst"] = max(stats["worst"], rel)
+        stats["accumulates"] += 1
+
+    ov = {"round": 1, "epoch": 1, "dataset_kwargs.scale": 0.02, **overrides}
+    cls.quantize, compress.QuantPayload.accumulate = q_spy, a_spy
+    try:
+        _run(cfg_name, ov, tmp_path / "g", "cuda")
+    finally:
+        cls.quantize, compress.QuantPayload.accumulate = q_orig, a_orig
+    assert stats["uploads"] > 0 and stats["accumulates"] > 0, stats
+    assert stats["worst"] < 1e-12, stats
+
+
+def test_resnet18_training_fused_bn_halo_bitwise(hip, tmp_path):
+    """Training with bn1 applied inside conv2's halo loader (Fn.DeferredBN; the fused conv also
+    writes the planes and ReLU bits the backward reads) is bitwise the run without the fusion,
+    and the fused kernels ran."""
+    from distributed_learning_simulator_amd.ops import hip as H
+
+    ov = {"round": 1, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
+          "learning_rate": 0.01}
+    H.planes_launches.clear()
+    with options.override(bn_fused_halo=True):
+        a, ra = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    assert H.planes_launches["fwd_bn_fused"] > 0, H.planes_launches
+    with options.override(bn_fused_halo=False):
+        b, rb = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    assert torch.equal(a.server.global_parameter, b.server.global_parameter)
+    assert _losses(ra) == _losses(rb)

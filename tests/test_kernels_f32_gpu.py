@@ -750,3 +750,82 @@ def test_layernorm_planes_feed_plane_linear(hip):
     out = hip.linear_fwd(y.reshape(K, B * L, D), w, bias, w_split=ws, x_planes=yp.reshape(K, 2, B * L, D))
     assert hip.planes_launches["linear_fwd"] == before + 1
     _close(out, torch.einsum("knd,kod->kno", _d(y).reshape(K, B * L, D), _d(w)) + _d(bias)[:, None])
+
+
+@pytest.mark.parametrize("case", [
+    # K, B, H (= W), C, N, relu, valid samples of client 0 (None: all): the three halo shapes
+    (2, 2, 32, 64, 64, True, None),
+    (3, 3, 16, 128, 128, True, 2),
+    (2, 4, 8, 256, 256, False, 3),
+    (1, 6, 8, 128, 256, True, None),   # two N tiles per row block
+])
+def test_halo_conv_with_fused_bn_input(hip, case):
+    """conv_halo_bn_fwd (csrc/conv_halo.hip BNF: BatchNorm(+ReLU) applied in the halo loader)
+    equals the unfused BN apply → split planes → halo conv bit for bit (same coefficients, same
+    fma / max / split per element), output and its epilogue statistics alike; rows of invalid
+    samples read as zero; and both agree with the fp64 oracle of conv(relu(bn(x)))."""
+    K, B, H, C, N, relu, nv = case
+    torch.manual_seed(3)
+    x = _f(K, B, H, H, C, scale=2.0) + 0.5
+    gamma, beta = _f(K, C) * 0.5 + 1.0, _f(K, C) * 0.2
+    w = _f(K, N, 3, 3, C, scale=0.05)
+    n = N * 9 * C
+    wpl = torch.empty((K, 2, n), dtype=torch.bfloat16, device=DEV)
+    hip.split_rows(w.reshape(K, n).contiguous(), wpl)
+    ws = wpl[:, 0].unflatten(1, (N, 3, 3, C))
+    valid = None if nv is None else torch.tensor([nv] + [B] * (K - 1), dtype=torch.int32, device=DEV)
+    vrows = None if valid is None else valid * (H * H)
+    x3 = x.reshape(K, -1, C)
+    # unfused: BN apply writing planes only, then the plane (halo) conv with epilogue statistics
+    y, mean, rstd, yp = hip.bn_fwd(x3, gamma, beta, vrows, relu, None, planes=2)
+    parts = hip.conv_stats_parts(B * H * H)
+    st_a = torch.empty((K, parts, 2, N), device=DEV)
+    ref_out = hip.conv_fwd(y.view(K, B, H, H, C), w, 1, 1, w_split=ws, x_planes=yp.view(K, 2, B, H, H, C),
+                           stats=st_a, stats_valid=valid)
+    # fused
+    coef, mean2, rstd2 = hip.bn_coef(x3, gamma, beta, vrows)
+    assert torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+    st_b = torch.empty_like(st_a)
+    out = hip.conv_halo_bn_fwd(x, coef, relu, vrows, w, ws, stats=st_b, stats_valid=valid)
+    assert out is not None
+    assert torch.equal(out, ref_out), (out - ref_out).abs().max()
+    assert torch.equal(st_a, st_b)
+    # fp64 oracle
+    xd = _d(x).view(K, -1, C)
+    rows = xd.shape[1]
+    keep = torch.ones(K, rows, 1, dtype=torch.float64)
+    if vrows is not None:
+        keep = (torch.arange(rows).view(1, rows) < vrows.cpu().view(K, 1)).double().unsqueeze(-1)
+    cnt = keep.sum(1)
+    mu = (xd * keep).sum(1) / cnt
+    var = (((xd - mu[:, None]) ** 2) * keep).sum(1) / cnt
+    z = (xd - mu[:, None]) / torch.sqrt(var[:, None] + 1e-5) * _d(gamma)[:, None] + _d(beta)[:, None]
+    if relu:
+        z = z.clamp(min=0)
+    z = (z * keep).view(K, B, H, H, C)
+    _close(out, ref.conv_fwd(z, _d(w), 1, 1))
+
+
+def test_resnet18_eval_fused_bn_equals_unfused(hip):
+    """The batched utility evaluation (GTG-Shapley's cost) with bn1 fused into conv2's halo loader
+    gives bitwise the same losses and correct counts as the unfused evaluation, and the fused
+    kernels actually ran."""
+    from distributed_learning_simulator_amd import options
+    from distributed_learning_simulator_amd.data.datasets import create_dataset_collection
+    from distributed_learning_simulator_amd.engine.trainer import CohortTrainer, HyperParameter
+    from distributed_learning_simulator_amd.models.zoo import build_model
+
+    dev = torch.device(DEV)
+    dc = create_dataset_collection("CIFAR10", {"n_train": 256, "n_test": 700}, 0, dev, torch.float32, image_channels=8)
+    model = build_model("ResNet18", dc.spec)
+    tr = CohortTrainer(model, dc, HyperParameter(epoch=1, batch_size=64), dev, torch.float32, capacity=1)
+    g = torch.Generator().manual_seed(0)
+    rows = torch.stack([model.layout.init_flat(g) for _ in range(3)]).to(dev)
+    hip.planes_launches.clear()
+    with options.override(bn_fused_halo=True):
+        lf, cf, n = tr.evaluate(rows, max_images=1024)
+    assert hip.planes_launches["fwd_bn_fused"] > 0, hip.planes_launches
+    with options.override(bn_fused_halo=False):
+        lu, cu, _ = tr.evaluate(rows, max_images=1024)
+    assert torch.equal(cf, cu)
+    assert torch.equal(lf, lu), (lf - lu).abs().max()

@@ -1,6 +1,6 @@
-"""1 rank ≡ 2 ranks on the GPU.
+"""1 rank ≡ 2 ranks ≡ 4 ranks on the GPU.
 
-Two rank processes share the one GPU of the box (gloo carries the collectives: RCCL needs a GPU
+Two (four) rank processes share the one GPU of the box (gloo carries the collectives: RCCL needs a GPU
 per rank; the code path above the communicator is the RCCL one). Each rank trains its half of
 the clients with the native kernels; FedAvg reduces the fp64 accumulators across ranks. With
 deterministic kernels (split-K chosen per client, ordered folds, no atomics) every client's
@@ -47,7 +47,10 @@ def _worker(rank, world, port, tmp, q):
     commmod.shutdown()
 
 
-def test_two_ranks_on_one_gpu_equal_one_rank(hip, tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_on_one_gpu_equal_one_rank(hip, tmp_path, world):
+    """6 clients dealt round-robin over `world` rank processes (3 / 2 / 1-2 clients each, the
+    small-cohort launch rules of an 8-GPU round's per-rank share)."""
     from distributed_learning_simulator_amd.config import config_from_dict
     from distributed_learning_simulator_amd.parallel.comm import Comm
     from distributed_learning_simulator_amd.session import Session
@@ -60,15 +63,16 @@ def test_two_ranks_on_one_gpu_equal_one_rank(hip, tmp_path):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path / f"r{r}"), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path / f"r{r}"), q)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    g0, g1 = torch.from_numpy(out[0][1]), torch.from_numpy(out[1][1])
-    assert torch.equal(g0, g1), "server replicas diverged"
+    g0 = torch.from_numpy(out[0][1])
+    for r in range(1, world):
+        assert torch.equal(g0, torch.from_numpy(out[r][1])), f"server replica {r} diverged"
     diff = (g0 - ref).abs()
     # bitwise up to rare fp64-order ties at the fp32 cast
     assert (diff > 0).float().mean().item() < 1e-5, (diff > 0).sum()
