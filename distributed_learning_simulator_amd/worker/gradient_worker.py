@@ -31,6 +31,7 @@ from ..message import FlatParameterMessage
 from ..ops import fl
 from ..options import OPTIONS
 from ..server.aggregation_server import AggregationServer
+from ..utils.logging import get_logger
 from .aggregation_worker import AggregationWorker
 
 
@@ -123,25 +124,41 @@ class GradientWorker(AggregationWorker):
         for s in range(S):
             acc = self._new_accumulator(P, tr.device)
             if sched is not None and s < sched.steps:
-                for w0 in range(0, len(local), cap):
+                w0 = 0
+                while w0 < len(local):
                     w1 = min(len(local), w0 + cap)
                     K = w1 - w0
                     idx = sched.idx[s, w0:w1]
                     valid = sched.counts[s, w0:w1]
-                    x = tr._gather(sess.dc.train, idx)
-                    y = sess.dc.train.gather_labels(idx)
-                    loss, correct = tr.forward_loss(K, x, y, valid, shared=True)
-                    loss.sum().backward()
+                    try:
+                        x = tr._gather(sess.dc.train, idx)
+                        y = sess.dc.train.gather_labels(idx)
+                        loss, correct = tr.forward_loss(K, x, y, valid, shared=True)
+                        loss.sum().backward()
+                        with torch.no_grad():
+                            g = b.grad[:K]
+                            if wd:  # compute_gradient (`gradient_worker.py:13-26`)
+                                g.add_(theta0, alpha=wd)
+                            payload = self._process_gradient(g)
+                    except torch.OutOfMemoryError:
+                        # the planned wave did not fit (the activation probe measures one client;
+                        # allocator fragmentation at many clients can exceed it): halve the wave
+                        # for the rest of the run and redo this one — nothing of it was accumulated
+                        if cap == 1:
+                            raise
+                        x = y = loss = correct = g = None
+                        cap = tr.capacity = max(1, cap // 2)
+                        torch.cuda.empty_cache()
+                        get_logger().warning("wave of %d clients ran out of memory: waves of %d from here", K, cap)
+                        continue
                     with torch.no_grad():
-                        g = b.grad[:K]
-                        if wd:  # compute_gradient (`gradient_worker.py:13-26`)
-                            g.add_(theta0, alpha=wd)
-                        self._accumulate(acc, self._process_gradient(g), sched.active[s, w0:w1], sizes[w0:w1])
+                        self._accumulate(acc, payload, sched.active[s, w0:w1], sizes[w0:w1])
                         vf = valid.float()
                         ee = min(e, epochs - 1)
                         stats.loss_sum[ee, w0:w1] += loss.detach() * vf
                         stats.correct[ee, w0:w1] += correct
                         stats.samples[ee, w0:w1] += vf
+                    w0 = w1
             self._reduce(acc)
             with torch.no_grad():
                 grad = self._finalize(acc)
