@@ -388,6 +388,7 @@ def workload_config(args, rounds: int) -> dict:
             return {}
         ev = sv.evaluations_per_round.get(max(sv.evaluations_per_round, default=0), 0)
         return {"subset_evaluations_last_round": ev, "gtg_iterations_last_round": sv.iterations_last,
+                "gtg_converged": getattr(sv, "converged_last", None), "gtg_max_iterations": sv.max_iterations,
                 "subset_evaluations_per_s": ev / s_per_round, "utility_images_per_evaluation": sess.dc.spec.n_test}
 
     return {"config": {**cfg, **common}, "extra": gtg_extra,

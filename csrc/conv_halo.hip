@@ -45,8 +45,13 @@ __device__ __forceinline__ void hwait_vm() {
 // per-channel (scale, shift) and ReLU, splits to hi / lo and writes the same 16-B LDS slots the
 // plane DMA would fill — bit-identical operands to BN-apply-then-planes, without the normalised
 // tensor ever reaching HBM. Forward (row-major B) with one halo buffer only.
-template <int IMG, int TH, int TW, int BN, int WM, int WN, bool BKM, int MINW, int HB, int NBS, bool BNF = false>
+// BNM: 0 plain; 1 fused BN (ResNet block: bn_x contiguous [.., C], training writes split planes +
+// ReLU bits); 2 fused BN over a DenseNet channel prefix (bn_x rows at stride ldx inside the block
+// buffer, bn_c ≤ C real channels — the rest of the 32-channel chunk stages as zero — training
+// writes the normalised activation in fp32 at row stride bn_ldy)
+template <int IMG, int TH, int TW, int BN, int WM, int WN, bool BKM, int MINW, int HB, int NBS, int BNM = 0>
 __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTParams p) {
+  constexpr bool BNF = BNM != 0, DENSE = BNM == 2;
   static_assert((HB == 2 && NBS == 3) || (HB == 1 && (NBS == 2 || NBS == 3)), "pipeline shape");
   static_assert(!BNF || (HB == 1 && !BKM), "fused BN input: forward, one halo buffer");
   constexpr int BM = IMG * TH * TW;
@@ -104,6 +109,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   // (BNF) rows of samples past the BN's valid rows read as zero, like the padding; h_ctr: the halo
   // row is one of this row block's own output pixels (written out when bn_yp is set)
   bool h_bnok[HI], h_ctr[HI];
+  int h_pix[DENSE ? HI : 1];  // (DENSE: the halo row's pixel index, for the fp32 activation rows)
   const int bn_rows = BNF ? (p.bn_valid ? p.bn_valid[client] : p.B * p.H * p.W) : 0;
 #pragma unroll
   for (int i = 0; i < HI; ++i) {
@@ -118,6 +124,7 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
     h_ch[i] = lc * 8;
     h_bnok[i] = !BNF || pix < bn_rows;
     h_ctr[i] = ok && hh >= 1 && hh <= TH && ww >= 1 && ww <= TW;
+    if constexpr (DENSE) h_pix[i] = pix;
   }
   // ---- weight loader (as conv_pl.hip): row-major rows (i·NW + w)·16 + lane/4; k-major k-rows
   // (i·NW + w)·RPI + lane/CPR with the 32-element segment swizzle of the k-major image
@@ -145,7 +152,11 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   const float* bcoef = BNF ? p.bn_coef + (long)client * p.C * 2 : nullptr;
   const long bn_rc = (long)p.B * p.H * p.W * p.C;  // (elements of one plane of one client)
   bf16_t* bn_yph = (BNF && p.bn_yp && n0 == 0) ? p.bn_yp + (long)client * 2 * bn_rc : nullptr;
-  uint8_t* bn_mk = (BNF && p.bn_mask && n0 == 0) ? p.bn_mask + (long)client * (bn_rc >> 3) : nullptr;
+  uint8_t* bn_mk = (BNF && p.bn_mask && n0 == 0)
+                      ? p.bn_mask + (long)client * ((DENSE ? (long)p.M * p.bn_ldy : bn_rc) >> 3)
+                      : nullptr;
+  float* bn_ny = (DENSE && p.bn_y && n0 == 0) ? p.bn_y + (long)client * p.bn_y_cs : nullptr;
+  const int bn_creal = DENSE ? p.bn_c : p.C;
   auto issue_halo = [&](int c, int buf) {
     const bool live = c < nchunks;
     unsigned char* Hs = smem + H_OFF + buf * 2 * H_PL;
@@ -159,8 +170,12 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
         const bool okv = ok && h_bnok[i];
         const int e = (ok ? h_off[i] : 0) + c * 32;
         const int ch = c * 32 + h_ch[i];
-        const float4 x0 = *reinterpret_cast<const float4*>(bxc + e);
-        const float4 x1 = *reinterpret_cast<const float4*>(bxc + e + 4);
+        // (DENSE) real channels of the lane's 8: ≥ 8 all, 4 the first half (bn_c % 4 == 0), ≤ 0
+        // none — channels past the prefix are other layers' (maybe unwritten) slots: never read
+        const int cv = bn_creal - ch;
+        float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+        if (!DENSE || cv > 0) x0 = *reinterpret_cast<const float4*>(bxc + e);
+        if (!DENSE || cv >= 8) x1 = *reinterpret_cast<const float4*>(bxc + e + 4);
         const float4* cf = reinterpret_cast<const float4*>(bcoef + 2 * ch);  // (scale, shift) pairs
         const float4 c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3];
         float v[8] = {fmaf(x0.x, c0.x, c0.y), fmaf(x0.y, c0.z, c0.w), fmaf(x0.z, c1.x, c1.y), fmaf(x0.w, c1.z, c1.w),
@@ -168,14 +183,14 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           if (p.bn_relu) v[j] = fmaxf(v[j], 0.f);
-          if (!okv) v[j] = 0.f;
+          if (!okv || (DENSE && cv <= (j < 4 ? 0 : 4))) v[j] = 0.f;
         }
         uint32_t hi[4], lo[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) split_pair(v[2 * j], v[2 * j + 1], hi[j], lo[j]);
         *reinterpret_cast<uint4*>(d + lane * 16) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
         *reinterpret_cast<uint4*>(d + H_PL + lane * 16) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-        if (bn_yph && inimg && h_ctr[i]) {  // this row block's own pixels: planes + ReLU bits out
+        if (!DENSE && bn_yph && inimg && h_ctr[i]) {  // this row block's own pixels: planes + ReLU bits out
           *reinterpret_cast<uint4*>(bn_yph + e) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
           *reinterpret_cast<uint4*>(bn_yph + bn_rc + e) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
           if (bn_mk) {
@@ -183,6 +198,19 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
 #pragma unroll
             for (int j = 0; j < 8; ++j) m |= (v[j] > 0.f ? 1u : 0u) << j;
             bn_mk[e >> 3] = (uint8_t)m;
+          }
+        }
+        if constexpr (DENSE) {
+          if (bn_ny && inimg && h_ctr[i] && cv > 0) {  // own pixels: the fp32 activation (bn_apply's bits)
+            const long o = (long)h_pix[i] * p.bn_ldy + ch;
+            *reinterpret_cast<float4*>(bn_ny + o) = make_float4(v[0], v[1], v[2], v[3]);
+            if (cv >= 8) *reinterpret_cast<float4*>(bn_ny + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            if (bn_mk) {  // (bn_ldy % 8 == 0: whole bytes) the ReLU bits bn_apply would have written
+              uint32_t m = 0;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) m |= (v[j] > 0.f ? 1u : 0u) << j;
+              bn_mk[o >> 3] = (uint8_t)m;
+            }
           }
         }
       } else {
@@ -329,11 +357,11 @@ void launch_halo(const ConvNTParams& p, int K, hipStream_t s) {
                        dim3(WM * WN * 64), 0, s, p);
 }
 
-template <int IMG, int TH, int TW, int BN, int WM, int WN, int NBS>
+template <int IMG, int TH, int TW, int BN, int WM, int WN, int NBS, int BNM = 1>
 void launch_halo_bnf(const ConvNTParams& p, int K, hipStream_t s) {
   const int tilesM = IMG == 1 ? p.B * (p.OH / TH) : p.B / IMG;
   const int grid = K * tilesM * cdiv(p.N, BN);
-  hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, false, 1, 1, NBS, true>), dim3(grid),
+  hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, false, 1, 1, NBS, BNM>), dim3(grid),
                      dim3(WM * WN * 64), 0, s, p);
 }
 
@@ -348,9 +376,19 @@ void conv_halo_set_variant(int v) { g_halo_variant = v; }
 // one of the compiled tile shapes fits this launch: full-width row blocks of 256 GEMM rows
 static int halo_config(const ConvNTParams& p) {
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.pad_w != 1 || p.dil != 1) return -1;
-  if (p.OH != p.H || p.OW != p.W || p.out_s > 1 || p.C % 32 || p.N % 8 || p.ldx % 8 || p.R != 9 * p.C) return -1;
+  const bool dense = p.bn_x != nullptr && p.bn_c > 0;
+  if (p.OH != p.H || p.OW != p.W || p.out_s > 1 || p.C % 32 || p.N % (dense ? 4 : 8) || p.ldx % 8 || p.R != 9 * p.C)
+    return -1;
   if ((p.x_lo == 0 && p.bn_x == nullptr) || p.wsplit == nullptr) return -1;
-  if (p.bn_x != nullptr && (p.b_kmajor || p.ldx != p.C)) return -1;
+  if (p.bn_x != nullptr && (p.b_kmajor || (!dense && p.ldx != p.C))) return -1;
+  if (dense) {  // DenseNet growth conv (N = growth ≤ 32): 32-wide N tiles, 4 waves of 64 x 32
+    if (p.N > 32 || p.bn_c % 4 || p.bn_c > p.C || p.bn_c > p.ldx || (p.bn_y && p.bn_ldy % 4)) return -1;
+    if (p.bn_mask && (!p.bn_y || p.bn_ldy % 8 || p.bn_c % 8)) return -1;
+    if (p.OW == 32 && p.OH % 8 == 0) return 4;            // 1 × 8 × 32
+    if (p.OW == 16 && p.OH == 16) return 5;               // 1 × 16 × 16
+    if (p.OW == 8 && p.OH == 8 && p.B % 4 == 0) return 6;  // 4 × 8 × 8
+    return -1;
+  }
   if (p.OW == 32 && p.OH % 8 == 0 && p.N <= 64) return 0;  // 1 × 8 × 32, BN 64
   if (p.OW == 16 && p.OH == 16) return 1;                   // 1 × 16 × 16, BN 128
   if (p.OW == 8 && p.OH == 8 && p.B % 2 == 0) return 2;     // 2 × 8 × 8, BN 128
@@ -377,11 +415,16 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
     switch (cfg) {
       case 0: launch_halo_bnf<1, 8, 32, 64, 4, 2, 3>(p, K, s); break;
       case 1: launch_halo_bnf<1, 16, 16, 128, 4, 2, 2>(p, K, s); break;
-      default: launch_halo_bnf<2, 8, 8, 128, 4, 2, 2>(p, K, s); break;
+      case 2: launch_halo_bnf<2, 8, 8, 128, 4, 2, 2>(p, K, s); break;
+      case 4: launch_halo_bnf<1, 8, 32, 32, 4, 1, 3, 2>(p, K, s); break;  // 62 KB
+      case 5: launch_halo_bnf<1, 16, 16, 32, 4, 1, 3, 2>(p, K, s); break;  // 62 KB
+      case 6: launch_halo_bnf<4, 8, 8, 32, 4, 1, 3, 2>(p, K, s); break;    // 78 KB
+      default: return false;
     }
     return true;
   }
   const int v = g_halo_variant >= 0 ? g_halo_variant : (cfg == 2 ? 2 : 1);
+  if (cfg > 3) return false;
   switch (cfg * 3 + v) {
     case 0: launch_halo<1, 8, 32, 64, 4, 1, 2, 3>(p, K, s); break;    // 120 KB, 4 waves
     case 1: launch_halo<1, 8, 32, 64, 4, 2, 1, 3>(p, K, s); break;    // 73 KB, 8 waves
@@ -410,14 +453,12 @@ bool conv_halo_bn_supported(int B, int H, int W, int C, int N) {
   return g_halo_mode != 0 && g_halo_variant < 0 && cfg >= 0 && cfg != 3 && (long)B * H * W * C * 4 < (1L << 31);
 }
 
-bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, const int* valid_rows,
-                      const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y, long y_cs, int K, int B,
-                      int H, int W, int C, int N, float* stats, const int* stats_valid, hipStream_t s,
-                      bf16_t* yp, uint8_t* mask) {
+static ConvNTParams halo_bn_params(const float* x, long x_cs, int ldx, const float* coef, int relu,
+                                   const int* valid_rows, const bf16_t* wsplit, long ws_cs, long ws_plane, int rep,
+                                   float* y, long y_cs, int ldy, int B, int H, int W, int C, int N, float* stats,
+                                   const int* stats_valid) {
   ConvNTParams p{};
   p.f32 = 1;
-  p.bn_yp = yp;
-  p.bn_mask = mask;
   p.bn_x = x;
   p.bn_x_cs = x_cs;
   p.bn_coef = coef;
@@ -434,14 +475,52 @@ bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, co
   p.M = B * H * W; p.N = N; p.R = 9 * C;
   p.wKH = 3; p.wKW = 3; p.kh_off = 2; p.kw_off = 2; p.kh_step = 1; p.kw_step = 1;
   p.out_s = 1;
-  p.ldx = C; p.ldy = N;
+  p.ldx = ldx; p.ldy = ldy;
   p.fd_ohw = make_fastdiv((uint32_t)(H * W));
   p.fd_ow = make_fastdiv((uint32_t)W);
   p.fd_kwc = make_fastdiv((uint32_t)(3 * C));
   p.fd_c = make_fastdiv((uint32_t)C);
   p.stats = stats;
   p.stats_valid = stats_valid;
+  return p;
+}
+
+bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, const int* valid_rows,
+                      const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y, long y_cs, int K, int B,
+                      int H, int W, int C, int N, float* stats, const int* stats_valid, hipStream_t s,
+                      bf16_t* yp, uint8_t* mask) {
+  ConvNTParams p = halo_bn_params(x, x_cs, C, coef, relu, valid_rows, wsplit, ws_cs, ws_plane, rep, y, y_cs, N, B, H,
+                                  W, C, N, stats, stats_valid);
+  p.bn_yp = yp;
+  p.bn_mask = mask;
   const long wb = (ws_plane + (long)N * p.R) * 2;
   if (wb >= (long)OOB_OFF || (long)p.M * C * 4 >= (1L << 31)) return false;
+  return conv_halo(p, K, s);
+}
+
+bool conv_halo_bn_dense_supported(int B, int H, int W, int C, int N) {
+  ConvNTParams p{};
+  p.bn_x = reinterpret_cast<const float*>(16);  // (shape check only)
+  p.wsplit = reinterpret_cast<const bf16_t*>(16);
+  p.bn_c = 4;
+  p.B = B; p.H = H; p.W = W; p.C = C; p.OH = H; p.OW = W; p.KH = 3; p.KW = 3;
+  p.stride = 1; p.pad = 1; p.pad_w = 1; p.dil = 1; p.N = N; p.R = 9 * C; p.ldx = C; p.out_s = 1;
+  return g_halo_mode != 0 && g_halo_variant < 0 && halo_config(p) >= 4;
+}
+
+bool conv_halo_bn_dense_fwd(const float* x, long x_cs, int ldx, int creal, const float* coef, int relu,
+                            const int* valid_rows, const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y,
+                            long y_cs, int ldy, int K, int B, int H, int W, int C, int N, float* stats,
+                            const int* stats_valid, float* ny, long ny_cs, int ldny, uint8_t* mask, hipStream_t s) {
+  ConvNTParams p = halo_bn_params(x, x_cs, ldx, coef, relu, valid_rows, wsplit, ws_cs, ws_plane, rep, y, y_cs, ldy, B,
+                                  H, W, C, N, stats, stats_valid);
+  p.bn_c = creal;
+  p.bn_y = ny;
+  p.bn_y_cs = ny_cs;
+  p.bn_ldy = ldny;
+  p.bn_mask = mask;
+  const long wb = (ws_plane + (long)N * p.R) * 2;
+  if (wb >= (long)OOB_OFF || (long)p.M * ldx * 4 >= (1L << 31)) return false;
+  if (halo_config(p) < 4) return false;
   return conv_halo(p, K, s);
 }

@@ -119,6 +119,14 @@ struct ConvNTParams {
   // pass would have written for the conv's weight gradient and the BN's backward
   bf16_t* bn_yp;
   uint8_t* bn_mask;
+  // (DenseNet channel prefix, bn_c > 0) bn_x rows at stride ldx inside the block buffer, only the
+  // first bn_c ≤ C channels real (C: the 32-padded chunking of the weight rows; the rest stage as
+  // zero); training writes the normalised activation in fp32 to bn_y (row stride bn_ldy, client
+  // stride bn_y_cs) — the tensor the weight gradient and the BN backward read
+  int bn_c;
+  float* bn_y;
+  long bn_y_cs;
+  int bn_ldy;
 };
 
 // BN-backward partial request handed to conv_dgrad (see ConvNTParams::bnb)
@@ -219,6 +227,11 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s);
 // applied in the halo loader (ConvNTParams::bn_*); false: shape outside the halo kernels (the
 // caller applies the BN and runs the plain conv)
 bool conv_halo_bn_supported(int B, int H, int W, int C, int N);
+// BN forward (scale, shift) coefficients of the first C channels from running fp64 sums
+// [K][2][ldp] (client stride sums_cs), no pass over the input
+void bn_coef_sums(const double* sums, long sums_cs, int ldp, const float* gamma, const float* beta,
+                  const int* valid_rows, long g_cs, int K, int R, int C, float eps, int rep, float* mean, float* rstd,
+                  float* coef, hipStream_t s);
 // BN apply with precomputed (scale, shift) coefficients (bn_fwd coef_out) → split planes (+ ReLU bits)
 void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
                    bf16_t* yp, uint8_t* rmask, hipStream_t s);
@@ -226,6 +239,16 @@ bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, co
                       const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y, long y_cs, int K, int B,
                       int H, int W, int C, int N, float* stats, const int* stats_valid, hipStream_t s,
                       bf16_t* yp = nullptr, uint8_t* mask = nullptr);
+// DenseNet growth conv: BN(+ReLU) of the first creal channels of the block buffer x (row stride
+// ldx) applied in the halo loader; coef [K][C][2] and the weight planes [N][3][3][C] padded to C =
+// 32·⌈creal/32⌉ channels (zero); y rows at stride ldy (the block buffer's new channels); ny
+// (optional, training): the normalised activation [K][B·H·W][ldny] fp32, mask (optional, with ny,
+// creal % 8 == 0): its ReLU bits [K][B·H·W][ldny / 8]
+bool conv_halo_bn_dense_supported(int B, int H, int W, int C, int N);
+bool conv_halo_bn_dense_fwd(const float* x, long x_cs, int ldx, int creal, const float* coef, int relu,
+                            const int* valid_rows, const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y,
+                            long y_cs, int ldy, int K, int B, int H, int W, int C, int N, float* stats,
+                            const int* stats_valid, float* ny, long ny_cs, int ldny, uint8_t* mask, hipStream_t s);
 void conv_halo_set_mode(int m);  // -1 shape rule, 0 never, 1 whenever supported
 void conv_halo_set_variant(int v);  // -1 default, 0..2 pipeline / tile variant (benchmarks)
 bool conv_tn_pl_supported(const ConvTNParams& p);

@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(32 * G) bn_coef_kernel(const PT* __restrict__ 
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                       float* __restrict__ coef, float* __restrict__ dgamma,
                                                       float* __restrict__ dbeta, long dg_cs, long g_cs, int K, int R, int C,
-                                                      float eps, int rep, int bwd) {
+                                                      float eps, int rep, int bwd, int ldp, long pcs) {
   // partials are summed in fp64 (the conv-epilogue statistics arrive as thousands of 32-row
   // partials per channel; Σx² − n·μ² then keeps its precision), in a fixed order
   __shared__ double red[2][G][33];
@@ -277,10 +277,13 @@ __global__ void __launch_bounds__(32 * G) bn_coef_kernel(const PT* __restrict__ 
   const int c = blockIdx.x * 32 + cl;
   double d0 = 0.0, d1 = 0.0;
   if (c < C) {
-    const PT* part = ws + (long)k * nparts * 2 * C;
+    // (ldp / pcs: row length / client stride of the partial rows when they cover more channels
+    // than C — a DenseNet block's running sums, read for a channel prefix; 0 = C / nparts·2C)
+    const int lp = ldp ? ldp : C;
+    const PT* part = ws + (long)k * (pcs ? pcs : (long)nparts * 2 * lp);
     for (int b = grp; b < nparts; b += G) {
-      d0 += part[(long)b * 2 * C + c];
-      d1 += part[(long)b * 2 * C + C + c];
+      d0 += part[(long)b * 2 * lp + c];
+      d1 += part[(long)b * 2 * lp + lp + c];
     }
   }
   red[0][grp][cl] = d0;
@@ -687,11 +690,11 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
       hipLaunchKernelGGL(part_fold_kernel, dim3(nfold, K), dim3(256), 0, s, pre_part, nparts, 2 * C, folds, nfold);
       launch_coef<TT, double>(dim3(cdiv(C, 32), K), s, (const double*)folds, nfold, CP(gamma), CP(beta), valid_rows,
                               (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
-                              (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+                              (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0, 0, 0L);
     } else if (!counters || pre_part) {
       launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, part, nparts, CP(gamma), CP(beta), valid_rows,
                              (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
-                             (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0);
+                             (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0, 0, 0L);
     }
     if (apply) {
       DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
@@ -741,11 +744,11 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
                            nfold);
         launch_coef<TT, double>(dim3(cdiv(C, 32), K), s, (const double*)folds, nfold, CP(gamma), (const TT*)nullptr,
                                 valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs,
-                                g_cs, K, R, C, 0.f, 1, 1);
+                                g_cs, K, R, C, 0.f, 1, 1, 0, 0L);
       } else {
         launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, pre_part, pre_nparts, CP(gamma), (const TT*)nullptr,
                                valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs,
-                               g_cs, K, R, C, 0.f, 1, 1);
+                               g_cs, K, R, C, 0.f, 1, 1, 0, 0L);
       }
     } else {
       DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
@@ -754,11 +757,23 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
     if (!counters && !pre_part)
       launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, (const float*)part, (int)grid.x, CP(gamma), (const TT*)nullptr,
                              valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K,
-                             R, C, 0.f, 1, 1);
+                             R, C, 0.f, 1, 1, 0, 0L);
     DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                      valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx, dxp,
                                      dx_f32));
   });
+}
+
+void bn_coef_sums(const double* sums, long sums_cs, int ldp, const float* gamma, const float* beta,
+                  const int* valid_rows, long g_cs, int K, int R, int C, float eps, int rep, float* mean, float* rstd,
+                  float* coef, hipStream_t s) {
+  // BN forward coefficients from running fp64 sums [K][2][ldp] (Σx, Σx² of each channel), read for
+  // the first C channels: no pass over x (DenseNet: a channel's statistics are the same for every
+  // later layer that normalises it, so they are summed once, from the producing conv's epilogue)
+  using TT = float;
+  launch_coef<TT, double>(dim3(cdiv(C, 32), K), s, sums, 1, gamma, beta, valid_rows, (const float*)nullptr,
+                          (const float*)nullptr, mean, rstd, coef, (float*)nullptr, (float*)nullptr, 0L, g_cs, K, R, C,
+                          eps, rep, 0, ldp, sums_cs);
 }
 
 long col_sum_workspace_floats(int K, long rows, int C) {

@@ -121,6 +121,7 @@ class GTGShapleyValue(_Base):
         # counts (one iteration = n permutations) waste nothing.
         self.parallel_iterations = parallel_iterations
         self.eval_batch = 32
+        self.converged_last = None
 
     def _marginals(self, perms: list[list], v0: float, vN: float) -> list[list[tuple]]:
         """Position-by-position lock-step over `perms` with within-round truncation: one batched
@@ -151,6 +152,7 @@ class GTGShapleyValue(_Base):
             get_logger().info("GTG: between-round truncation (|v(N)-v0| = %.5f)", abs(vN - v0))
             self.evaluations_per_round[round_number] = self.evaluations - e0
             self.iterations_last = 0
+            self.converged_last = "between_round_truncation"
             self._finish({p: 0.0 for p in players})
             return
         rng = random.Random(self.seed * 1_000_003 + round_number)
@@ -193,6 +195,8 @@ class GTGShapleyValue(_Base):
         get_logger().info("GTG round %s: %d iterations, %d subset evaluations", round_number, it, self.evaluations)
         self.evaluations_per_round[round_number] = self.evaluations - e0
         self.iterations_last = it
+        # True: the mean change fell under converge_threshold; False: stopped at max_iterations
+        self.converged_last = done
         self._finish(means)
 
 

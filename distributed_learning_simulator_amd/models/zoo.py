@@ -248,7 +248,7 @@ class DenseBlock(Seq):
         lps = [Fn.DenseLayerParams(P.w(l.norm.gamma), P.w(l.norm.beta), P.g(l.norm.gamma), P.g(l.norm.beta),
                                    P.w(l.conv.w), P.g(l.conv.w)) for l in self.children]
         rps = x.shape[2] * x.shape[3]
-        return Fn.dense_block(x, ctx.token, lps, self.growth, ctx.valid_rows(rps))
+        return Fn.dense_block(x, ctx.token, lps, self.growth, ctx.valid_rows(rps), training=ctx.training)
 
 
 class DenseNetNet(Module):

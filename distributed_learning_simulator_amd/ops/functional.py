@@ -809,7 +809,7 @@ class _DenseBlock(torch.autograd.Function):
     SURVEY §2.7), BN with batch statistics (`util/model.py:23`)."""
 
     @staticmethod
-    def forward(ctx, x, token, layers, growth, valid_rows):
+    def forward(ctx, x, token, layers, growth, valid_rows, training=True):
         be = _be(x)
         K, B, H, W, c0 = x.shape
         L = len(layers)
@@ -818,17 +818,18 @@ class _DenseBlock(torch.autograd.Function):
         F[..., :c0].copy_(x)
         native = be is not ref
         saved = []
+        halo = native and x.dtype == torch.float32 and OPTIONS.dense_bn_halo
         # Per-channel batch statistics are the same for every later layer that normalises a
-        # channel (only γ/β differ), so they are computed ONCE per channel: the block input's in
-        # one pass, each new slice's from its conv epilogue (Σ / Σ² partials) — instead of a
-        # statistics pass over the whole growing prefix in every layer (O(L²) → O(L) bytes).
-        # (OPTIONS.dense_stats_cache; off by default: alternating A/B on the 100-client DenseNet-40
-        # round gave 13.47 s with the cache vs 13.43 s without — the per-layer stack / cast / sum
-        # launches cost what the skipped statistics passes save)
-        cache = native and x.dtype == torch.float32 and OPTIONS.bn_epilogue_stats and OPTIONS.dense_stats_cache
+        # channel (only γ/β differ), so with the fused growth convs they can be summed ONCE per
+        # channel (OPTIONS.dense_stats_cache): the block input's in one pass, each new slice's from
+        # its conv's epilogue partials — running fp64 sums S [K, 2, Ct] that the coefficient kernel
+        # reads for the prefix — instead of a statistics pass over the whole growing prefix in every
+        # layer (O(L²) → O(L) bytes).
+        cache = halo and OPTIONS.dense_stats_cache and all(
+            be.halo_bn_dense_ok(F[..., : c0 + i * growth], lp.w) for i, lp in enumerate(layers))
+        R = B * H * W
         if cache:
-            R = B * H * W
-            S = torch.empty((K, 2, Ct), dtype=torch.float64, device=x.device)  # Σx, Σx² per channel
+            S = torch.zeros((K, 2, Ct), dtype=torch.float64, device=x.device)
             x3 = F[..., :c0].reshape(K, R, c0)
             if valid_rows is not None:
                 keep = (torch.arange(R, device=x.device).view(1, R) < valid_rows.view(K, 1)).unsqueeze(-1)
@@ -839,17 +840,25 @@ class _DenseBlock(torch.autograd.Function):
         for i, lp in enumerate(layers):
             ci = c0 + i * growth
             xi = F[..., :ci].reshape(K, -1, ci)
-            if cache:
-                # the fp64 totals as two fp32 parts (value + rounding residual): the coefficient
-                # kernel sums parts in fp64, so Σx² − n·μ² keeps the totals' fp64 precision
-                hi = S[:, :, :ci].to(torch.float32)
-                pre = torch.stack((hi, (S[:, :, :ci] - hi.double()).to(torch.float32)), dim=1)  # [K, 2, 2, ci]
-                y, mean, rstd, mask = be.bn_fwd(xi, lp.gamma, lp.beta, valid_rows, True, None, with_mask=True,
-                                                pre_stats=pre)
-                part = torch.empty((K, be.conv_stats_parts(R), 2, growth), dtype=torch.float32, device=x.device)
-                be.conv_fwd(y.view(K, B, H, W, ci), lp.w, 1, 1, out=F[..., ci : ci + growth], stats=part,
-                            stats_valid=samples)
-                S[:, :, ci : ci + growth] = part.sum(dim=1, dtype=torch.float64)
+            if native and halo and be.halo_bn_dense_ok(F[..., :ci], lp.w):
+                # BN + ReLU applied in the growth conv's halo loader (csrc/conv_halo.hip BNM 2): the
+                # prefix is read in place once per 32-channel chunk for all nine taps; the normalised
+                # activation is written only in training (the weight gradient and BN backward read it)
+                part = None
+                if cache:
+                    coef, mean, rstd = be.bn_coef_sums(S, ci, lp.gamma, lp.beta, R, valid_rows)
+                    part = torch.empty((K, be.conv_stats_parts(R), 2, growth), dtype=torch.float32, device=x.device)
+                else:
+                    coef, mean, rstd = be.bn_coef(xi, lp.gamma, lp.beta, valid_rows)
+                y = torch.empty((K, B * H * W, ci), dtype=x.dtype, device=x.device) if training else None
+                # ReLU bits for the backward where whole bytes fit (ci % 8 == 0; otherwise it gates on y)
+                mask = (torch.empty((K, B * H * W, ci // 8), dtype=torch.uint8, device=x.device)
+                        if training and ci % 8 == 0 else None)
+                ok = be.conv_halo_bn_dense_fwd(F[..., :ci], coef, True, valid_rows, lp.w, F[..., ci : ci + growth],
+                                               stats=part, stats_valid=samples if cache else None, ny=y, mask=mask)
+                assert ok, "dense halo conv refused a shape halo_bn_dense_ok accepted"
+                if cache:
+                    S[:, :, ci : ci + growth] = part.sum(dim=1, dtype=torch.float64)
             elif native:
                 y, mean, rstd, mask = be.bn_fwd(xi, lp.gamma, lp.beta, valid_rows, True, None, with_mask=True)
                 be.conv_fwd(y.view(K, B, H, W, ci), lp.w, 1, 1, out=F[..., ci : ci + growth])
@@ -897,9 +906,10 @@ class _DenseBlock(torch.autograd.Function):
                     lp.gbeta.copy_(dbeta)
                 dF[..., :ci] += dx.view(K, B, H, W, ci).to(dF.dtype)
         ctx.saved = None
-        return dF[..., :c0].contiguous().to(dF_out.dtype), None, None, None, None
+        return dF[..., :c0].contiguous().to(dF_out.dtype), None, None, None, None, None
 
 
-def dense_block(x, token, layers: list[DenseLayerParams], growth: int, valid_rows=None):
-    """All layers of a DenseNet block in one buffer (see _DenseBlock)."""
-    return _DenseBlock.apply(x, token, layers, growth, valid_rows)
+def dense_block(x, token, layers: list[DenseLayerParams], growth: int, valid_rows=None, training: bool = True):
+    """All layers of a DenseNet block in one buffer (see _DenseBlock). `training=False`: no
+    backward will run, so the normalised activations are not kept."""
+    return _DenseBlock.apply(x, token, layers, growth, valid_rows, training)

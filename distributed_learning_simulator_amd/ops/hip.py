@@ -588,7 +588,9 @@ def bn_coef(x, gamma, beta, valid_rows=None, eps=1e-5, pre_stats=None):
     nothing applied: the consumer conv applies them while staging its input (conv_halo_bn_fwd).
     Same statistics / coefficient kernels (and bits) as bn_fwd."""
     K, R, C = x.shape
-    assert x.dtype == F32 and x.is_contiguous()
+    assert x.dtype == F32
+    x, ldx = _pix_stride(x)  # (a channel prefix of DenseNet's block buffer is read in place)
+    assert x.stride(0) == R * ldx, "client stride of a strided BN input must be R*ld"
     g_cs, rep = _client_view(gamma, K)
     mean = torch.empty((K, C), dtype=torch.float32, device=x.device)
     rstd = torch.empty((K, C), dtype=torch.float32, device=x.device)
@@ -599,8 +601,24 @@ def bn_coef(x, gamma, beta, valid_rows=None, eps=1e-5, pre_stats=None):
         assert pre_stats.dtype == torch.float32 and pre_stats.is_contiguous()
         assert pre_stats.shape[0] == K and pre_stats.shape[2:] == (2, C), pre_stats.shape
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), NULL, NULL, _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, 0, eps, rep, _p(ws),
-              NULL, _p(_bn_counters(K, x.device)), 1, _s(), C, _p(pre_stats),
+              NULL, _p(_bn_counters(K, x.device)), 1, _s(), ldx, _p(pre_stats),
               0 if pre_stats is None else pre_stats.shape[1], NULL, 1, _p(coef), 0)
+    return coef, mean, rstd
+
+
+def bn_coef_sums(sums, C: int, gamma, beta, R: int, valid_rows=None, eps=1e-5):
+    """bn_coef from running fp64 per-channel sums `sums` [K, 2, ld] (Σx, Σx² over the valid rows)
+    for the first C channels, with no pass over x (DenseNet block: the statistics of a channel are
+    summed once, from the epilogue of the conv that produced it)."""
+    K = sums.shape[0]
+    assert sums.dtype == torch.float64 and sums.is_contiguous() and sums.shape[1] == 2 and C <= sums.shape[2]
+    g_cs, rep = _client_view(gamma, K)
+    mean = torch.empty((K, C), dtype=torch.float32, device=sums.device)
+    rstd = torch.empty((K, C), dtype=torch.float32, device=sums.device)
+    coef = torch.empty((K, C, 2), dtype=torch.float32, device=sums.device)
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    _C.bn_coef_sums(_p(sums), sums.stride(0), sums.shape[2], _p(gamma), _p(beta), _p(vr), g_cs, K, R, C, eps, rep,
+                    _p(mean), _p(rstd), _p(coef), _s())
     return coef, mean, rstd
 
 
@@ -651,6 +669,77 @@ def conv_halo_bn_fwd(x, coef, relu: bool, valid_rows, w, w_split, stats=None, st
     if ok:
         planes_launches["fwd_bn_fused"] += 1
     return y if ok else None
+
+
+def _c32(c: int) -> int:
+    return (c + 31) // 32 * 32
+
+
+def halo_bn_dense_ok(x, w) -> bool:
+    """conv_halo_bn_dense_fwd serves this DenseNet layer: x the channel prefix [K, B, H, W, c]
+    of the block buffer (fp32, uniform pixel stride), w [Kw, N ≤ 32, 3, 3, c]."""
+    K, B, H, W, C = x.shape
+    if x.dtype != F32 or w.dtype != F32 or w.dim() != 5 or tuple(w.shape[2:]) != (3, 3, C) or C % 4:
+        return False
+    xs, ldx = _pix_stride(x)
+    if xs.data_ptr() != x.data_ptr() or ldx % 8 or x.stride(0) != B * H * W * ldx:
+        return False
+    return bool(_C.conv_halo_bn_dense_supported(B, H, W, _c32(C), w.shape[1]))
+
+
+def dense_weight_planes(w) -> torch.Tensor:
+    """[Kw, 2, N, 3, 3, C32] split planes of a growth conv's weight zero-padded to 32-channel
+    chunks (the halo kernel stages whole chunks; tap rows then start 64-B aligned)."""
+    Kw, N, KH, KW, C = w.shape
+    C32 = _c32(C)
+    wp = torch.zeros((Kw, N, KH, KW, C32), dtype=F32, device=w.device)
+    wp[..., :C].copy_(w)
+    return split_planes(wp)
+
+
+def conv_halo_bn_dense_fwd(x, coef, relu: bool, valid_rows, w, out, w_planes=None, stats=None, stats_valid=None,
+                           ny=None, mask=None) -> bool:
+    """DenseNet growth conv out = conv3x3(relu?(BN(x))) with the BN applied in the halo loader
+    (csrc/conv_halo.hip BNM 2): x [K, B, H, W, c] the block buffer's channel prefix read in place,
+    coef [K, c, 2] its (scale, shift) pairs (bn_coef), out [K, B, H, W, N] the buffer's new
+    channels (written in place). `ny` [K, B·H·W, c] fp32 (training): the normalised activation
+    (what bn_fwd would have returned as y) for the weight gradient and the BN backward. No
+    normalised copy of the prefix is written otherwise. `mask` [K, B·H·W, c/8] uint8 (with `ny`,
+    c % 8 == 0): its ReLU bits, which bn_bwd reads instead of ny. False: shape not served."""
+    K, B, H, W, C = x.shape
+    Kw, N = w.shape[0], w.shape[1]
+    C32 = _c32(C)
+    xs, ldx = _pix_stride(x)
+    assert xs.data_ptr() == x.data_ptr(), "x must be a pixel-strided view"
+    y, ldy = _pix_stride(out)
+    assert y.data_ptr() == out.data_ptr() and out.shape == (K, B, H, W, N), "out must be a pixel-strided view"
+    assert coef.shape == (K, C, 2) and coef.dtype == F32
+    cp = coef
+    if C32 != C:
+        cp = torch.zeros((K, C32, 2), dtype=F32, device=x.device)
+        cp[:, :C].copy_(coef)
+    cp = cp.contiguous()
+    if w_planes is None:
+        w_planes = dense_weight_planes(w)
+    assert w_planes.shape == (Kw, 2, N, 3, 3, C32) and w_planes.dtype == BF16 and w_planes.is_contiguous()
+    rep = K // Kw
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    if stats is not None:
+        assert stats.shape == (K, conv_stats_parts(B * H * W), 2, N) and stats.is_contiguous()
+        if stats_valid is not None:
+            stats_valid = stats_valid.to(torch.int32).contiguous()
+    if ny is not None:
+        assert ny.shape == (K, B * H * W, C) and ny.dtype == F32 and ny.is_contiguous()
+    if mask is not None:
+        assert ny is not None and C % 8 == 0 and mask.shape == (K, B * H * W, C // 8) and mask.dtype == torch.uint8
+        assert mask.is_contiguous()
+    ok = _C.conv_halo_bn_dense_fwd(_p(xs), xs.stride(0), ldx, C, _p(cp), int(relu), _p(vr), _p(w_planes),
+                                   w_planes.stride(0) if Kw > 1 else 0, w_planes.stride(1), rep, _p(y), y.stride(0),
+                                   ldy, K, B, H, W, C32, N, _p(stats), _p(stats_valid), _p(ny),
+                                   ny.stride(0) if ny is not None else 0, C, _p(mask), _s())
+    if ok:
+        planes_launches["fwd_bn_dense"] += 1
+    return bool(ok)
 
 
 def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None,

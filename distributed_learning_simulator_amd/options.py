@@ -49,10 +49,15 @@ class RuntimeOptions:
     bn_bwd_parts: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_BWD_PARTS", True))
     """BN backward partial sums from the consuming conv's dgrad epilogue (off: own reduction)."""
     bn_fused_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_HALO", True))
-    """Inference: a BN(+ReLU) whose only reader is a 3x3 stride-1 conv is applied in that conv's
-    halo loader (ops.functional.bn_relu_conv3x3_eval; off: BN apply pass + plane conv)."""
-    dense_stats_cache: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_STATS_CACHE", False))
-    """DenseNet blocks compute each channel's statistics once (measured no faster: off)."""
+    """A BN(+ReLU) whose only reader is a 3x3 stride-1 conv (ResNet BasicBlock bn1) is applied in
+    that conv's halo loader (ops.functional DeferredBN; off: BN apply pass + plane conv)."""
+    dense_bn_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_BN_HALO", True))
+    """DenseNet growth convs apply their BN + ReLU in the halo loader over the block buffer's
+    channel prefix (off: BN apply pass + implicit-GEMM conv)."""
+    dense_stats_cache: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_STATS_CACHE", True))
+    """DenseNet blocks (fused growth convs) sum each channel's statistics once, from the producing
+    conv's epilogue, into running fp64 sums the BN coefficients read (off: a statistics pass over
+    the prefix per layer)."""
     bn_fused_coef: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_COEF", False))
     """BN coefficients in a last-arriver stage of the statistics kernel (measured slower: off)."""
     # --- reductions

@@ -307,3 +307,26 @@ def test_resnet18_training_fused_bn_halo_bitwise(hip, tmp_path):
         b, rb = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
     assert torch.equal(a.server.global_parameter, b.server.global_parameter)
     assert _losses(ra) == _losses(rb)
+
+def test_densenet40_training_fused_bn_halo(hip, tmp_path):
+    """DenseNet-40 training with the growth convs' BN + ReLU applied in the halo loader
+    (csrc/conv_halo.hip BNM 2, Fn._DenseBlock): deterministic (two runs bitwise equal), and equal
+    to the unfused run to rounding (the fused conv sums its taps in 32-channel chunks)."""
+    from distributed_learning_simulator_amd.ops import hip as H
+
+    ov = {"round": 1, "epoch": 1, "worker_number": 4, "model_name": "densenet40", "dataset_kwargs.scale": 0.01,
+          "learning_rate": 0.01}
+    H.planes_launches.clear()
+    with options.override(dense_bn_halo=True):
+        a, ra = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
+        a2, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a2", "cuda")
+    assert H.planes_launches["fwd_bn_dense"] > 0, H.planes_launches
+    with options.override(dense_bn_halo=False):
+        b, rb = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    with options.override(dense_bn_halo=True, dense_stats_cache=True):
+        c, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "c", "cuda")
+    pa, pb = a.server.global_parameter, b.server.global_parameter
+    assert torch.equal(pa, a2.server.global_parameter)
+    for p in (pa, c.server.global_parameter):
+        rel = ((p - pb).abs().max() / pb.abs().max()).item()
+        assert rel < 1e-4, rel

@@ -806,6 +806,98 @@ def test_halo_conv_with_fused_bn_input(hip, case):
     _close(out, ref.conv_fwd(z, _d(w), 1, 1))
 
 
+DENSE_HALO_CASES = [
+    # K, Kw, B, H, c (prefix), Ct (block buffer), N, valid samples of client 0
+    (2, 2, 4, 32, 28, 160, 12, None),   # block 1, c % 8 == 4 (half a lane group real)
+    (2, 2, 4, 32, 16, 160, 12, 3),      # first layer, invalid rows
+    (3, 1, 4, 16, 172, 304, 12, None),  # block 2, one shared weight (rep = K)
+    (2, 2, 4, 8, 436, 448, 12, 2),      # block 3: the last chunk runs to the buffer's end
+    (2, 2, 4, 32, 64, 96, 32, None),    # 32 new channels: the full N tile
+]
+
+
+@pytest.mark.parametrize("case", DENSE_HALO_CASES)
+def test_dense_growth_conv_with_fused_bn(hip, case):
+    """DenseNet growth conv with BN + ReLU over the block buffer's channel prefix applied in the
+    halo loader (csrc/conv_halo.hip BNM 2): the prefix is read in place, channels past it are
+    never read (they hold NaN here), the normalised activation it writes equals bn_fwd's y bit for
+    bit, its output lands in the buffer's new channels only, and the conv matches the unfused
+    BN-apply → conv and the fp64 oracle of conv(relu(bn(x)))."""
+    K, Kw, B, H, c, Ct, N, nv = case
+    torch.manual_seed(5)
+    F = _f(K, B, H, H, Ct, scale=2.0) + 0.5
+    F[..., c:] = float("nan")
+    x = F[..., :c]
+    gamma, beta = _f(K, c) * 0.5 + 1.0, _f(K, c) * 0.2
+    w = _f(Kw, N, 3, 3, c, scale=0.05)
+    valid = None if nv is None else torch.tensor([nv] + [B] * (K - 1), dtype=torch.int32, device=DEV)
+    vrows = None if valid is None else valid * (H * H)
+    assert hip.halo_bn_dense_ok(x, w)
+    x3 = x.reshape(K, -1, c)
+    y_ref, mean, rstd, m_ref = hip.bn_fwd(x3, gamma, beta, vrows, True, None, with_mask=True)
+    assert (m_ref is not None) == (c % 8 == 0)
+    unfused = hip.conv_fwd(y_ref.view(K, B, H, H, c), w, 1, 1)
+    coef, mean2, rstd2 = hip.bn_coef(x3, gamma, beta, vrows)
+    assert torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+    ny = torch.empty((K, B * H * H, c), device=DEV)
+    before = F.clone()
+    mask = torch.empty_like(m_ref) if m_ref is not None else None
+    assert hip.conv_halo_bn_dense_fwd(x, coef, True, vrows, w, F[..., c : c + N], ny=ny, mask=mask)
+    torch.cuda.synchronize()
+    assert torch.equal(ny, y_ref), (ny - y_ref).abs().max()
+    if mask is not None:
+        assert torch.equal(mask, m_ref)
+    out = F[..., c : c + N]
+    assert not torch.isnan(out).any()
+    rest = torch.cat([F[..., :c], F[..., c + N :]], dim=-1)
+    rest_b = torch.cat([before[..., :c], before[..., c + N :]], dim=-1)
+    assert torch.equal(rest.nan_to_num(7.0), rest_b.nan_to_num(7.0)), "wrote outside its output channels"
+    _close(out, unfused)
+    # evaluation form: no activation written, same output
+    F2 = before.clone()
+    assert hip.conv_halo_bn_dense_fwd(F2[..., :c], coef, True, vrows, w, F2[..., c : c + N])
+    assert torch.equal(F2[..., c : c + N], out)
+    xd = _d(x3)
+    rows = xd.shape[1]
+    keep = torch.ones(K, rows, 1, dtype=torch.float64)
+    if vrows is not None:
+        keep = (torch.arange(rows).view(1, rows) < vrows.cpu().view(K, 1)).double().unsqueeze(-1)
+    cnt = keep.sum(1)
+    mu = (xd * keep).sum(1) / cnt
+    var = (((xd - mu[:, None]) ** 2) * keep).sum(1) / cnt
+    z = (xd - mu[:, None]) / torch.sqrt(var[:, None] + 1e-5) * _d(gamma)[:, None] + _d(beta)[:, None]
+    z = (z.clamp(min=0) * keep).view(K, B, H, H, c)
+    _close(out, ref.conv_fwd(z, _d(w).expand(K, -1, -1, -1, -1), 1, 1))
+
+
+def test_densenet40_eval_fused_bn_halo(hip):
+    """DenseNet-40 batched evaluation with the growth convs' BN fused into the halo loader agrees
+    with the unfused evaluation (the conv's K order differs — taps padded to 32-channel chunks —
+    so equal to rounding, not bitwise), and the fused kernels ran."""
+    from distributed_learning_simulator_amd import options
+    from distributed_learning_simulator_amd.data.datasets import create_dataset_collection
+    from distributed_learning_simulator_amd.engine.trainer import CohortTrainer, HyperParameter
+    from distributed_learning_simulator_amd.models.zoo import build_model
+
+    dev = torch.device(DEV)
+    dc = create_dataset_collection("CIFAR10", {"n_train": 256, "n_test": 300}, 0, dev, torch.float32, image_channels=8)
+    model = build_model("densenet40", dc.spec)
+    tr = CohortTrainer(model, dc, HyperParameter(epoch=1, batch_size=64), dev, torch.float32, capacity=1)
+    g = torch.Generator().manual_seed(0)
+    rows = torch.stack([model.layout.init_flat(g) for _ in range(2)]).to(dev)
+    hip.planes_launches.clear()
+    with options.override(dense_bn_halo=True):
+        lf, cf, n = tr.evaluate(rows, max_images=512)
+    assert hip.planes_launches["fwd_bn_dense"] > 0, hip.planes_launches
+    with options.override(dense_bn_halo=False):
+        lu, cu, _ = tr.evaluate(rows, max_images=512)
+    with options.override(dense_bn_halo=True, dense_stats_cache=True):
+        lc, cc, _ = tr.evaluate(rows, max_images=512)
+    for lo, co in ((lf, cf), (lc, cc)):
+        assert (co - cu).abs().max().item() <= 2
+        assert (lo - lu).abs().max().item() <= 1e-5 * lu.abs().max().item(), (lo - lu).abs().max()
+
+
 def test_resnet18_eval_fused_bn_equals_unfused(hip):
     """The batched utility evaluation (GTG-Shapley's cost) with bn1 fused into conv2's halo loader
     gives bitwise the same losses and correct counts as the unfused evaluation, and the fused
