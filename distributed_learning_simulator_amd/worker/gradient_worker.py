@@ -97,10 +97,10 @@ class GradientWorker(AggregationWorker):
         theta0 = b.theta[:1]
         nbytes = self._wire_bytes_per_client()
         # OPTIONS.shared_planes: the shared row's (hi, lo) weight planes feed the split-plane GEMMs
-        # of every client (rep = K; the SGD kernel keeps them current with θ). Off by default:
-        # measured on sign-SGD ResNet-50 (224², batch 128) it lost to the register-staged split
-        # kernels (29.4 s/round at 8 clients per wave vs 26.5 s), and the planes' activation
-        # memory shrinks the wave (tests/test_gpu_sessions.py covers the path)
+        # of every client (rep = K; the SGD kernel keeps them current with θ), so forward and dgrad
+        # run the LDS-DMA plane kernels. Measured on sign-SGD ResNet-50 (224², batch 128, 7 clients
+        # per wave): 3.18 s per vote step vs 3.51 s on the register-staged split kernels
+        # (profiles/r4_c10_signsgd_*.log); tests/test_gpu_sessions.py covers the path
         split = b.split[:1] if (b.split is not None and OPTIONS.shared_planes) else None
         if split is not None:
             fl.split_rows(theta0, split)
@@ -140,7 +140,7 @@ class GradientWorker(AggregationWorker):
                             if wd:  # compute_gradient (`gradient_worker.py:13-26`)
                                 g.add_(theta0, alpha=wd)
                             payload = self._process_gradient(g)
-                    except torch.OutOfMemoryError:
+                    except torch.OutOfMemoryError as oom:
                         # the planned wave did not fit (the activation probe measures one client;
                         # allocator fragmentation at many clients can exceed it): halve the wave
                         # for the rest of the run and redo this one — nothing of it was accumulated
@@ -149,7 +149,10 @@ class GradientWorker(AggregationWorker):
                         x = y = loss = correct = g = None
                         cap = tr.capacity = max(1, cap // 2)
                         torch.cuda.empty_cache()
-                        get_logger().warning("wave of %d clients ran out of memory: waves of %d from here", K, cap)
+                        get_logger().warning("wave of %d clients ran out of memory (%s; %.1f GiB allocated, %.1f GiB "
+                                             "reserved): waves of %d from here", K, str(oom).split("\n")[0][:160],
+                                             torch.cuda.memory_allocated(tr.device) / 2**30,
+                                             torch.cuda.memory_reserved(tr.device) / 2**30, cap)
                         continue
                     with torch.no_grad():
                         self._accumulate(acc, payload, sched.active[s, w0:w1], sizes[w0:w1])
