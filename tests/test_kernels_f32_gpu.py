@@ -248,9 +248,10 @@ def test_dense_block_strided_kernels_match_cpu(hip, dtype, tol):
     layout = model.layout
     K = 3
     theta = torch.stack([layout.init_flat(torch.Generator().manual_seed(s)) for s in range(K)])
-    x = torch.randn(K, 6, 32, 32, 8)
+    g = torch.Generator().manual_seed(7)  # (fixed data: a ReLU input within rounding of 0 may gate
+    x = torch.randn(K, 6, 32, 32, 8, generator=g)  # differently on the two paths)
     x[..., 3:] = 0
-    y = torch.randint(0, 10, (K, 6))
+    y = torch.randint(0, 10, (K, 6), generator=g)
     valid = torch.tensor([6, 4, 1], dtype=torch.int32)
     out = {}
     for dev in ("cpu", "cuda"):
