@@ -416,20 +416,11 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
       case 0: launch_halo_bnf<1, 8, 32, 64, 4, 2, 3>(p, K, s); break;
       case 1: launch_halo_bnf<1, 16, 16, 128, 4, 2, 2>(p, K, s); break;
       case 2: launch_halo_bnf<2, 8, 8, 128, 4, 2, 2>(p, K, s); break;
-      default: {
-        // DenseNet growth convs: 4 waves of 64 x 32 or 8 waves of 32 x 32 per 256-row tile (the
-        // register-staged halo load splits over twice the waves; DLS_DENSE_HALO_WAVES)
-        const bool w8 = native_option(g_opt_dense_halo_waves, "DLS_DENSE_HALO_WAVES", 4) == 8;
-        switch (cfg * 2 + (w8 ? 1 : 0)) {
-          case 8: launch_halo_bnf<1, 8, 32, 32, 4, 1, 3, 2>(p, K, s); break;   // 62 KB
-          case 9: launch_halo_bnf<1, 8, 32, 32, 8, 1, 3, 2>(p, K, s); break;
-          case 10: launch_halo_bnf<1, 16, 16, 32, 4, 1, 3, 2>(p, K, s); break;  // 62 KB
-          case 11: launch_halo_bnf<1, 16, 16, 32, 8, 1, 3, 2>(p, K, s); break;
-          case 12: launch_halo_bnf<4, 8, 8, 32, 4, 1, 3, 2>(p, K, s); break;    // 78 KB
-          case 13: launch_halo_bnf<4, 8, 8, 32, 8, 1, 3, 2>(p, K, s); break;
-          default: return false;
-        }
-      }
+      case 4: launch_halo_bnf<1, 8, 32, 32, 4, 1, 3, 2>(p, K, s); break;  // 62 KB
+      case 5: launch_halo_bnf<1, 16, 16, 32, 4, 1, 3, 2>(p, K, s); break;  // 62 KB
+      case 6: launch_halo_bnf<4, 8, 8, 32, 4, 1, 3, 2>(p, K, s); break;    // 78 KB
+      // (8 waves of 32 x 32 per tile: bitwise the same, no faster — r4_c14_dn_w*.log)
+      default: return false;
     }
     return true;
   }

@@ -12,7 +12,6 @@ typedef uint16_t bf16_t;
 // — overrides it at any time between launches. Defined in elementwise.hip.
 constexpr int kOptUnset = -1000000;
 extern int g_opt_attn_mfma, g_opt_f32_smallk, g_opt_conv_gl, g_opt_pl_min_wg, g_opt_tn_kref, g_opt_bn_coef_groups;
-extern int g_opt_dense_halo_waves;
 int native_option(int& slot, const char* env, int dflt);
 bool set_native_option(const char* name, int value);  // false: unknown name
 
