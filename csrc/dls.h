@@ -141,6 +141,21 @@ struct BNBwdPartials {
   const int* valid;
 };
 
+// DenseNet growth-conv weight gradient with LDS halo reuse (conv_dense_wgrad.hip): dy [K][M][ldy]
+// (the growth channels of the block gradient), y [K][M][C] (the normalised prefix), dw rows
+// [N][3][3][C] at client stride dw_cs; part: nchunks·G per-workgroup slabs per client
+struct DenseWgradParams {
+  const float* dy;
+  long dy_cs;
+  int ldy;
+  const float* y;
+  long y_cs;
+  float* dw;
+  long dw_cs;
+  float* part;
+  int K, B, H, W, C, N, nchunks, G;
+};
+
 struct ConvTNParams {
   const bf16_t* dy;  // [K][M][Co]
   const bf16_t* x;   // [K][B][H][W][C]
@@ -249,6 +264,10 @@ bool conv_halo_bn_dense_fwd(const float* x, long x_cs, int ldx, int creal, const
                             const int* valid_rows, const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y,
                             long y_cs, int ldy, int K, int B, int H, int W, int C, int N, float* stats,
                             const int* stats_valid, float* ny, long ny_cs, int ldny, uint8_t* mask, hipStream_t s);
+bool dense_wgrad_supported(int B, int H, int W, int C, int N);
+long dense_wgrad_part_floats(int K, int B, int H, int W, int C);
+bool dense_wgrad(const float* dy, long dy_cs, int ldy, const float* y, long y_cs, float* dw, long dw_cs, float* part,
+                 int K, int B, int H, int W, int C, int N, hipStream_t s);
 void conv_halo_set_mode(int m);  // -1 shape rule, 0 never, 1 whenever supported
 void conv_halo_set_variant(int v);  // -1 default, 0..2 pipeline / tile variant (benchmarks)
 bool conv_tn_pl_supported(const ConvTNParams& p);

@@ -880,6 +880,7 @@ class _DenseBlock(torch.autograd.Function):
         K, B, H, W, Ct = F.shape
         g, c0 = ctx.growth, ctx.c0
         dF = dF_out.contiguous().clone() if native else dF_out.float().clone()
+        wgrad_halo = native and F.dtype == torch.float32 and OPTIONS.dense_wgrad_halo
         for i in range(len(ctx.layers) - 1, -1, -1):
             lp = ctx.layers[i]
             y, mean, rstd, mask = ctx.saved[i]
@@ -888,7 +889,7 @@ class _DenseBlock(torch.autograd.Function):
             yv = y.view(K, B, H, W, ci)
             xi = F[..., :ci].reshape(K, -1, ci)
             if native:
-                if lp.gw is not None:
+                if lp.gw is not None and not (wgrad_halo and be.dense_wgrad(d_out, y, lp.gw)):
                     be.conv_wgrad(d_out, yv, lp.gw, 1, 1)
                 # (BN partials from this dgrad's epilogue measured slower here: 14.57 vs 14.36 s per
                 # 100-client round — the strided x / gate reads cost more than the pass they replace)

@@ -671,6 +671,37 @@ def conv_halo_bn_fwd(x, coef, relu: bool, valid_rows, w, w_split, stats=None, st
     return y if ok else None
 
 
+_dw_part_cache: dict = {}
+
+
+def dense_wgrad(dy, y, gw) -> bool:
+    """DenseNet growth-conv weight gradient on the LDS-halo kernel (csrc/conv_dense_wgrad.hip):
+    dy [K, B, H, W, N] the block gradient's growth channels (a pixel-strided view, read in place),
+    y [K, B·H·W, C] the normalised prefix (contiguous), gw [K, N, 3, 3, C] the gradient rows
+    (written). False: shape not served (nothing ran)."""
+    K, B, H, W, N = dy.shape
+    if y.dim() != 3 or dy.dtype != F32 or y.dtype != F32 or not y.is_contiguous() or y.shape[:2] != (K, B * H * W):
+        return False
+    C = y.shape[2]
+    if not _C.dense_wgrad_supported(B, H, W, C, N):
+        return False
+    d, ldy = _pix_stride(dy)
+    if d.data_ptr() != dy.data_ptr() or ldy % 4 or dy.stride(0) != B * H * W * ldy:
+        return False
+    assert gw.shape == (K, N, 3, 3, C) and gw.dtype == F32 and gw[0].is_contiguous(), gw.shape
+    n = _C.dense_wgrad_part_floats(K, B, H, W, C)
+    key = (dy.device, torch.cuda.current_stream().cuda_stream)
+    part = _dw_part_cache.get(key)
+    if part is None or part.numel() < n:  # (grown, never shrunk: a captured graph keeps its pointer)
+        part = torch.empty(max(n, 1 << 16), dtype=F32, device=dy.device)
+        _dw_part_cache[key] = part
+    ok = _C.dense_wgrad(_p(d), dy.stride(0), ldy, _p(y), y.stride(0), _p(gw), gw.stride(0), _p(part), K, B, H, W, C, N,
+                        _s())
+    if ok:
+        planes_launches["wgrad_dense_halo"] += 1
+    return bool(ok)
+
+
 def _c32(c: int) -> int:
     return (c + 31) // 32 * 32
 

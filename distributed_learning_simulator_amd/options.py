@@ -54,6 +54,9 @@ class RuntimeOptions:
     dense_bn_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_BN_HALO", True))
     """DenseNet growth convs apply their BN + ReLU in the halo loader over the block buffer's
     channel prefix (off: BN apply pass + implicit-GEMM conv)."""
+    dense_wgrad_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_WGRAD_HALO", True))
+    """DenseNet growth-conv weight gradients on the LDS-halo kernel (the normalised prefix staged
+    once per pixel tile for all nine taps; off: the implicit-GEMM TN kernel)."""
     dense_stats_cache: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_STATS_CACHE", True))
     """DenseNet blocks (fused growth convs) sum each channel's statistics once, from the producing
     conv's epilogue, into running fp64 sums the BN coefficients read (off: a statistics pass over

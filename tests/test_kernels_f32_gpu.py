@@ -871,6 +871,34 @@ def test_dense_growth_conv_with_fused_bn(hip, case):
     _close(out, ref.conv_fwd(z, _d(w).expand(K, -1, -1, -1, -1), 1, 1))
 
 
+@pytest.mark.parametrize("case", [(2, 4, 32, 28, 160, 12), (3, 4, 16, 172, 304, 12), (2, 4, 8, 436, 448, 12),
+                                  (2, 2, 32, 16, 160, 12), (2, 4, 16, 64, 96, 16)])
+def test_dense_wgrad_halo(hip, case):
+    """DenseNet growth-conv weight gradient on the LDS-halo kernel (csrc/conv_dense_wgrad.hip:
+    16x16x32 MFMA, pixel-major operands read with the transposed LDS read) against the fp64 oracle
+    and the implicit-GEMM TN kernel; dY read in place from the block gradient's growth channels,
+    the gradient rows' neighbours untouched, and deterministic (two runs bitwise equal)."""
+    K, B, H, c, Ct, N = case
+    torch.manual_seed(13)
+    dG = _f(K, B, H, H, Ct)
+    dy = dG[..., c : c + N]
+    y = torch.relu(_f(K, B * H * H, c))
+    P = N * 9 * c + 24
+    gbuf = torch.full((K, P), 7.0, device=DEV)
+    gw = gbuf[:, 8 : 8 + N * 9 * c].unflatten(1, (N, 3, 3, c))
+    assert hip.dense_wgrad(dy, y, gw)
+    torch.cuda.synchronize()
+    assert torch.all(gbuf[:, :8] == 7.0) and torch.all(gbuf[:, 8 + N * 9 * c :] == 7.0)
+    oracle = ref.conv_wgrad(_d(dy.contiguous()), _d(y).view(K, B, H, H, c), (K, N, 3, 3, c), 1, 1)
+    _close(gw, oracle)
+    gw2 = torch.empty_like(gw)
+    hip.conv_wgrad(dy, y.view(K, B, H, H, c), gw2, 1, 1)
+    _close(gw, gw2, 2e-5)
+    again = torch.empty_like(gw)
+    assert hip.dense_wgrad(dy, y, again)
+    assert torch.equal(again, gw)
+
+
 def test_densenet40_eval_fused_bn_halo(hip):
     """DenseNet-40 batched evaluation with the growth convs' BN fused into the halo loader agrees
     with the unfused evaluation (the conv's K order differs — taps padded to 32-channel chunks —
