@@ -27,7 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t lds_off(int row, int half) { return (uint32_t)(row * 64 + ((half ^ ((row >> 3) & 1)) << 5)); }
 
 template <int IMG, int TH, int TW>
-__global__ void __launch_bounds__(576) dense_wgrad_kernel(DenseWgradParams p) {
+__global__ void __launch_bounds__(576) __attribute__((amdgpu_waves_per_eu(5, 8))) dense_wgrad_kernel(DenseWgradParams p) {
   constexpr int TP = IMG * TH * TW;  // GEMM k rows (pixels) per tile
   static_assert(TP % 32 == 0 && TW % 8 == 0, "tile");
   constexpr int HW2 = TW + 2, HH2 = TH + 2;
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(576) dense_wgrad_kernel(DenseWgradParams p) {
   const int rem = blockIdx.x - client * per_client;
   const int chunk = rem / p.G, g = rem - chunk * p.G;
   const int c0 = chunk * 32;
-  const float* __restrict__ yb = p.y + (long)client * p.y_cs;
+  const float* __restrict__ yb_ = p.y + (long)client * p.y_cs;
   const float* __restrict__ db = p.dy + (long)client * p.dy_cs;
   const int tpi = p.H / TH;  // row blocks per image (IMG == 1)
   const int tiles = IMG == 1 ? p.B * tpi : p.B / IMG;
@@ -56,50 +56,79 @@ __global__ void __launch_bounds__(576) dense_wgrad_kernel(DenseWgradParams p) {
   const int kh = tap / 3, kw = tap - kh * 3;
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
-  for (int t = g; t < tiles; t += p.G) {
+  // global → registers for tile t (issued one tile ahead: the loads of tile t + G fly while
+  // tile t's MFMAs run), registers → split bf16 planes in LDS
+  constexpr int YR = (HP * 4 + 575) / 576, DR = (TP * 4 + 575) / 576;
+  float4 ya[YR], yb[YR], dv[DR];
+  auto load_tile = [&](int t) {
     const int b0 = IMG == 1 ? t / tpi : t * IMG;
     const int h0 = IMG == 1 ? (t - (t / tpi) * tpi) * TH : 0;
-    __syncthreads();  // the previous tile's reads are done
-    // ---- Y halo: (halo row, 8-channel group) tasks; zeros outside the image / past the prefix
-    for (int task = tid; task < HP * 4; task += 576) {
+#pragma unroll
+    for (int r = 0; r < YR; ++r) {  // Y halo: (halo row, 8-channel group) tasks
+      const int task = tid + r * 576;
       const int hr = task >> 2, cg = task & 3;
       const int img = hr / (HH2 * HW2), r2 = hr - img * (HH2 * HW2);
       const int hh = r2 / HW2, ww = r2 - hh * HW2;
       const int ih = h0 - 1 + hh, iw = ww - 1;
-      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      const int c = c0 + cg * 8, cv = p.C - c;
+      const bool ok = task < HP * 4 && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const int c = c0 + cg * 8, cv = p.C - c;  // zeros outside the image / past the prefix
       const long e = (long)(((b0 + img) * p.H + (ok ? ih : 0)) * p.W + (ok ? iw : 0)) * p.C + c;
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-      if (ok && cv > 0) v0 = *reinterpret_cast<const float4*>(yb + e);
-      if (ok && cv >= 8) v1 = *reinterpret_cast<const float4*>(yb + e + 4);
-      uint32_t hi[4], lo[4];
-      split_pair(v0.x, v0.y, hi[0], lo[0]);
-      split_pair(v0.z, v0.w, hi[1], lo[1]);
-      split_pair(v1.x, v1.y, hi[2], lo[2]);
-      split_pair(v1.z, v1.w, hi[3], lo[3]);
-      const uint32_t off = lds_off(hr, cg >> 1) + ((cg & 1) << 4);
-      *reinterpret_cast<uint4*>(Yh + off) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-      *reinterpret_cast<uint4*>(Yl + off) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+      ya[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      yb[r] = ya[r];
+      if (ok && cv > 0) ya[r] = *reinterpret_cast<const float4*>(yb_ + e);
+      if (ok && cv >= 8) yb[r] = *reinterpret_cast<const float4*>(yb_ + e + 4);
     }
-    // ---- dY tile: (pixel, 4-channel group) tasks, n ≥ N zero (rows n 16..31 of the 64-B row unused)
-    for (int task = tid; task < TP * 4; task += 576) {
+#pragma unroll
+    for (int r = 0; r < DR; ++r) {  // dY tile: (pixel, 4-channel group) tasks, n ≥ N zero
+      const int task = tid + r * 576;
       const int pt = task >> 2, ng = task & 3;
       const int img = pt / (TH * TW), r2 = pt - img * (TH * TW);
       const int th = r2 / TW, tw = r2 - th * TW;
       const long pix = (long)((b0 + img) * p.H + h0 + th) * p.W + tw;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ng * 4 < p.N) v = *reinterpret_cast<const float4*>(db + pix * p.ldy + ng * 4);
-      uint32_t hi0, lo0, hi1, lo1;
-      split_pair(v.x, v.y, hi0, lo0);
-      split_pair(v.z, v.w, hi1, lo1);
-      const uint32_t off = lds_off(pt, 0) + (ng << 3);
-      *reinterpret_cast<uint2*>(Dh + off) = make_uint2(hi0, hi1);
-      *reinterpret_cast<uint2*>(Dl + off) = make_uint2(lo0, lo1);
+      dv[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (task < TP * 4 && ng * 4 < p.N) dv[r] = *reinterpret_cast<const float4*>(db + pix * p.ldy + ng * 4);
     }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int r = 0; r < YR; ++r) {
+      const int task = tid + r * 576;
+      if (task < HP * 4) {
+        const int hr = task >> 2, cg = task & 3;
+        uint32_t hi[4], lo[4];
+        split_pair(ya[r].x, ya[r].y, hi[0], lo[0]);
+        split_pair(ya[r].z, ya[r].w, hi[1], lo[1]);
+        split_pair(yb[r].x, yb[r].y, hi[2], lo[2]);
+        split_pair(yb[r].z, yb[r].w, hi[3], lo[3]);
+        const uint32_t off = lds_off(hr, cg >> 1) + ((cg & 1) << 4);
+        *reinterpret_cast<uint4*>(Yh + off) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+        *reinterpret_cast<uint4*>(Yl + off) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < DR; ++r) {
+      const int task = tid + r * 576;
+      if (task < TP * 4) {
+        const int pt = task >> 2, ng = task & 3;
+        uint32_t hi0, lo0, hi1, lo1;
+        split_pair(dv[r].x, dv[r].y, hi0, lo0);
+        split_pair(dv[r].z, dv[r].w, hi1, lo1);
+        const uint32_t off = lds_off(pt, 0) + (ng << 3);
+        *reinterpret_cast<uint2*>(Dh + off) = make_uint2(hi0, hi1);
+        *reinterpret_cast<uint2*>(Dl + off) = make_uint2(lo0, lo1);
+      }
+    }
+  };
+
+  if (g < tiles) load_tile(g);
+  for (int t = g; t < tiles; t += p.G) {
+    __syncthreads();  // the previous tile's reads are done
+    store_tile();
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS stores landed
     __syncthreads();
+    if (t + p.G < tiles) load_tile(t + p.G);
     // ---- this wave's tap over the tile's pixels
-#pragma unroll 2
+#pragma unroll 1
     for (int s = 0; s < TP / 32; ++s) {
       const int pt = 32 * s + 8 * g4 + q;  // (pt and pt + 4: one 8-aligned run of one image row)
       const int img = pt / (TH * TW), r2 = pt - img * (TH * TW);

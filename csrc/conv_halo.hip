@@ -80,7 +80,11 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   constexpr int LOOP = SCR + (BI * NW > NBI ? 1024 : 0);
   constexpr int SW = TN * 32 + 4;
   constexpr int EPI = NW * 32 * SW * 4;
-  constexpr int SMEM = LOOP > EPI ? LOOP : EPI;
+  // (BNF) channels whose (scale, shift) pairs sit in LDS, copied once per workgroup so the loader
+  // reads them without ordering against its output stores — sized where two workgroups still fit
+  // per CU (0: read from global memory; halo_config keeps C within it)
+  constexpr int COEF_C = !BNF ? 0 : DENSE ? (TW == 8 ? 0 : 512) : (TW == 32 ? 128 : TW == 8 ? 256 : 0);
+  constexpr int SMEM = LOOP + COEF_C * 8 > EPI ? LOOP + COEF_C * 8 : EPI;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int lane = threadIdx.x & 63;
@@ -157,26 +161,42 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
                       : nullptr;
   float* bn_ny = (DENSE && p.bn_y && n0 == 0) ? p.bn_y + (long)client * p.bn_y_cs : nullptr;
   const int bn_creal = DENSE ? p.bn_c : p.C;
+  float* coef_s = reinterpret_cast<float*>(smem + LOOP);
   auto issue_halo = [&](int c, int buf) {
     const bool live = c < nchunks;
     unsigned char* Hs = smem + H_OFF + buf * 2 * H_PL;
+    if constexpr (BNF) {
+      // the raw x of RG rows first, so their HBM round trips overlap (one wait per RG rows, not one
+      // per row: the output stores of a row would otherwise order the next row's loads after
+      // them), then per row: (scale, shift), ReLU, split, LDS store (+ the outputs)
+      // (RG 1 where the accumulators leave no VGPRs for it: TM·TN = 4 tiles, the l2 shape)
+      constexpr int RG = TM * TN >= 4 ? 1 : (HI < 3 ? HI : 3);
 #pragma unroll
-    for (int i = 0; i < HI; ++i) {
-      const bool ok = live && h_off[i] >= 0;
-      unsigned char* d = Hs + (i * NW + wid) * 1024;
-      if constexpr (BNF) {
-        // lane's 8 channels: h_off = pixel·C + lc·8 (the DMA's element offset, ldx == C)
+      for (int i0 = 0; i0 < HI; i0 += RG) {
+      float4 xa[RG], xb[RG];
+#pragma unroll
+      for (int i = i0; i < i0 + RG && i < HI; ++i) {
+        const bool ok = live && h_off[i] >= 0;
+        const int e = (ok ? h_off[i] : 0) + c * 32;  // lane's 8 channels: h_off = pixel·ldx + lc·8
+        // (DENSE) real channels of the lane's 8: ≥ 8 all, 4 the first half (bn_c % 4 == 0), ≤ 0
+        // none — channels past the prefix are other layers' (maybe unwritten) slots: never read
+        const int cv = bn_creal - (c * 32 + h_ch[i]);
+        xa[i - i0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        xb[i - i0] = xa[i - i0];
+        if (!DENSE || cv > 0) xa[i - i0] = *reinterpret_cast<const float4*>(bxc + e);
+        if (!DENSE || cv >= 8) xb[i - i0] = *reinterpret_cast<const float4*>(bxc + e + 4);
+      }
+#pragma unroll
+      for (int i = i0; i < i0 + RG && i < HI; ++i) {
+        const bool ok = live && h_off[i] >= 0;
+        unsigned char* d = Hs + (i * NW + wid) * 1024;
         const bool inimg = ok;
         const bool okv = ok && h_bnok[i];
         const int e = (ok ? h_off[i] : 0) + c * 32;
         const int ch = c * 32 + h_ch[i];
-        // (DENSE) real channels of the lane's 8: ≥ 8 all, 4 the first half (bn_c % 4 == 0), ≤ 0
-        // none — channels past the prefix are other layers' (maybe unwritten) slots: never read
         const int cv = bn_creal - ch;
-        float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
-        if (!DENSE || cv > 0) x0 = *reinterpret_cast<const float4*>(bxc + e);
-        if (!DENSE || cv >= 8) x1 = *reinterpret_cast<const float4*>(bxc + e + 4);
-        const float4* cf = reinterpret_cast<const float4*>(bcoef + 2 * ch);  // (scale, shift) pairs
+        const float4 x0 = xa[i - i0], x1 = xb[i - i0];
+        const float4* cf = reinterpret_cast<const float4*>((COEF_C ? coef_s : bcoef) + 2 * ch);  // (scale, shift)
         const float4 c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3];
         float v[8] = {fmaf(x0.x, c0.x, c0.y), fmaf(x0.y, c0.z, c0.w), fmaf(x0.z, c1.x, c1.y), fmaf(x0.w, c1.z, c1.w),
                       fmaf(x1.x, c2.x, c2.y), fmaf(x1.y, c2.z, c2.w), fmaf(x1.z, c3.x, c3.y), fmaf(x1.w, c3.z, c3.w)};
@@ -213,14 +233,20 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
             }
           }
         }
-      } else {
+      }
+      }
+      // (the LDS writes of a register-staged halo must land before the barrier that publishes it)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    } else {
+#pragma unroll
+      for (int i = 0; i < HI; ++i) {
+        const bool ok = live && h_off[i] >= 0;
+        unsigned char* d = Hs + (i * NW + wid) * 1024;
         const uint32_t off = (uint32_t)(h_off[i] + c * 32) * 2u;
         hdma16(ar, d, ok ? off : OOB_OFF);
         hdma16(ar, d + H_PL, ok ? off + a_lo : OOB_OFF);
       }
     }
-    // (the LDS writes of a register-staged halo must land before the barrier that publishes it)
-    if constexpr (BNF) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   };
   auto issue_w = [&](int s, int slot) {
     const bool live = s < nsteps;
@@ -306,6 +332,10 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_halo_kernel(ConvNTPara
   // issue order: halo(0), w(0) [, w(1)] | step s: [wait, barrier] w(s+NBS-1), (HB 2, tap 0)
   // halo(c+1), MFMAs; HB 1: a chunk start first retires the old halo's reads (barrier), loads
   // the new one and waits for everything
+  if constexpr (COEF_C > 0) {
+    for (int i = threadIdx.x; i < 2 * p.C; i += NW * 64) coef_s[i] = bcoef[i];
+    __syncthreads();
+  }
   issue_halo(0, 0);
   issue_w(0, 0);
   if constexpr (NBS == 3) issue_w(1, 1);
@@ -381,6 +411,9 @@ static int halo_config(const ConvNTParams& p) {
     return -1;
   if ((p.x_lo == 0 && p.bn_x == nullptr) || p.wsplit == nullptr) return -1;
   if (p.bn_x != nullptr && (p.b_kmajor || (!dense && p.ldx != p.C))) return -1;
+  // (the LDS copy of the BN coefficients: kernel COEF_C)
+  if (p.bn_x != nullptr && p.C > (dense ? (p.OW == 8 ? 1 << 30 : 512) : (p.OW == 32 ? 128 : p.OW == 8 ? 256 : 1 << 30)))
+    return -1;
   if (dense) {  // DenseNet growth conv (N = growth ≤ 32): 32-wide N tiles, 4 waves of 64 x 32
     if (p.N > 32 || p.bn_c % 4 || p.bn_c > p.C || p.bn_c > p.ldx || (p.bn_y && p.bn_ldy % 4)) return -1;
     if (p.bn_mask && (!p.bn_y || p.bn_ldy % 8 || p.bn_c % 8)) return -1;
