@@ -265,36 +265,51 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ theta, con
   const float a = lr[k];
   const bool fs = first[k] != 0;
   const long base = (long)k * ld;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P4; i += (long)gridDim.x * blockDim.x) {
-    float4 t = reinterpret_cast<float4*>(theta + base)[i];
-    float4 g = reinterpret_cast<const float4*>(grad + base)[i];
-    float tv[4] = {t.x, t.y, t.z, t.w}, gv[4] = {g.x, g.y, g.z, g.w};
-    float mv[4];
-    if (momentum != 0.f) {
-      float4 m = reinterpret_cast<float4*>(mom + base)[i];
-      mv[0] = m.x;
-      mv[1] = m.y;
-      mv[2] = m.z;
-      mv[3] = m.w;
+  // two float4 per thread per trip, both loaded before either is stored: the stores of one trip
+  // would otherwise order the next trip's loads behind them (one HBM round trip per float4)
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x; i0 < P4; i0 += 2 * stride) {
+    float4 t[2], g[2], m[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long i = i0 + u * stride;
+      if (i < P4) {
+        t[u] = reinterpret_cast<float4*>(theta + base)[i];
+        g[u] = reinterpret_cast<const float4*>(grad + base)[i];
+        if (momentum != 0.f) m[u] = reinterpret_cast<float4*>(mom + base)[i];
+      }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gg = gv[j] + wd * tv[j];
+    for (int u = 0; u < 2; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= P4) break;
+      float tv[4] = {t[u].x, t[u].y, t[u].z, t[u].w}, gv[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+      float mv[4] = {0.f, 0.f, 0.f, 0.f};
       if (momentum != 0.f) {
-        mv[j] = fs ? gg : momentum * mv[j] + (1.f - dampening) * gg;
-        gg = nesterov ? gg + momentum * mv[j] : mv[j];
+        mv[0] = m[u].x;
+        mv[1] = m[u].y;
+        mv[2] = m[u].z;
+        mv[3] = m[u].w;
       }
-      tv[j] -= a * gg;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float gg = gv[j] + wd * tv[j];
+        if (momentum != 0.f) {
+          mv[j] = fs ? gg : momentum * mv[j] + (1.f - dampening) * gg;
+          gg = nesterov ? gg + momentum * mv[j] : mv[j];
+        }
+        tv[j] -= a * gg;
+      }
+      reinterpret_cast<float4*>(theta + base)[i] = make_float4(tv[0], tv[1], tv[2], tv[3]);
+      if (momentum != 0.f) reinterpret_cast<float4*>(mom + base)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      if (shadow) {
+        uint2 uu;
+        uu.x = (uint32_t)f2bf(tv[0]) | ((uint32_t)f2bf(tv[1]) << 16);
+        uu.y = (uint32_t)f2bf(tv[2]) | ((uint32_t)f2bf(tv[3]) << 16);
+        reinterpret_cast<uint2*>(shadow + base)[i] = uu;
+      }
+      if (split) store_split4(split, k, ld, i, tv);
     }
-    reinterpret_cast<float4*>(theta + base)[i] = make_float4(tv[0], tv[1], tv[2], tv[3]);
-    if (momentum != 0.f) reinterpret_cast<float4*>(mom + base)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
-    if (shadow) {
-      uint2 u;
-      u.x = (uint32_t)f2bf(tv[0]) | ((uint32_t)f2bf(tv[1]) << 16);
-      u.y = (uint32_t)f2bf(tv[2]) | ((uint32_t)f2bf(tv[3]) << 16);
-      reinterpret_cast<uint2*>(shadow + base)[i] = u;
-    }
-    if (split) store_split4(split, k, ld, i, tv);
   }
 }
 
