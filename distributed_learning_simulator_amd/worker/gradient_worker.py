@@ -109,6 +109,9 @@ class GradientWorker(AggregationWorker):
         one = torch.ones(1, dtype=torch.bool, device=tr.device)
         firsts = (torch.ones(1, dtype=torch.bool, device=tr.device), torch.zeros(1, dtype=torch.bool, device=tr.device))
         e = 0
+        if tr.device.type == "cuda" and round_num == 1:
+            get_logger().info("gradient worker: %.1f GiB allocated before the first wave (%d clients per wave)",
+                              torch.cuda.memory_allocated(tr.device) / 2**30, cap)
         try:
             self._steps(S, sched, local, cap, tr, sess, b, wd, theta0, sizes, stats, epochs, P, clients, nbytes,
                         steps_per_epoch, on_epoch, split, lr_e, one, firsts)
