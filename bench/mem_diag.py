@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--K", type=int, nargs="+", default=[1, 2, 4])
     ap.add_argument("--shared", type=int, default=1, help="1: all clients read parameter row 0 (sign-SGD)")
     ap.add_argument("--planes", type=int, default=1, help="1: weight planes live (split-plane GEMMs)")
+    ap.add_argument("--scale", type=float, default=0.002, help="dataset_kwargs scale (procedural above the limit)")
     args = ap.parse_args()
     from distributed_learning_simulator_amd.data.datasets import create_dataset_collection, get_spec
     from distributed_learning_simulator_amd.engine.memory import probe_activation_bytes, state_bytes_per_client
@@ -35,8 +36,8 @@ def main():
 
     build.build()
     dev = torch.device("cuda", 0)
-    spec = get_spec(args.dataset, {"scale": 0.002})
-    dc = create_dataset_collection(args.dataset, {"scale": 0.002}, 0, dev, torch.float32,
+    spec = get_spec(args.dataset, {"scale": args.scale})
+    dc = create_dataset_collection(args.dataset, {"scale": args.scale}, 0, dev, torch.float32,
                                    image_channels=stored_image_channels(args.model, spec))
     model = build_model(args.model, dc.spec)
     hyper = HyperParameter(epoch=1, batch_size=args.batch, learning_rate=0.001)
@@ -64,7 +65,8 @@ def main():
         loss.sum().backward()
         torch.cuda.synchronize()
         peak = torch.cuda.max_memory_allocated() - base
-        print(json.dumps({"K": K, "shared": args.shared, "planes": args.planes, "fwd_peak_mib": fwd_peak / 2**20,
+        print(json.dumps({"K": K, "scale": args.scale, "base_mib": base / 2**20, "materialized": dc.train.materialized,
+                          "shared": args.shared, "planes": args.planes, "fwd_peak_mib": fwd_peak / 2**20,
                           "step_peak_mib": peak / 2**20, "per_client_mib": peak / K / 2**20,
                           "probe_ratio": peak / K / max(probe, 1)}), flush=True)
         del tr, x, y, loss
