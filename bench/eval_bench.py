@@ -36,6 +36,8 @@ def main():
                     help="1: bn1 applied in conv2's halo loader (options.bn_fused_halo), 0: unfused")
     ap.add_argument("--n-test", type=int, default=10000)
     ap.add_argument("--no-planes", action="store_true", help="A/B: evaluate without weight planes")
+    ap.add_argument("--halo-mode", type=int, nargs="+", default=[-1],
+                    help="conv_halo_set_mode: -1 shape rule, 1 every supported shape (the 4x4 l4 convs too)")
     args = ap.parse_args()
 
     from distributed_learning_simulator_amd.ops import build
@@ -57,13 +59,17 @@ def main():
 
     from distributed_learning_simulator_amd import options
 
-    settings = [(mi, st, fu) for mi in args.max_images for st in args.streams for fu in args.fused]
+    from distributed_learning_simulator_amd.ops import hip
+
+    settings = [(mi, st, fu, hm) for mi in args.max_images for st in args.streams for fu in args.fused
+                for hm in args.halo_mode]
     best = {}
     out = {}
     for _ in range(args.rounds):
-        for mi, st, fu in settings:
+        for mi, st, fu, hm in settings:
             tr.num_streams = st
             options.update(bn_fused_halo=bool(fu))
+            hip._C.conv_halo_set_mode(hm)
             tr.evaluate(rows, max_images=mi)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -71,14 +77,15 @@ def main():
                 loss, corr, n = tr.evaluate(rows, max_images=mi)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / args.iters
-            if dt < best.get((mi, st, fu), float("inf")):
-                best[(mi, st, fu)] = dt
-                out[(mi, st, fu)] = (n, float((corr / n).mean()))
-    for (mi, st, fu), dt in best.items():
-        n, acc = out[(mi, st, fu)]
+            if dt < best.get((mi, st, fu, hm), float("inf")):
+                best[(mi, st, fu, hm)] = dt
+                out[(mi, st, fu, hm)] = (n, float((corr / n).mean()))
+    hip._C.conv_halo_set_mode(-1)
+    for (mi, st, fu, hm), dt in best.items():
+        n, acc = out[(mi, st, fu, hm)]
         imgs = args.M * n
         print(json.dumps({"bench": "eval_resnet18_fp32", "M": args.M, "n_test": n, "planes": not args.no_planes,
-                          "max_images": mi, "streams": st, "bn_fused_halo": bool(fu), "ms_per_chunk": dt * 1e3, "ms_per_model": dt * 1e3 / args.M,
+                          "max_images": mi, "streams": st, "bn_fused_halo": bool(fu), "halo_mode": hm, "ms_per_chunk": dt * 1e3, "ms_per_model": dt * 1e3 / args.M,
                           "images_per_s": imgs / dt, "fwd_tflops": imgs * FWD_GFLOP_RESNET18_CIFAR / dt / 1e3,
                           "acc_mean": acc}), flush=True)
 
