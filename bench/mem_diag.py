@@ -60,7 +60,7 @@ def main():
         torch.cuda.synchronize()
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
-        loss, _ = tr.forward_loss(K, x, y, valid, shared=bool(args.shared))
+        loss, correct = tr.forward_loss(K, x, y, valid, shared=bool(args.shared))
         fwd_peak = torch.cuda.max_memory_allocated() - base
         loss.sum().backward()
         torch.cuda.synchronize()
@@ -69,8 +69,9 @@ def main():
                           "shared": args.shared, "planes": args.planes, "fwd_peak_mib": fwd_peak / 2**20,
                           "step_peak_mib": peak / 2**20, "per_client_mib": peak / K / 2**20,
                           "probe_ratio": peak / K / max(probe, 1)}), flush=True)
-        del tr, x, y, loss
-        tr = None
+        # (`correct` too: any live output keeps the whole graph, and the convolutions' activations
+        # live in its contexts)
+        del tr, x, y, loss, correct
 
 
 if __name__ == "__main__":

@@ -164,6 +164,11 @@ class GradientWorker(AggregationWorker):
                         stats.loss_sum[ee, w0:w1] += loss.detach() * vf
                         stats.correct[ee, w0:w1] += correct
                         stats.samples[ee, w0:w1] += vf
+                    # drop this wave's autograd graph before the next wave's forward: the
+                    # convolutions keep their activations in the graph's contexts until it dies,
+                    # so a live `loss` doubled the wave's footprint (bench/oom_diag.py: the second
+                    # 15-client wave of sign-SGD ResNet-50 ran out of memory at 285 GB)
+                    x = y = loss = correct = g = payload = None
                     w0 = w1
             self._reduce(acc)
             with torch.no_grad():

@@ -146,6 +146,37 @@ def test_sign_sgd_bytes(tmp_path):
     assert result["metrics"][0]["comm_bytes_up"] == 3 * steps * ((P + 7) // 8)
 
 
+def test_gradient_worker_frees_each_wave_graph(tmp_path, monkeypatch):
+    """A synchronous-gradient step trained in several waves must drop a wave's autograd graph
+    before the next wave's forward: the convolutions keep activations in the graph's contexts, so
+    a live `loss` from the previous wave doubled the footprint (sign-SGD ResNet-50's second
+    15-client wave ran out of memory)."""
+    import weakref
+
+    from distributed_learning_simulator_amd.engine import trainer as trainer_mod
+
+    orig = trainer_mod.CohortTrainer.forward_loss
+    prev: list = []
+    waves = [0]
+
+    def forward_loss(self, K, *a, **kw):
+        if kw.get("shared"):
+            waves[0] += 1
+            if prev:
+                gc_alive = [r() is not None for r in prev]
+                assert not any(gc_alive), "the previous wave's loss graph is still alive"
+            prev.clear()
+        loss, correct = orig(self, K, *a, **kw)
+        if kw.get("shared"):
+            prev.extend([weakref.ref(loss), weakref.ref(correct)])
+        return loss, correct
+
+    monkeypatch.setattr(trainer_mod.CohortTrainer, "forward_loss", forward_loss)
+    _run("sign_sgd/cifar10.yaml", {"epoch": 1, "worker_number": 4, "model_name": "LeNet5", "cohort_size": 2,
+                                   "dataset_kwargs.scale": 0.02, "log_level": "WARNING"}, tmp_path)
+    assert waves[0] >= 4  # two waves per step
+
+
 def test_iid_keeps_best_validation_model(tmp_path, monkeypatch):
     """IID sampling ⇒ each client uploads its best-validation-accuracy model of the round
     (reference aggregation_worker.py:28-29,82-86), not the last epoch's."""
