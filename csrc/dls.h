@@ -247,6 +247,9 @@ bool conv_halo_bn_supported(int B, int H, int W, int C, int N);
 void bn_coef_sums(const double* sums, long sums_cs, int ldp, const float* gamma, const float* beta,
                   const int* valid_rows, long g_cs, int K, int R, int C, float eps, int rep, float* mean, float* rstd,
                   float* coef, hipStream_t s);
+// running fp64 channel sums of a DenseNet block: out[k·out_cs + j·ldo + c] = Σ_p part[k][p][j][c]
+// (part [K][nparts][2][g] fp32 conv-epilogue partials; 2·g ≤ 1024)
+void part_sum_f64(const float* part, int K, int nparts, int g, double* out, long out_cs, int ldo, hipStream_t s);
 // BN apply with precomputed (scale, shift) coefficients (bn_fwd coef_out) → split planes (+ ReLU bits)
 void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
                    bf16_t* yp, uint8_t* rmask, hipStream_t s);

@@ -226,6 +226,41 @@ static int coef_groups() {
   return native_option(g_opt_bn_coef_groups, "DLS_BN_COEF_GROUPS", 8) == 32 ? 32 : 8;
 }
 
+// DenseNet running channel sums: out[k·out_cs + j·ldo + c] = Σ_p part[k][p][j][c] in fp64 (j = Σx, Σx²;
+// c < g new channels) — the epilogue partials of one growth conv summed into the block's running
+// sums in one launch (one 1024-thread workgroup per client, four independent fp64 chains per
+// thread so the loads pipeline, all combined in a fixed order: deterministic). Replaces a PyTorch
+// fp64 reduction over the middle dimension plus a strided copy (≈ 170 µs per layer).
+__global__ void __launch_bounds__(1024) part_sum_f64_kernel(const float* __restrict__ part, int nparts, int g,
+                                                            double* __restrict__ out, long out_cs, int ldo) {
+  __shared__ double red[1024];
+  const int k = blockIdx.x, ncol = 2 * g, t = threadIdx.x;
+  const int groups = 1024 / ncol;  // (host: ncol <= 1024)
+  const int col = t % ncol, grp = t / ncol;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (grp < groups) {
+    const float* pk = part + (long)k * nparts * ncol + col;
+    const long st = (long)groups * ncol;
+    int p = grp;
+    for (; p + 3 * groups < nparts; p += 4 * groups) {
+      const float* q = pk + (long)p * ncol;
+      a0 += (double)q[0];
+      a1 += (double)q[st];
+      a2 += (double)q[2 * st];
+      a3 += (double)q[3 * st];
+    }
+    for (; p < nparts; p += groups) a0 += (double)pk[(long)p * ncol];
+  }
+  red[t] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (t < ncol) {
+    double a = 0.0;
+    for (int q = 0; q < groups; ++q) a += red[q * ncol + t];
+    out[(long)k * out_cs + (long)(t / g) * ldo + (t % g)] = a;
+  }
+}
+
+
 // First stage for the conv-epilogue statistics, which arrive as one partial per 32 GEMM rows
 // (2,048 per client on a 32x32x64 layer): a single (32-channel, client) workgroup reading them
 // one after another took ~0.4 ms per BN layer (latency-bound: 2 x 33 workgroups on 256 CUs).
@@ -762,6 +797,11 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
                                      valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx, dxp,
                                      dx_f32));
   });
+}
+
+void part_sum_f64(const float* part, int K, int nparts, int g, double* out, long out_cs, int ldo, hipStream_t s) {
+  if (K == 0) return;
+  hipLaunchKernelGGL(part_sum_f64_kernel, dim3(K), dim3(1024), 0, s, part, nparts, g, out, out_cs, ldo);
 }
 
 void bn_coef_sums(const double* sums, long sums_cs, int ldp, const float* gamma, const float* beta,

@@ -176,6 +176,14 @@ def _build_locked(force: bool, jobs: int, verbose: bool) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    # a host function left undefined (e.g. declared in dls.h but defined inside an anonymous
+    # namespace) links fine into a shared object and only fails at import: dlopen it (RTLD_NOW) in
+    # a child process here, on the build machine, instead
+    r = subprocess.run([sys.executable, "-c", "import ctypes, sys; ctypes.CDLL(sys.argv[1])", tmp],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        os.remove(tmp)
+        raise RuntimeError(f"the linked extension does not load:\n{r.stderr.strip()[-2000:]}")
     os.replace(tmp, TARGET)
     if source_hash() != digest:  # a source changed during the build: rebuild what it touched
         return _build_locked(False, jobs, verbose)

@@ -858,7 +858,7 @@ class _DenseBlock(torch.autograd.Function):
                                                stats=part, stats_valid=samples if cache else None, ny=y, mask=mask)
                 assert ok, "dense halo conv refused a shape halo_bn_dense_ok accepted"
                 if cache:
-                    S[:, :, ci : ci + growth] = part.sum(dim=1, dtype=torch.float64)
+                    be.part_sum_f64(part, S[:, :, ci : ci + growth])
             elif native:
                 y, mean, rstd, mask = be.bn_fwd(xi, lp.gamma, lp.beta, valid_rows, True, None, with_mask=True)
                 be.conv_fwd(y.view(K, B, H, W, ci), lp.w, 1, 1, out=F[..., ci : ci + growth])

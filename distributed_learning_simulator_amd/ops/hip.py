@@ -622,6 +622,16 @@ def bn_coef_sums(sums, C: int, gamma, beta, R: int, valid_rows=None, eps=1e-5):
     return coef, mean, rstd
 
 
+def part_sum_f64(part, out):
+    """out[k, j, c] = Σ_p part[k, p, j, c] in fp64, fixed order (DenseNet running channel sums):
+    `part` [K, parts, 2, g] fp32 conv-epilogue partials, `out` an fp64 [K, 2, g] view with unit
+    channel stride (a channel slice of the block's [K, 2, Ct] sums)."""
+    K, nparts, two, g = part.shape
+    assert two == 2 and part.dtype == F32 and part.is_contiguous() and 2 * g <= 1024
+    assert out.dtype == torch.float64 and out.shape == (K, 2, g) and out.stride(2) == 1
+    _C.part_sum_f64(_p(part), K, nparts, g, _p(out), out.stride(0), out.stride(1), _s())
+
+
 def halo_bn_ok(shape, w) -> bool:
     """conv_halo_bn_fwd serves a [K, B, H, W, C] fp32 input and a 3x3 weight of this shape."""
     K, B, H, W, C = shape

@@ -871,6 +871,22 @@ def test_dense_growth_conv_with_fused_bn(hip, case):
     _close(out, ref.conv_fwd(z, _d(w).expand(K, -1, -1, -1, -1), 1, 1))
 
 
+@pytest.mark.parametrize("K,nparts,g,Ct,c0", [(3, 2048, 12, 64, 28), (2, 7, 12, 40, 0), (2, 513, 16, 96, 80),
+                                              (1, 64, 128, 256, 64)])
+def test_part_sum_f64(hip, K, nparts, g, Ct, c0):
+    """DenseNet running sums: the conv-epilogue partials [K, parts, 2, g] summed in fp64 into a
+    channel slice of [K, 2, Ct], other channels untouched."""
+    torch.manual_seed(0)
+    part = _f(K, nparts, 2, g, scale=3.0)
+    S = torch.full((K, 2, Ct), 7.0, dtype=torch.float64, device=DEV)
+    hip.part_sum_f64(part, S[:, :, c0 : c0 + g])
+    exp = torch.full((K, 2, Ct), 7.0, dtype=torch.float64)
+    exp[:, :, c0 : c0 + g] = _d(part).sum(dim=1)
+    out = S.cpu()
+    assert torch.equal(out[:, :, :c0], exp[:, :, :c0]) and torch.equal(out[:, :, c0 + g :], exp[:, :, c0 + g :])
+    assert (out - exp).abs().max().item() <= 1e-12 * exp.abs().max().item()
+
+
 @pytest.mark.parametrize("case", [(2, 4, 32, 28, 160, 12), (3, 4, 16, 172, 304, 12), (2, 4, 8, 436, 448, 12),
                                   (2, 2, 32, 16, 160, 12), (2, 4, 16, 64, 96, 16)])
 def test_dense_wgrad_halo(hip, case):
