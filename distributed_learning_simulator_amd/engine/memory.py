@@ -107,15 +107,9 @@ def plan_capacity(wanted: int, layout, model, dc, hyper, device, compute_dtype,
     state = state_bytes_per_client(layout, compute_dtype, hyper.optimizer_name)
     with DEVICE_LOCK:
         act = probe_activation_bytes(model, dc, hyper, device, compute_dtype)
-    # allocator slack: the probe already over-counts a wave's clients (one client's saved tensors
-    # + twice its largest; measured 10.3-10.5 GB per client against an 11.6 GB probe at 15 clients of
-    # ResNet-50 224², profiles/r4_c21_mem_*.log, r4_c27_signsgd.log)
-    per_client = state + int(act * 1.05)
+    per_client = state + int(act * 1.15)  # allocator slack
     free, _total = torch.cuda.mem_get_info(device)
     cap = max(1, min(wanted, int(math.floor(fraction * free / max(per_client, 1)))))
-    # balanced waves: as many waves as the cap needs, each as full as the others (128 clients at a
-    # cap of 17: 8 waves of 16, not 7 of 17 and one of 9)
-    cap = -(-wanted // -(-wanted // cap))
     get_logger().info("memory plan: %.1f MiB state + %.1f MiB activations per client, %.1f GiB free "
                       "-> %d of %d clients resident per wave", state / 2**20, act / 2**20, free / 2**30, cap, wanted)
     return cap
