@@ -250,6 +250,12 @@ void bn_coef_sums(const double* sums, long sums_cs, int ldp, const float* gamma,
 // running fp64 channel sums of a DenseNet block: out[k·out_cs + j·ldo + c] = Σ_p part[k][p][j][c]
 // (part [K][nparts][2][g] fp32 conv-epilogue partials; 2·g ≤ 1024)
 void part_sum_f64(const float* part, int K, int nparts, int g, double* out, long out_cs, int ldo, hipStream_t s);
+// fp64 Σx, Σx² of the C channels of x [K][R rows at stride ldx] over each client's first valid[k]
+// rows → out[k·out_cs + j·ldo + c] (j = 0: Σx, 1: Σx²); ws: chan_sums_f64_ws(R, C) doubles per
+// client; 2·C ≤ 1024
+long chan_sums_f64_ws(int R, int C);
+void chan_sums_f64(const float* x, long x_cs, int ldx, int K, int R, int C, const int* valid, double* ws, double* out,
+                   long out_cs, int ldo, hipStream_t s);
 // BN apply with precomputed (scale, shift) coefficients (bn_fwd coef_out) → split planes (+ ReLU bits)
 void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
                    bf16_t* yp, uint8_t* rmask, hipStream_t s);

@@ -231,7 +231,8 @@ static int coef_groups() {
 // sums in one launch (one 1024-thread workgroup per client, four independent fp64 chains per
 // thread so the loads pipeline, all combined in a fixed order: deterministic). Replaces a PyTorch
 // fp64 reduction over the middle dimension plus a strided copy (≈ 170 µs per layer).
-__global__ void __launch_bounds__(1024) part_sum_f64_kernel(const float* __restrict__ part, int nparts, int g,
+template <typename T>
+__global__ void __launch_bounds__(1024) part_sum_f64_kernel(const T* __restrict__ part, int nparts, int g,
                                                             double* __restrict__ out, long out_cs, int ldo) {
   __shared__ double red[1024];
   const int k = blockIdx.x, ncol = 2 * g, t = threadIdx.x;
@@ -239,11 +240,11 @@ __global__ void __launch_bounds__(1024) part_sum_f64_kernel(const float* __restr
   const int col = t % ncol, grp = t / ncol;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (grp < groups) {
-    const float* pk = part + (long)k * nparts * ncol + col;
+    const T* pk = part + (long)k * nparts * ncol + col;
     const long st = (long)groups * ncol;
     int p = grp;
     for (; p + 3 * groups < nparts; p += 4 * groups) {
-      const float* q = pk + (long)p * ncol;
+      const T* q = pk + (long)p * ncol;
       a0 += (double)q[0];
       a1 += (double)q[st];
       a2 += (double)q[2 * st];
@@ -260,6 +261,45 @@ __global__ void __launch_bounds__(1024) part_sum_f64_kernel(const float* __restr
   }
 }
 
+
+// DenseNet block input: fp64 Σx, Σx² of every channel over a chunk of `rb` rows (rows at stride
+// ldx, rows past the client's valid count excluded) → part[k][chunk][2][C]; part_sum_f64_kernel<double>
+// then folds the chunks in order into the running sums (replaces PyTorch casts + reductions)
+__global__ void __launch_bounds__(256) chan_sums_f64_kernel(const float* __restrict__ x, long x_cs, int ldx, int R,
+                                                            int C, const int* __restrict__ valid, int rb,
+                                                            double* __restrict__ part, int nch) {
+  __shared__ double r0[256], r1[256];
+  const int k = blockIdx.y, ch = blockIdx.x, t = threadIdx.x;
+  const int nv = valid ? min(valid[k], R) : R;
+  const int rbeg = ch * rb, rend = min(nv, rbeg + rb);
+  const float* xk = x + (long)k * x_cs;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    const int ctn = min(256, C - c0), S = 256 / ctn;
+    const int cc = t % ctn, sg = t / ctn;
+    double s0 = 0.0, s1 = 0.0;
+    if (sg < S) {
+#pragma unroll 4
+      for (int r = rbeg + sg; r < rend; r += S) {
+        const double v = (double)xk[(long)r * ldx + c0 + cc];
+        s0 += v;
+        s1 = fma(v, v, s1);
+      }
+    }
+    r0[t] = s0;
+    r1[t] = s1;
+    __syncthreads();
+    if (sg == 0) {
+      for (int j = 1; j < S; ++j) {
+        s0 += r0[j * ctn + cc];
+        s1 += r1[j * ctn + cc];
+      }
+      double* pp = part + ((long)k * nch + ch) * 2 * C + c0 + cc;
+      pp[0] = s0;
+      pp[C] = s1;
+    }
+    __syncthreads();
+  }
+}
 
 // First stage for the conv-epilogue statistics, which arrive as one partial per 32 GEMM rows
 // (2,048 per client on a 32x32x64 layer): a single (32-channel, client) workgroup reading them
@@ -801,7 +841,18 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
 
 void part_sum_f64(const float* part, int K, int nparts, int g, double* out, long out_cs, int ldo, hipStream_t s) {
   if (K == 0) return;
-  hipLaunchKernelGGL(part_sum_f64_kernel, dim3(K), dim3(1024), 0, s, part, nparts, g, out, out_cs, ldo);
+  hipLaunchKernelGGL(part_sum_f64_kernel<float>, dim3(K), dim3(1024), 0, s, part, nparts, g, out, out_cs, ldo);
+}
+
+long chan_sums_f64_ws(int R, int C) { return (long)cdiv(R, 256) * 2 * C; }  // doubles per client
+
+void chan_sums_f64(const float* x, long x_cs, int ldx, int K, int R, int C, const int* valid, double* ws, double* out,
+                   long out_cs, int ldo, hipStream_t s) {
+  if (K == 0 || R == 0) return;
+  const int rb = 256, nch = cdiv(R, rb);
+  hipLaunchKernelGGL(chan_sums_f64_kernel, dim3(nch, K), dim3(256), 0, s, x, x_cs, ldx, R, C, valid, rb, ws, nch);
+  hipLaunchKernelGGL(part_sum_f64_kernel<double>, dim3(K), dim3(1024), 0, s, (const double*)ws, nch, C, out, out_cs,
+                     ldo);
 }
 
 void bn_coef_sums(const double* sums, long sums_cs, int ldp, const float* gamma, const float* beta,

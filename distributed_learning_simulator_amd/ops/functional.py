@@ -831,11 +831,14 @@ class _DenseBlock(torch.autograd.Function):
         if cache:
             S = torch.zeros((K, 2, Ct), dtype=torch.float64, device=x.device)
             x3 = F[..., :c0].reshape(K, R, c0)
-            if valid_rows is not None:
-                keep = (torch.arange(R, device=x.device).view(1, R) < valid_rows.view(K, 1)).unsqueeze(-1)
-                x3 = torch.where(keep, x3, torch.zeros((), dtype=x3.dtype, device=x.device))
-            S[:, 0, :c0] = x3.sum(dim=1, dtype=torch.float64)
-            S[:, 1, :c0] = (x3 * x3).sum(dim=1, dtype=torch.float64)
+            if 2 * c0 <= 1024:  # (the fixed-order fp64 kernel's column limit)
+                be.chan_sums_f64(x3, valid_rows, S[:, :, :c0])
+            else:
+                if valid_rows is not None:
+                    keep = (torch.arange(R, device=x.device).view(1, R) < valid_rows.view(K, 1)).unsqueeze(-1)
+                    x3 = torch.where(keep, x3, torch.zeros((), dtype=x3.dtype, device=x.device))
+                S[:, 0, :c0] = x3.sum(dim=1, dtype=torch.float64)
+                S[:, 1, :c0] = (x3.double() * x3.double()).sum(dim=1)
             samples = valid_rows // (H * W) if valid_rows is not None else None
         for i, lp in enumerate(layers):
             ci = c0 + i * growth

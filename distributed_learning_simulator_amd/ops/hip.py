@@ -632,6 +632,20 @@ def part_sum_f64(part, out):
     _C.part_sum_f64(_p(part), K, nparts, g, _p(out), out.stride(0), out.stride(1), _s())
 
 
+def chan_sums_f64(x, valid_rows, out):
+    """out[k, 0, c] = Σ x[k, r, c], out[k, 1, c] = Σ x[k, r, c]² over r < valid_rows[k] (all rows
+    if None), in fp64 with a fixed order (DenseNet block input's running sums). `x` [K, R, C] fp32
+    with unit channel stride (a channel prefix of a wider buffer is fine); `out` an fp64 [K, 2, C]
+    view with unit channel stride."""
+    K, R, C = x.shape
+    x, ldx = _pix_stride(x)
+    assert x.dtype == F32 and x.stride(0) == R * ldx and 2 * C <= 1024
+    assert out.dtype == torch.float64 and out.shape == (K, 2, C) and out.stride(2) == 1
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    ws = torch.empty(max(1, K * _C.chan_sums_f64_ws(R, C)), dtype=torch.float64, device=x.device)
+    _C.chan_sums_f64(_p(x), x.stride(0), ldx, K, R, C, _p(vr), _p(ws), _p(out), out.stride(0), out.stride(1), _s())
+
+
 def halo_bn_ok(shape, w) -> bool:
     """conv_halo_bn_fwd serves a [K, B, H, W, C] fp32 input and a 3x3 weight of this shape."""
     K, B, H, W, C = shape

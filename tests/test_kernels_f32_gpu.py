@@ -887,6 +887,27 @@ def test_part_sum_f64(hip, K, nparts, g, Ct, c0):
     assert (out - exp).abs().max().item() <= 1e-12 * exp.abs().max().item()
 
 
+@pytest.mark.parametrize("K,R,C,ld,valid", [(3, 65536, 24, 168, None), (2, 4096, 312, 312, [4096, 1000]),
+                                            (2, 1000, 168, 200, [999, 0]), (1, 300, 8, 8, [257])])
+def test_chan_sums_f64(hip, K, R, C, ld, valid):
+    """DenseNet block input's running sums: fp64 Σx, Σx² per channel over each client's valid rows,
+    read from a channel prefix of a wider buffer."""
+    torch.manual_seed(1)
+    buf = _f(K, R, ld, scale=2.0)
+    x = buf[..., :C]
+    vr = torch.tensor(valid, dtype=torch.int32, device=DEV) if valid is not None else None
+    S = torch.full((K, 2, C + 5), 3.0, dtype=torch.float64, device=DEV)
+    hip.chan_sums_f64(x, vr, S[:, :, :C])
+    xd = _d(x)
+    if valid is not None:
+        keep = torch.arange(R).view(1, R, 1) < torch.tensor(valid).view(K, 1, 1)
+        xd = torch.where(keep, xd, torch.zeros((), dtype=xd.dtype))
+    exp = torch.stack([xd.sum(dim=1), (xd * xd).sum(dim=1)], dim=1)
+    out = S.cpu()
+    assert torch.equal(out[:, :, C:], torch.full((K, 2, 5), 3.0, dtype=torch.float64))
+    assert (out[:, :, :C] - exp).abs().max().item() <= 1e-12 * exp.abs().max().item()
+
+
 @pytest.mark.parametrize("case", [(2, 4, 32, 28, 160, 12), (3, 4, 16, 172, 304, 12), (2, 4, 8, 436, 448, 12),
                                   (2, 2, 32, 16, 160, 12), (2, 4, 16, 64, 96, 16)])
 def test_dense_wgrad_halo(hip, case):
