@@ -380,6 +380,8 @@ void adam_step(float* theta, const float* grad, float* m, float* v, bf16_t* shad
 void broadcast_rows(float* theta, bf16_t* shadow, const float* src, int K, long P, long ld, hipStream_t s);
 // split[k] = (bf16 hi plane, bf16 lo plane) of theta[k] rows ([K][2][ld] bf16)
 void split_rows(const float* theta, bf16_t* split, int K, long P, long ld, hipStream_t s);
+// [K][2][rows][C32] split planes of rows of C fp32 values (client stride w_cs) zero-padded to C32
+void split_rows_padded(const float* w, long w_cs, int K, int rows, int C, int C32, bf16_t* out, hipStream_t s);
 void delta_rows(const float* theta, const float* base, float* out, int K, long P, long ld, hipStream_t s);
 // out += Σ_k w_k x[k] / num += Σ w m x, den += Σ w m: fp64 accumulators (in place)
 void weighted_sum(const float* x, const double* w, double* out, int K, long P, long ld, hipStream_t s);

@@ -254,6 +254,23 @@ __global__ void __launch_bounds__(256) split_rows_kernel(const float* __restrict
   }
 }
 
+// split planes of rows of C values zero-padded to C32 (DenseNet growth-conv weights for the halo
+// kernel, which stages whole 32-channel chunks): out[k][p][r][c] = split_p(c < C ? w[k][r][c] : 0),
+// one launch instead of a zero fill, a strided copy and the split pass
+__global__ void __launch_bounds__(256) split_rows_padded_kernel(const float* __restrict__ w, long w_cs, int rows, int C,
+                                                                int C32, bf16_t* __restrict__ out) {
+  const int k = blockIdx.y;
+  const long n = (long)rows * C32;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int r = (int)(i / C32), c = (int)(i - (long)r * C32);
+  const float v = c < C ? w[(long)k * w_cs + (long)r * C + c] : 0.f;
+  bf16_t hi, lo;
+  split2(v, hi, lo);
+  out[(long)k * 2 * n + i] = hi;
+  out[(long)k * 2 * n + n + i] = lo;
+}
+
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ theta, const float* __restrict__ grad,
                                                   float* __restrict__ mom, bf16_t* __restrict__ shadow,
                                                   bf16_t* __restrict__ split,
@@ -892,6 +909,13 @@ void sgd_step(float* theta, const float* grad, float* mom, bf16_t* shadow, bf16_
   dim3 grid(grid_for(P4, 256, 1024), K);
   hipLaunchKernelGGL(sgd_kernel, grid, dim3(256), 0, s, theta, grad, mom, shadow, split, lr, active, first, P4, ld, wd,
                      momentum, dampening, nesterov);
+}
+
+void split_rows_padded(const float* w, long w_cs, int K, int rows, int C, int C32, bf16_t* out, hipStream_t s) {
+  const long n = (long)rows * C32;
+  if (K == 0 || n == 0) return;
+  hipLaunchKernelGGL(split_rows_padded_kernel, dim3((unsigned)cdiv(n, 256), K), dim3(256), 0, s, w, w_cs, rows, C, C32,
+                     out);
 }
 
 void split_rows(const float* theta, bf16_t* split, int K, long P, long ld, hipStream_t s) {

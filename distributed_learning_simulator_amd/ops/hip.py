@@ -747,9 +747,10 @@ def dense_weight_planes(w) -> torch.Tensor:
     chunks (the halo kernel stages whole chunks; tap rows then start 64-B aligned)."""
     Kw, N, KH, KW, C = w.shape
     C32 = _c32(C)
-    wp = torch.zeros((Kw, N, KH, KW, C32), dtype=F32, device=w.device)
-    wp[..., :C].copy_(w)
-    return split_planes(wp)
+    assert w.dtype == F32 and w[0].is_contiguous()
+    out = torch.empty((Kw, 2, N, KH, KW, C32), dtype=BF16, device=w.device)
+    _C.split_rows_padded(_p(w), w.stride(0) if Kw > 1 else 0, Kw, N * KH * KW, C, C32, _p(out), _s())
+    return out
 
 
 def conv_halo_bn_dense_fwd(x, coef, relu: bool, valid_rows, w, out, w_planes=None, stats=None, stats_valid=None,
