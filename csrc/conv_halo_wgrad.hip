@@ -38,7 +38,10 @@ __device__ __forceinline__ uint32_t wh_off(int row, int slot) {
 
 constexpr int kSlab = 64 * 9 * 64;  // floats of one workgroup's partial dW block
 
-// XM: 0 X as bf16 planes, 1 fp32, 2 fp32 + BatchNorm(+ReLU) in the loader; DM: 0 dY planes, 1 fp32.
+// XM: 0 X as bf16 planes, 1 fp32, 2 fp32 + BatchNorm(+ReLU) in the loader; DM: 0 dY planes, 1 fp32,
+// 2 the BatchNorm backward of an fp32 output gradient applied in the loader (HaloWgradParams bb_*):
+// the consumer of a BN's input gradient stages it from (dy, x, ReLU bits) itself, and writes its
+// split planes for the dgrad on the way — no separate BN-backward apply pass over HBM.
 // Tiles of TH rows × TW columns of one image (TW ≤ W: a 32-wide image is two column tiles).
 // LDS holds two tiles (X halo + dY, hi and lo planes each): tile t + 1 is written from registers
 // into the other buffer halfway through tile t's MFMAs, and tile t + 2's global loads are issued
@@ -54,9 +57,10 @@ __global__ void __launch_bounds__(768, 1) halo_wgrad_kernel(HaloWgradParams p) {
   constexpr int XT = (HP * 8 + NT - 1) / NT, DT = (TP * 8 + NT - 1) / NT;
   constexpr int KS = TP / 16;
   static_assert(TP % 16 == 0 && TW % 8 == 0 && XT <= 32 && KS >= 2, "tile");
-  constexpr int COEF = XM == 2 ? 512 : 0;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + COEF];
+  constexpr int COEF = XM == 2 ? 512 : 0, DCOEF = DM == 2 ? 768 : 0;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + COEF + DCOEF];
   float* const coef_s = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* const dcoef_s = reinterpret_cast<float*>(smem + 2 * BUF + COEF);  // (DM 2) (a, d, e) × 64
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -80,16 +84,30 @@ __global__ void __launch_bounds__(768, 1) halo_wgrad_kernel(HaloWgradParams p) {
                             (uint32_t)(XM == 0 ? (p.x_lo + npix * p.ldx) * 2 : npix * p.ldx * 4));
   const auto dr = make_rsrc(reinterpret_cast<const unsigned char*>(p.dy) + client * p.dy_cs * (DM == 0 ? 2 : 4),
                             (uint32_t)(DM == 0 ? (p.dy_lo + npix * p.ldy) * 2 : npix * p.ldy * 4));
+  // (DM 2) the BN's raw input rows share dy's layout; its ReLU bits: one byte per 8 channels
+  const auto br = make_rsrc(DM == 2 ? reinterpret_cast<const unsigned char*>(p.bb_x) + client * p.dy_cs * 4
+                                    : reinterpret_cast<const unsigned char*>(p.dy),
+                            (uint32_t)(DM == 2 ? npix * p.ldy * 4 : 0));
+  const uint8_t* const bmk = DM == 2 && p.bb_mask ? p.bb_mask + client * npix * (p.N >> 3) + (n0 >> 3) : nullptr;
+  const int brows = DM == 2 ? (p.bb_valid ? p.bb_valid[client] : (int)npix) : 0;
+  bf16_t* const bdx = DM == 2 && p.bb_dxp && cb == 0 ? p.bb_dxp + client * 2 * npix * p.N + n0 : nullptr;
   const uint32_t x_lo = (uint32_t)(p.x_lo * 2), d_lo = (uint32_t)(p.dy_lo * 2);
   const int xrows = XM == 2 ? (p.x_valid ? p.x_valid[client] : (int)npix) : 0;
   if constexpr (XM == 2) {
     if (tid < 128) coef_s[tid] = p.coef[((long)client * p.C + c0) * 2 + tid];
-    __syncthreads();
   }
+  if constexpr (DM == 2) {
+    if (tid < 192) dcoef_s[tid] = p.bb_coef[((long)client * p.N + n0) * 3 + tid];
+  }
+  if constexpr (XM == 2 || DM == 2) __syncthreads();
 
   // ---- global → registers (one tile), registers → the LDS planes of a buffer
   u32x4_t xa[XT], xb[XT], da[DT], db[DT];
   uint32_t xok = 0;  // (XM 2) staged halo row inside the image and a valid sample
+  // (DM 2) the BN's raw input, the task's ReLU byte (bit 8: a valid row) and pixel
+  u32x4_t ba[DM == 2 ? DT : 1], bb[DM == 2 ? DT : 1];
+  uint32_t bm[DM == 2 ? DT : 1];
+  int bpix[DM == 2 ? DT : 1];
   auto load_tile = [&](int t) {
     const int b = t / tpi, r = t - b * tpi;
     const int h0 = (r / tcols) * TH, w0 = (r - (r / tcols) * tcols) * TW;
@@ -125,9 +143,17 @@ __global__ void __launch_bounds__(768, 1) halo_wgrad_kernel(HaloWgradParams p) {
         da[i] = __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? off : OOB_OFF, 0, 0);
         db[i] = __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? off + d_lo : OOB_OFF, 0, 0);
       } else {
+        // (DM 2: rows past the BN's valid ones are zero whatever dy and x hold — not loaded)
+        const bool okv = ok && (DM != 2 || pix < brows);
         const uint32_t off = (uint32_t)(pix * p.ldy + n0 + slot * 8) * 4u;
-        da[i] = __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? off : OOB_OFF, 0, 0);
-        db[i] = __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? off + 16 : OOB_OFF, 0, 0);
+        da[i] = __builtin_amdgcn_raw_buffer_load_b128(dr, okv ? off : OOB_OFF, 0, 0);
+        db[i] = __builtin_amdgcn_raw_buffer_load_b128(dr, okv ? off + 16 : OOB_OFF, 0, 0);
+        if constexpr (DM == 2) {
+          ba[i] = __builtin_amdgcn_raw_buffer_load_b128(br, okv ? off : OOB_OFF, 0, 0);
+          bb[i] = __builtin_amdgcn_raw_buffer_load_b128(br, okv ? off + 16 : OOB_OFF, 0, 0);
+          bm[i] = okv ? (bmk ? (uint32_t)bmk[(long)pix * (p.N >> 3) + slot] : 0xffu) | 0x100u : 0u;
+          bpix[i] = pix;
+        }
       }
     }
   };
@@ -189,10 +215,29 @@ __global__ void __launch_bounds__(768, 1) halo_wgrad_kernel(HaloWgradParams p) {
           hi = make_uint4(da[i].x, da[i].y, da[i].z, da[i].w);
           lo = make_uint4(db[i].x, db[i].y, db[i].z, db[i].w);
         } else {
-          const float v[8] = {__uint_as_float(da[i].x), __uint_as_float(da[i].y), __uint_as_float(da[i].z),
-                              __uint_as_float(da[i].w), __uint_as_float(db[i].x), __uint_as_float(db[i].y),
-                              __uint_as_float(db[i].z), __uint_as_float(db[i].w)};
+          float v[8] = {__uint_as_float(da[i].x), __uint_as_float(da[i].y), __uint_as_float(da[i].z),
+                        __uint_as_float(da[i].w), __uint_as_float(db[i].x), __uint_as_float(db[i].y),
+                        __uint_as_float(db[i].z), __uint_as_float(db[i].w)};
+          if constexpr (DM == 2) {
+            const float xv[8] = {__uint_as_float(ba[i].x), __uint_as_float(ba[i].y), __uint_as_float(ba[i].z),
+                                 __uint_as_float(ba[i].w), __uint_as_float(bb[i].x), __uint_as_float(bb[i].y),
+                                 __uint_as_float(bb[i].z), __uint_as_float(bb[i].w)};
+            const float* cf = dcoef_s + slot * 24;  // (a, d, e) of the slot's 8 channels
+            const uint32_t m = bm[i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float gd = ((m >> j) & 1u) ? v[j] : 0.f;
+              v[j] = (m & 0x100u) ? fmaf(cf[3 * j], gd, fmaf(cf[3 * j + 2], xv[j], cf[3 * j + 1])) : 0.f;
+            }
+          }
           split8(v, hi, lo);
+          if constexpr (DM == 2) {
+            if (bdx) {  // (dY's planes for the dgrad: the hi / lo slots bn_bwd_apply would have stored)
+              bf16_t* const hp = bdx + (long)bpix[i] * p.N + slot * 8;
+              *reinterpret_cast<uint4*>(hp) = hi;
+              *reinterpret_cast<uint4*>(hp + npix * p.N) = lo;
+            }
+          }
         }
         const uint32_t o = wh_off(pt, slot);
         *reinterpret_cast<uint4*>(Ds + o) = hi;
@@ -260,6 +305,25 @@ __global__ void __launch_bounds__(768, 1) halo_wgrad_kernel(HaloWgradParams p) {
     for (int ks = KS / 2; ks < KS; ++ks) kstep(cur, ks);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS stores landed
     __syncthreads();
+  }
+
+  if constexpr (DM == 2) {
+    // (the images past the valid samples were skipped: their dY planes are zeros, as the BN
+    // backward writes there; the pixel groups split those tiles like the valid ones)
+    const int all = p.B * tpi;
+    if (bdx && tiles < all) {
+      const int z_beg = tiles + (int)((long)(all - tiles) * g / p.G), z_end = tiles + (int)((long)(all - tiles) * (g + 1) / p.G);
+      for (int task = tid; task < (z_end - z_beg) * TP * 8; task += NT) {
+        const int t = z_beg + task / (TP * 8), r = task - (task / (TP * 8)) * (TP * 8);
+        const int b = t / tpi, rt = t - b * tpi;
+        const int h0 = (rt / tcols) * TH, w0 = (rt - (rt / tcols) * tcols) * TW;
+        const int pt = r >> 3, slot = r & 7;
+        const int th = pt / TW, tw = pt - th * TW;
+        bf16_t* const hp = bdx + (long)((b * p.H + h0 + th) * p.W + w0 + tw) * p.N + slot * 8;
+        *reinterpret_cast<uint4*>(hp) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(hp + npix * p.N) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
   }
 
   // ---- this wave's three 32 x 32 blocks: lane holds rows n = (e & 3) + 8(e >> 2) + 4·hf, column
@@ -357,8 +421,9 @@ long halo_wgrad_part_floats(int K, int B, int H, int W, int C, int N) {
 
 bool halo_wgrad(HaloWgradParams p, int xm, int dm, hipStream_t s) {
   const int cfg = halo_wgrad_cfg(p.B, p.H, p.W, p.C, p.N);
-  if (cfg < 0 || xm < 0 || xm > 2 || dm < 0 || dm > 1) return false;
+  if (cfg < 0 || xm < 0 || xm > 2 || dm < 0 || dm > 2) return false;
   if (p.ldx % 8 || p.ldy % 8 || (xm == 2 && p.coef == nullptr)) return false;
+  if (dm == 2 && (p.bb_x == nullptr || p.bb_coef == nullptr || p.ldy != p.N)) return false;
   if (((uintptr_t)p.dw & 15) || p.dw_cs % 4) return false;  // (the fold's 16-B stores)
   if (p.sgd.theta && (((uintptr_t)p.sgd.theta & 15) || ((uintptr_t)p.sgd.split & 7) || p.sgd.th_cs % 4 ||
                       p.sgd.sp_cs % 4 || p.sgd.sp_lo % 4 || (p.sgd.momentum != 0.f && ((uintptr_t)p.sgd.mom & 15))))
@@ -366,20 +431,26 @@ bool halo_wgrad(HaloWgradParams p, int xm, int dm, hipStream_t s) {
   const long npix = (long)p.B * p.H * p.W;
   const long xb = xm == 0 ? (p.x_lo + npix * p.ldx) * 2 : npix * p.ldx * 4;
   const long db = dm == 0 ? (p.dy_lo + npix * p.ldy) * 2 : npix * p.ldy * 4;
+  if (dm == 2 && npix * p.N * 2 * 2 >= (1L << 31)) return false;  // (bb_dxp: 32-bit element offsets)
   if (xb >= (long)OOB_OFF || db >= (long)OOB_OFF) return false;
   p.nblk = p.N / 64;
   p.cblk = p.C / 64;
   p.G = halo_wgrad_G(cfg, p.B, p.H, p.W, p.C, p.N);
   if (p.G > 1 && p.part == nullptr) return false;
   const int grid = p.K * p.G * p.nblk * p.cblk;
-#define DLS_HW_LAUNCH1(TH, TW, U)                                                                             \
-  switch (xm * 2 + dm) {                                                                                      \
-    case 0: hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, 0, 0, U>), dim3(grid), dim3(768), 0, s, p); break; \
-    case 1: hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, 0, 1, U>), dim3(grid), dim3(768), 0, s, p); break; \
-    case 2: hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, 1, 0, U>), dim3(grid), dim3(768), 0, s, p); break; \
-    case 3: hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, 1, 1, U>), dim3(grid), dim3(768), 0, s, p); break; \
-    case 4: hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, 2, 0, U>), dim3(grid), dim3(768), 0, s, p); break; \
-    default: hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, 2, 1, U>), dim3(grid), dim3(768), 0, s, p); break; \
+#define DLS_HW_LAUNCH_XD(TH, TW, U, XM, DM) \
+  hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, XM, DM, U>), dim3(grid), dim3(768), 0, s, p)
+#define DLS_HW_LAUNCH1(TH, TW, U)                               \
+  switch (xm * 3 + dm) {                                        \
+    case 0: DLS_HW_LAUNCH_XD(TH, TW, U, 0, 0); break;          \
+    case 1: DLS_HW_LAUNCH_XD(TH, TW, U, 0, 1); break;          \
+    case 2: DLS_HW_LAUNCH_XD(TH, TW, U, 0, 2); break;          \
+    case 3: DLS_HW_LAUNCH_XD(TH, TW, U, 1, 0); break;          \
+    case 4: DLS_HW_LAUNCH_XD(TH, TW, U, 1, 1); break;          \
+    case 5: DLS_HW_LAUNCH_XD(TH, TW, U, 1, 2); break;          \
+    case 6: DLS_HW_LAUNCH_XD(TH, TW, U, 2, 0); break;          \
+    case 7: DLS_HW_LAUNCH_XD(TH, TW, U, 2, 1); break;          \
+    default: DLS_HW_LAUNCH_XD(TH, TW, U, 2, 2); break;         \
   }
 #define DLS_HW_LAUNCH(TH, TW) \
   if (unroll == 2) {          \
@@ -396,6 +467,7 @@ bool halo_wgrad(HaloWgradParams p, int xm, int dm, hipStream_t s) {
   }
 #undef DLS_HW_LAUNCH
 #undef DLS_HW_LAUNCH1
+#undef DLS_HW_LAUNCH_XD
   if (p.G > 1) {
     const long total4 = (long)p.K * p.N * 9 * p.C / 4;
     hipLaunchKernelGGL(halo_wgrad_fold_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, p);

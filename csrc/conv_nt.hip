@@ -442,10 +442,15 @@ void conv_nt(ConvNTParams p, int K, int variant, hipStream_t s) {
   if (!launch_variant(variant, p, K, va, vb, bkm, s)) fprintf(stderr, "conv_nt: bad variant %d\n", variant);
 }
 
+void wt_planes(const bf16_t* wsplit, long ws_cs, long ws_plane, bf16_t* wt, int Kw, int Co, int Ci, hipStream_t s) {
+  hipLaunchKernelGGL(wt_planes_kernel, dim3(Kw * 2 * 9, Co / 32, Ci / 32), dim3(256), 0, s, wsplit, ws_cs, ws_plane, wt,
+                     Co, Ci);
+}
+
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc, long w_cs, int K, int rep, int B, int OH, int OW,
                 int Co, int H, int W, int Ci, int KH, int KW, int stride, int pad, int variant, int f32, hipStream_t s,
                 int ld_dy, long dy_cs, const bf16_t* wsplit, long ws_cs, long ws_plane, long x_lo, int acc_compact,
-                const BNBwdPartials* bnb, bf16_t* wt_buf, const uint8_t* acc_mask) {
+                const BNBwdPartials* bnb, bf16_t* wt_buf, const uint8_t* acc_mask, int wt_ready) {
   ConvNTParams p{};
   p.acc_mask = acc_mask;
   if (bnb) {  // (the epilogue's partial rows are the dX rows of a single stride-1 launch)
@@ -515,9 +520,11 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
     if (variant < 0 && !f32 && Ci <= 64 && vec_width(Ci) == 8 && vec_width(Co) == 8) variant = 14;
     if (wt_buf && f32 && x_lo != 0 && wsplit && KH == 3 && KW == 3 && pad == 1 && Co % 32 == 0 && Ci % 32 == 0) {
       // transposed flipped weight planes → the forward (row-major B) tiles
+      // (wt_ready: built earlier by wt_planes — before a fused SGD step rewrote the weight planes)
       const int Kw = K / rep;
-      hipLaunchKernelGGL(wt_planes_kernel, dim3(Kw * 2 * 9, Co / 32, Ci / 32), dim3(256), 0, s, wsplit, ws_cs, ws_plane,
-                         wt_buf, Co, Ci);
+      if (!wt_ready)
+        hipLaunchKernelGGL(wt_planes_kernel, dim3(Kw * 2 * 9, Co / 32, Ci / 32), dim3(256), 0, s, wsplit, ws_cs,
+                           ws_plane, wt_buf, Co, Ci);
       p.b_kmajor = 0;
       p.wsplit = wt_buf;
       p.ws_cs = 2L * 9 * Ci * Co;

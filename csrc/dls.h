@@ -230,9 +230,7 @@ struct SgdEpi {
   float wd, momentum, dampening;
   int nesterov;
 };
-// the epilogue the next conv_tn / halo_wgrad binding call takes (set_sgd_epilogue; consumed once)
-SgdEpi take_sgd_epi();
-void set_sgd_epi(const SgdEpi& e);
+// (passed with each conv_tn / halo_wgrad launch: bindings.cpp sgd_arg)
 
 struct HaloWgradParams {
   const void* dy;
@@ -249,6 +247,16 @@ struct HaloWgradParams {
   // optional [K] valid samples: tiles of later images (zero dY and X: the BN passes wrote zeros
   // there) are skipped — the pixel groups split the valid images' tiles only
   const int* valid_img;
+  // (dy mode 2) dY is the input gradient of a BatchNorm(+ReLU) whose OUTPUT gradient dy holds
+  // (fp32): dY = r < bb_valid[k] ? fmaf(a, relu' ? dy : 0, fmaf(e, bb_x, d)) : 0 — bn_bwd_apply's
+  // arithmetic — with bb_coef [K][N][3] = (a, d, e), relu' from the bits bb_mask [K][rows][N / 8]
+  // (nullptr: no gate) and bb_x the BN's raw input (rows at stride ldy). The c-block-0 workgroups
+  // also store dY's split planes at bb_dxp ([K][2][rows][N]) for the dgrad — zeros for skipped images
+  const float* bb_x;
+  const uint8_t* bb_mask;
+  const float* bb_coef;
+  const int* bb_valid;
+  bf16_t* bb_dxp;
   float* dw;
   long dw_cs;
   float* part;
@@ -258,7 +266,8 @@ struct HaloWgradParams {
 };
 bool halo_wgrad_supported(int B, int H, int W, int C, int N);
 long halo_wgrad_part_floats(int K, int B, int H, int W, int C, int N);
-// xm: 0 x planes, 1 x fp32, 2 x fp32 + BN(+ReLU); dm: 0 dy planes, 1 dy fp32. false: not served
+// xm: 0 x planes, 1 x fp32, 2 x fp32 + BN(+ReLU); dm: 0 dy planes, 1 dy fp32, 2 BN backward of an
+// fp32 dy (bb_*). false: not served
 bool halo_wgrad(HaloWgradParams p, int xm, int dm, hipStream_t s);
 
 struct ConvTNParams {
@@ -332,7 +341,10 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* acc
                 bf16_t* wt_buf = nullptr,
                 // acc_mask: bits [K][rows][Ci / 8] gating acc (acc · bit): the identity shortcut's
                 // gradient dy·relu' from the block output's gradient and ReLU mask, never stored
-                const uint8_t* acc_mask = nullptr);
+                const uint8_t* acc_mask = nullptr,
+                int wt_ready = 0);  // wt_buf already holds the transposed planes (wt_planes)
+// the transposed flipped weight planes of a 3x3 dgrad (conv_dgrad wt_buf), built ahead of the dgrad
+void wt_planes(const bf16_t* wsplit, long ws_cs, long ws_plane, bf16_t* wt, int Kw, int Co, int Ci, hipStream_t s);
 void conv_tn(ConvTNParams p, int K, int variant, hipStream_t s);
 int conv_tn_num_variants();
 // split-K factor the launch will use (callers zero the gradient rows first when > 1)
@@ -435,7 +447,9 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
             int dx_f32 = 1,  // dxp / dx_f32: split planes of dX (fp32, contiguous) with or without dX; relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
                              // stride ldx, acc_dx: dx += (DenseNet block-buffer gradient)
             const float* pre_part = nullptr,  // [K][pre_nparts][2C] Σĝ / Σĝx̂ partials from the dgrad
-            int pre_nparts = 0);              // epilogue that produced dy (ConvNTParams::bnb): no reduction pass
+            int pre_nparts = 0,               // epilogue that produced dy (ConvNTParams::bnb): no reduction pass
+            float* coef_ext = nullptr,        // [K][C][3] (a, d, e) kept for a later stage instead of ws
+            int stage = 0);                   // 0 coefficients + apply, 1 coefficients only, 2 apply only
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
             long rows_per_client, int C, float eps, int rep, int f32, hipStream_t s,
             bf16_t* yp = nullptr);  // yp (fp32): y's split planes [K][2][rows][C] as well

@@ -975,14 +975,6 @@ void sgd_step_seg(float* theta, const float* grad, float* mom, bf16_t* split, co
                      active, first, 0L, ld, wd, momentum, dampening, nesterov, seg);
 }
 
-static SgdEpi g_sgd_epi{};
-SgdEpi take_sgd_epi() {
-  const SgdEpi e = g_sgd_epi;
-  g_sgd_epi = SgdEpi{};
-  return e;
-}
-void set_sgd_epi(const SgdEpi& e) { g_sgd_epi = e; }
-
 void split_rows_padded(const float* w, long w_cs, int K, int rows, int C, int C32, bf16_t* out, hipStream_t s) {
   const long n = (long)rows * C32;
   if (K == 0 || n == 0) return;

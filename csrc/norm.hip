@@ -869,13 +869,16 @@ void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
             float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s,
-            int ldx, int acc_dx, bf16_t* dxp, int dx_f32, const float* pre_part, int pre_nparts) {
+            int ldx, int acc_dx, bf16_t* dxp, int dx_f32, const float* pre_part, int pre_nparts, float* coef_ext,
+            int stage) {
+  // stage 0: coefficients + apply; 1: coefficients (and dγ, dβ) only, into coef_ext — a consumer
+  // applies them in its loader (conv_halo_wgrad.hip dy mode 2); 2: the apply alone from coef_ext
   if (!f32 || acc_dx || (ldx != 0 && ldx != C)) {  // planes: fp32, contiguous dX only
     dxp = nullptr;
     dx_f32 = 1;
   }
   if (ldx == 0) ldx = C;
-  float* coef = ws;
+  float* coef = coef_ext ? coef_ext : ws;
   float* part = ws + (long)3 * C * K;
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
@@ -883,7 +886,8 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   if (V != 8) rmask = nullptr;
   BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1, counters};
   DISPATCH_T(f32, {
-    if (pre_part) {  // Σĝ / Σĝx̂ from the dgrad epilogue that produced dy: coefficients only
+    if (stage == 2) {
+    } else if (pre_part) {  // Σĝ / Σĝx̂ from the dgrad epilogue that produced dy: coefficients only
       if (pre_nparts > FOLD && pre_nparts <= cdiv(R, 32)) {
         const int nfold = cdiv(pre_nparts, FOLD);
         double* folds = reinterpret_cast<double*>(ws + bn_fold_offset(K, R, C));
@@ -901,13 +905,14 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
       DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                        mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
     }
-    if (!counters && !pre_part)
+    if (!counters && !pre_part && stage != 2)
       launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, (const float*)part, (int)grid.x, CP(gamma), (const TT*)nullptr,
                              valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K,
                              R, C, 0.f, 1, 1, 0, 0L);
-    DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
-                                     valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx, dxp,
-                                     dx_f32));
+    if (stage != 1)
+      DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
+                                       valid_rows, coef, R, C, relu, MP(dx), MP(dpre), rpb, rmask, ldx, acc_dx, dxp,
+                                       dx_f32));
   });
 }
 

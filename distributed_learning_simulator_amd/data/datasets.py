@@ -286,6 +286,34 @@ class DatasetCollection:
     def validation_labels(self) -> torch.Tensor:
         return self.test.labels[self.validation_indices]
 
+    def merge_validation_into_train(self, seed: int) -> None:
+        """`merge_validation_to_training_set` (reference config.py:27, consumed by its external
+        toolbox): the Validation phase (a seeded half of the test split, `split_validation`) is
+        appended to the training split — its samples become training indices n_train.. — and the
+        collection keeps no Validation phase (so no keep-best-model selection); the server tests
+        on the other half. Device-resident splits only (materialised images, token sets)."""
+        if self.graph is not None:
+            raise ValueError("merge_validation_to_training_set: graph datasets have no separate validation split")
+        self.split_validation(seed)
+        tr, te, vi = self.train, self.test, self.validation_indices
+        if isinstance(tr, ImageDataset):
+            if tr.data is None or te.data is None:
+                raise ValueError("merge_validation_to_training_set: needs materialised image splits "
+                                 "(this dataset is generated on the fly; lower dataset_kwargs.scale)")
+            tr.data = torch.cat([tr.data, te.data.index_select(0, vi.to(te.data.device))])
+            tr.source = torch.cat([tr.source, te.source[vi]])
+            tr.source_dev = tr.source.to(tr.device)
+            tr._proto32 = None
+        elif isinstance(tr, TextDataset):
+            tr.tokens = torch.cat([tr.tokens, te.tokens.index_select(0, vi.to(te.tokens.device))])
+            tr.lengths = torch.cat([tr.lengths, te.lengths.index_select(0, vi.to(te.lengths.device))])
+        else:
+            raise ValueError(f"merge_validation_to_training_set: unsupported split type {type(tr).__name__}")
+        tr.labels = torch.cat([tr.labels, te.labels[vi]])
+        tr.labels_dev = tr.labels.to(tr.labels_dev.device)
+        tr.n = int(tr.labels.shape[0])
+        self.validation_indices = None  # (merged: no Validation phase left)
+
 
 def create_dataset_collection(name: str, dataset_kwargs: dict | None, seed: int, device,
                               dtype=torch.float32, image_channels: int | None = None) -> DatasetCollection:

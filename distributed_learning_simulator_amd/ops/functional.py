@@ -156,6 +156,38 @@ class DeferredBN:
             self.pending = False
 
 
+# deferred BN backward applies (DeferredBNBwd) taken by a halo weight gradient's loader ("wgrad")
+# or run as their own pass ("materialized"): tests, reports
+bn_bwd_defer_count = {"wgrad": 0, "materialized": 0}
+
+
+class DeferredBNBwd:
+    """A training BatchNorm's input gradient dX whose apply pass is deferred to the conv that
+    produced the BN's input (OPTIONS.bn_bwd_in_wgrad): the BN backward computed only its
+    coefficients (a, d, e) and dγ / dβ, and hands autograd the planes-only alias of an unwritten
+    `dxp`. That conv's backward runs its halo weight gradient first, in dY mode 2
+    (csrc/conv_halo_wgrad.hip), which builds dX = a·(dy·relu') + e·x + d in its loader and stores
+    the planes for the dgrad on the way; any other consumer calls `materialize()` — the ordinary
+    apply pass into the same planes, with the same bits."""
+
+    __slots__ = ("dy", "x", "mask", "coef", "valid_rows", "dxp", "pending")
+
+    def __init__(self, dy, x, mask, coef, valid_rows, dxp):
+        self.dy, self.x, self.mask, self.coef, self.valid_rows, self.dxp = dy, x, mask, coef, valid_rows, dxp
+        self.pending = True
+
+    def materialize(self):
+        if self.pending:
+            from . import hip
+
+            hip.bn_bwd_apply_planes(self.dy, self.x, self.mask, self.coef, self.valid_rows, self.dxp)
+            self.pending = False
+            bn_bwd_defer_count["materialized"] += 1
+
+    def wgrad_args(self):
+        return (self.dy, self.x, self.mask, self.coef, self.valid_rows, self.dxp)
+
+
 class _Conv(torch.autograd.Function):
     """Conv2d over the client dim. If the input carries more channels than the weight (image
     data stored zero-padded to 8 channels), the weight is zero-padded to match and only the
@@ -255,6 +287,58 @@ class _Conv(torch.autograd.Function):
         return y
 
     @staticmethod
+    def _wgrad(ctx, dy, x, w, dyp, be, bbd=None, sgd_ok=True) -> bool:
+        """The weight gradient (or the SGD step fused into it). `bbd` (DeferredBNBwd): only the halo
+        kernel's BN-backward dY mode — returns False, launching nothing, when it cannot serve;
+        `sgd_ok` False: store dW (the flat step covers the weight)."""
+        if bbd is not None:
+            if not (ctx.stride == 1 and ctx.pad == 1 and w.shape[2] == 3 and w.shape[3] == 3):
+                return False
+            sgd = ctx.sgd if sgd_ok else None
+            if ctx.bn_src is not None:
+                xr, coef, relu, vrows = ctx.bn_src
+                ok = be.halo_wgrad(dy, xr, ctx.gw, bn=(coef, relu, vrows), valid=ctx.valid, sgd=sgd,
+                                   bn_bwd=bbd.wgrad_args())
+            else:
+                ok = be.halo_wgrad(dy, x, ctx.gw, x_planes=ctx.xp, valid=ctx.valid, sgd=sgd, bn_bwd=bbd.wgrad_args())
+            if ok and sgd is not None:
+                sgd[0].done.add(sgd[1])
+            return bool(ok)
+        padded = w.shape[-1] > ctx.ci
+        K = x.shape[0]
+        sgd = ctx.sgd if not padded else None
+        stepped = False
+        gw = torch.empty((K,) + tuple(w.shape[1:]), dtype=torch.float32, device=dy.device) if padded else ctx.gw
+        if be is ref:
+            gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (K,) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
+            if ctx.gb is not None:
+                ctx.gb.copy_(dy.float().sum(dim=(1, 2, 3)))
+        elif ctx.bn_src is not None:
+            # x's planes were never written: the halo wgrad applies the BN to the raw tensor
+            xr, coef, relu, vrows = ctx.bn_src
+            if not be.halo_wgrad(dy, xr, gw, dy_planes=dyp, bn=(coef, relu, vrows), valid=ctx.valid,
+                                 sgd=sgd):
+                raise RuntimeError("conv2d backward: the halo wgrad refused a shape its forward accepted")
+            stepped = sgd is not None
+        elif (ctx.halo_wgrad and ctx.stride == 1 and ctx.pad == 1 and w.shape[2] == 3 and w.shape[3] == 3
+              and not padded and be.halo_wgrad(dy, x, gw, dy_planes=dyp, x_planes=ctx.xp, valid=ctx.valid,
+                                               sgd=sgd)):
+            stepped = sgd is not None
+        elif dyp is not None:
+            stepped = be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad, dy_planes=dyp, x_planes=ctx.xp, sgd=sgd)
+        else:
+            if ctx.x_planes_only:
+                raise RuntimeError("conv2d backward: fp32 dY with a planes-only input")
+            be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad)
+            if ctx.gb is not None:
+                be.bias_grad(dy, ctx.gb)
+        if padded:
+            ctx.gw.copy_(gw[..., : ctx.ci])
+        if stepped:
+            sgd[0].done.add(sgd[1])  # (this weight's optimiser step ran in its wgrad)
+        return True
+
+    @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         be = _be(dy)
@@ -282,6 +366,27 @@ class _Conv(torch.autograd.Function):
             if acc is None:
                 link.receiver_done = True  # (a late donor hands its dX to autograd instead)
         dyp = _planes_of(dy)
+        wgrad_done = False
+        wt_pre = None
+        bbd = getattr(dy, "_dls_bnbwd", None)
+        if bbd is not None and bbd.pending:
+            # dY is a deferred BN input gradient (DeferredBNBwd): the halo weight gradient applies
+            # the BN backward in its loader and writes dY's planes, so it runs before the dgrad
+            if ctx.gw is not None and be is not ref and ctx.halo_wgrad and w.shape[-1] == ctx.ci:
+                sgd_ok = True
+                if ctx.sgd is not None and ctx.needs_input_grad[0]:
+                    # its SGD epilogue rewrites the weight planes the dgrad reads: the dgrad's
+                    # transposed copy is built first, or the flat step takes this weight
+                    wt_pre = (be.dgrad_wt_prebuild(dy.shape, w, ctx.w_split, x.shape[2:4], ctx.stride, ctx.pad)
+                              if ctx.dgrad_wt and ctx.w_split is not None and not acc_compact and ctx.donor is None
+                              else None)
+                    sgd_ok = wt_pre is not None
+                wgrad_done = _Conv._wgrad(ctx, dy, x, w, dyp, be, bbd, sgd_ok=sgd_ok)
+            if wgrad_done:
+                bbd.pending = False
+                bn_bwd_defer_count["wgrad"] += 1
+            else:
+                bbd.materialize()
         if dyp is not None and ctx.xp is None:
             raise RuntimeError("conv2d backward: dY planes without the input's planes")
         if dyp is None:
@@ -317,6 +422,8 @@ class _Conv(torch.autograd.Function):
                     kw["acc_mask"] = acc_mask
                 if ctx.dgrad_wt:
                     kw["wt"] = True
+                if wt_pre is not None:
+                    kw["wt_buf"] = wt_pre
                 dx = be.conv_dgrad(dy, w, x.shape[2:4], ctx.stride, ctx.pad, acc=acc, **kw)
                 if bnb is not None:
                     bnb.part, bnb.key = part, (dx.data_ptr(), dx._version)
@@ -324,39 +431,8 @@ class _Conv(torch.autograd.Function):
                 dx = dx[..., : ctx.ci]
         elif acc is not None:
             dx = acc if acc_mask is None else MaskedGrad(acc, acc_mask).dense()
-        if ctx.gw is not None:
-            padded = w.shape[-1] > ctx.ci
-            K = x.shape[0]
-            sgd = ctx.sgd if not padded else None
-            stepped = False
-            gw = torch.empty((K,) + tuple(w.shape[1:]), dtype=torch.float32, device=dy.device) if padded else ctx.gw
-            if be is ref:
-                gw.copy_(ref.conv_wgrad(dy.float(), x.float(), (K,) + tuple(w.shape[1:]), ctx.stride, ctx.pad))
-                if ctx.gb is not None:
-                    ctx.gb.copy_(dy.float().sum(dim=(1, 2, 3)))
-            elif ctx.bn_src is not None:
-                # x's planes were never written: the halo wgrad applies the BN to the raw tensor
-                xr, coef, relu, vrows = ctx.bn_src
-                if not be.halo_wgrad(dy, xr, gw, dy_planes=dyp, bn=(coef, relu, vrows), valid=ctx.valid,
-                                     sgd=sgd):
-                    raise RuntimeError("conv2d backward: the halo wgrad refused a shape its forward accepted")
-                stepped = sgd is not None
-            elif (ctx.halo_wgrad and ctx.stride == 1 and ctx.pad == 1 and w.shape[2] == 3 and w.shape[3] == 3
-                  and not padded and be.halo_wgrad(dy, x, gw, dy_planes=dyp, x_planes=ctx.xp, valid=ctx.valid,
-                                                   sgd=sgd)):
-                stepped = sgd is not None
-            elif dyp is not None:
-                stepped = be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad, dy_planes=dyp, x_planes=ctx.xp, sgd=sgd)
-            else:
-                if ctx.x_planes_only:
-                    raise RuntimeError("conv2d backward: fp32 dY with a planes-only input")
-                be.conv_wgrad(dy, x, gw, ctx.stride, ctx.pad)
-                if ctx.gb is not None:
-                    be.bias_grad(dy, ctx.gb)
-            if padded:
-                ctx.gw.copy_(gw[..., : ctx.ci])
-            if stepped:
-                sgd[0].done.add(sgd[1])  # (this weight's optimiser step ran in its wgrad)
+        if ctx.gw is not None and not wgrad_done:
+            _Conv._wgrad(ctx, dy, x, w, dyp, be)
         if donor is not None and dx is not None and not donor.receiver_done:
             donor.grad = dx  # added by the block's first conv in its dgrad epilogue
             donor.compact = ctx.stride if compact else 0
@@ -627,6 +703,7 @@ class _BN(torch.autograd.Function):
         ctx.ggamma, ctx.gbeta, ctx.shape = ggamma, gbeta, x.shape
         ctx.bnb = bnb
         ctx.planes_on = OPTIONS.planes  # (the backward's dX-planes decision follows the forward's)
+        ctx.bwd_in_wgrad = OPTIONS.bn_bwd_in_wgrad
         ctx.residual_mask = OPTIONS.residual_mask
         yo = y.reshape(x.shape)
         if yp is not None:
@@ -668,6 +745,21 @@ class _BN(torch.autograd.Function):
             # as factors (MaskedGrad) — the backward writes no dpre tensor
             masked = (ctx.has_res and ctx.link is not None and ctx.relu and ctx.relu_mask is not None
                       and ctx.residual_mask and C % 8 == 0)
+            if (dxm == 2 and ctx.bwd_in_wgrad and not (ctx.has_res and not masked) and C % 64 == 0
+                    and (ctx.relu_mask is not None or not ctx.relu) and x3.is_contiguous()):
+                # coefficients only: the producing conv's halo weight gradient applies them in its
+                # dY loader and writes dX's planes (DeferredBNBwd), or materialize() does
+                coef = torch.empty((K, C, 3), dtype=torch.float32, device=dy3.device)
+                be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu, ctx.ggamma, ctx.gbeta, False,
+                          relu_mask=ctx.relu_mask, pre_part=pre, coef_out=coef)
+                dx, dxp = be.planes_buffer((K, R, C), dy3.device)
+                if masked:
+                    ctx.link.grad = MaskedGrad(dy3.view(ctx.shape), ctx.relu_mask)
+                dxo = dx.reshape(ctx.shape)
+                _tag_planes(dxo, dxp.view((K, 2) + tuple(ctx.shape[1:])), True)
+                dxo._dls_bnbwd = DeferredBNBwd(dy3, x3, ctx.relu_mask if ctx.relu else None, coef, ctx.valid_rows,
+                                               dxp)
+                return dxo, None, None, None, None, None, None, None, None, None, None, None
             out = be.bn_bwd(dy3, x3, y, mean, rstd, gamma, ctx.valid_rows, ctx.relu,
                             ctx.ggamma, ctx.gbeta, ctx.has_res and not masked, relu_mask=ctx.relu_mask,
                             dx_planes=dxm, pre_part=pre)

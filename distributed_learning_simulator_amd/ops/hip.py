@@ -293,8 +293,30 @@ def bn_bwd_parts_ok(dx_shape, stride: int, dtype) -> bool:
     return dtype == F32 and stride == 1 and Ci % 4 == 0 and B * H * W * Ci * 4 < WINDOW
 
 
+def _wt_dgrad_ok(Co, Ci, KH, KW, H, W, stride, pad, planes: bool, ws_p) -> bool:
+    # (halo shapes only — H, W >= 8: at 4 x 4 the implicit-GEMM k-major tiles win, and the
+    # transposition of 512 x 512 weight rows costs more than it saves: bench/epilogue_bench.py l4)
+    return bool(planes and ws_p and stride == 1 and pad == 1 and KH == 3 and KW == 3 and Co % 32 == 0
+                and Ci % 32 == 0 and nt_f32_variant < 0 and min(H, W) >= 8)
+
+
+def dgrad_wt_prebuild(dy_shape, w, w_split, in_hw, stride: int, pad: int):
+    """The transposed, flipped weight planes a planes dgrad of this shape would build
+    (conv_dgrad(wt=True)), built NOW — before a weight-gradient launch with the SGD epilogue
+    rewrites the weight planes — for conv_dgrad(wt_buf=). None: that dgrad would not use them."""
+    K, B, OH, OW, Co = dy_shape
+    Kw, Co2, KH, KW, Ci = w.shape
+    ws_p, ws_cs, ws_plane = _wsplit_args(w_split, w)
+    if not (w.dtype == F32 and planes_ok(Co, Ci, Co)
+            and _wt_dgrad_ok(Co, Ci, KH, KW, int(in_hw[0]), int(in_hw[1]), stride, pad, True, ws_p)):
+        return None
+    wt_buf = torch.empty(Kw * 2 * 9 * Ci * Co, dtype=BF16, device=w.device)
+    _C.wt_planes(ws_p, ws_cs, ws_plane, _p(wt_buf), Kw, Co, Ci, _s())
+    return wt_buf
+
+
 def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_planes=None, acc_compact=False,
-               bnb=None, acc_mask=None, wt: bool = False):
+               bnb=None, acc_mask=None, wt: bool = False, wt_buf=None):
     """dX (+ `acc`, a second gradient of the same input added in the epilogue: the identity
     residual branch of a ResNet block, so autograd never materialises the sum separately).
     `dy` may be a channel slice of a wider buffer (DenseNet block-buffer gradient).
@@ -309,7 +331,8 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
     `acc_mask` (fp32, with `acc`, not compact): ReLU bits [K, B·H·W, Ci / 8] gating `acc` — the
     identity shortcut's gradient dy·relu' read from the block output's gradient, never stored.
     `wt` (fp32 planes, 3x3 stride-1 pad-1): run the dgrad on the forward tiles with transposed,
-    flipped weight planes (built into a scratch buffer right before the launch)."""
+    flipped weight planes (built into a scratch buffer right before the launch, or `wt_buf` from
+    dgrad_wt_prebuild)."""
     K, B, OH, OW, Co = dy.shape
     Kw, Co2, KH, KW, Ci = w.shape
     H, W = int(in_hw[0]), int(in_hw[1])
@@ -378,16 +401,17 @@ def conv_dgrad(dy, w, in_hw, stride: int, pad: int, acc=None, w_split=None, dy_p
     if dy_planes is not None and ws_p and planes_ok(Co, Ci, ld_dy):
         dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
         planes_launches["dgrad"] += 1
-    wt_buf = None
-    # (halo shapes only — H, W >= 8: at 4 x 4 the implicit-GEMM k-major tiles win, and the
-    # transposition of 512 x 512 weight rows costs more than it saves: bench/epilogue_bench.py l4)
-    if (wt and dy_lo and ws_p and stride == 1 and pad == 1 and KH == 3 and KW == 3 and Co % 32 == 0
-            and Ci % 32 == 0 and nt_f32_variant < 0 and min(H, W) >= 8):
-        wt_buf = torch.empty(Kw * 2 * 9 * Ci * Co, dtype=BF16, device=dy.device)
+    wt_ready = wt_buf is not None
+    if (wt or wt_ready) and _wt_dgrad_ok(Co, Ci, KH, KW, H, W, stride, pad, bool(dy_lo), ws_p):
+        if wt_buf is None:
+            wt_buf = torch.empty(Kw * 2 * 9 * Ci * Co, dtype=BF16, device=dy.device)
         planes_launches["dgrad_wt"] += 1
+    else:
+        assert not wt_ready, "conv_dgrad: a prebuilt wt_buf for a dgrad that does not take it"
+        wt_buf = None
     _C.conv_dgrad(dyp, _p(w), _p(dx), _p(acc), w_cs, K, rep, B, OH, OW, Co, H, W, Ci, KH, KW, stride, pad,
                   nt_f32_variant if f32 else nt_variant, f32, _s(), ld_dy, dy_cs, ws_p, ws_cs, ws_plane, dy_lo,
-                  int(bool(acc_compact)), *bnb_args, _p(wt_buf), _p(acc_mask))
+                  int(bool(acc_compact)), *bnb_args, _p(wt_buf), _p(acc_mask), int(wt_ready))
     return dx
 
 
@@ -402,14 +426,17 @@ def _tn_part(numel: int, device) -> torch.Tensor:
     return _grown(_part_cache, (device, torch.cuda.current_stream().cuda_stream), numel, device)
 
 
-def _arm_sgd(sgd) -> None:
-    """Hand the next conv_tn / halo_wgrad launch its SGD epilogue (engine.params.FusedSGD ref:
-    (handle, name, element offset)): it steps the weight rows instead of storing dW."""
+def _sgd_arg(sgd):
+    """The SGD epilogue of one conv_tn / halo_wgrad launch (engine.params.FusedSGD ref: (handle,
+    name, element offset)), passed with that launch: it steps the weight rows instead of storing
+    dW. None: dW is stored."""
+    if sgd is None:
+        return None
     f, _, off = sgd
     wd, mom, damp, nest = f.hyper
     assert f.theta.stride(1) == 1 and f.mom.stride(0) == f.theta.stride(0) and f.split.is_contiguous()
-    _C.set_sgd_epilogue(_p(f.theta) + off * 4, _p(f.mom) + off * 4, _p(f.split) + off * 2, f.theta.stride(0),
-                        f.split.stride(0), f.split.stride(1), _p(f.lr), _p(f.active), _p(f.first), wd, mom, damp, nest)
+    return (_p(f.theta) + off * 4, _p(f.mom) + off * 4, _p(f.split) + off * 2, f.theta.stride(0), f.split.stride(0),
+            f.split.stride(1), _p(f.lr), _p(f.active), _p(f.first), float(wd), float(mom), float(damp), int(nest))
 
 
 def _tn_launch(dy, x, gw, dy_cs, x_cs, B, H, W, C, OH, OW, KH, KW, stride, pad, M, Co, R, K, f32, ldy, ldx,
@@ -431,9 +458,8 @@ def _tn_launch(dy, x, gw, dy_cs, x_cs, B, H, W, C, OH, OW, KH, KW, stride, pad, 
             gw.zero_()
     if sgd is not None:
         assert planes, "the SGD epilogue needs the plane TN kernels"
-        _arm_sgd(sgd)
     _C.conv_tn(dyp, xp, _p(gw), dy_cs, x_cs, gw.stride(0), B, H, W, C, OH, OW, KH, KW, stride, pad, M, Co, R, K, tv,
-               f32, _s(), ldy, ldx, part, dy_lo, x_lo)
+               f32, _s(), ldy, ldx, part, dy_lo, x_lo, _sgd_arg(sgd))
 
 
 def conv_wgrad(dy, x, gw, stride: int, pad: int, dy_planes=None, x_planes=None, sgd=None) -> bool:
@@ -477,14 +503,19 @@ def halo_wgrad_ok(x_shape, Co: int) -> bool:
     return bool(_C.halo_wgrad_supported(B, H, W, C, Co))
 
 
-def halo_wgrad(dy, x, gw, dy_planes=None, x_planes=None, bn=None, valid=None, sgd=None) -> bool:
+def halo_wgrad(dy, x, gw, dy_planes=None, x_planes=None, bn=None, valid=None, sgd=None, bn_bwd=None) -> bool:
     """3x3 / stride-1 / pad-1 weight gradient on the LDS-halo kernel (csrc/conv_halo_wgrad.hip)
     into the gradient rows gw [K, N, 3, 3, C]. dy [K, B, H, W, N] fp32 (contiguous) or its split
     planes `dy_planes` [K, 2, ...]; x [K, B, H, W, C]: its planes `x_planes`, or — `bn` = (coef
     [K, C, 2], relu, valid_rows) — the RAW input of a BatchNorm(+ReLU) that the loader applies
     (the operand bits of bn_apply's planes), or plain fp32. `valid` [K] (samples): the images past
     it carry zero dY and X (BatchNorm outputs) and are skipped. False: shape not served. `sgd` (a
-    FusedSGD ref): the kernel (or its fold) steps the weights instead of storing dW."""
+    FusedSGD ref): the kernel (or its fold) steps the weights instead of storing dW.
+    `bn_bwd` = (dy_out, x_bn, mask, coef [K, N, 3], valid_rows, dxp [K, 2, R, N]): dY is the input
+    gradient of a BatchNorm(+ReLU) — `dy_out` its output gradient (fp32, dy's shape), `x_bn` its
+    raw input, `mask` the ReLU bits (or None), `coef` bn_bwd(stage=1)'s coefficients — applied in the
+    loader (bn_bwd_apply's bits), and the kernel also writes dY's split planes into `dxp` for the
+    dgrad (`dy` / `dy_planes` are then the planes-only alias and ignored)."""
     K, B, H, W, N = dy.shape
     C = x.shape[-1]
     if x.shape != (K, B, H, W, C) or dy.dtype != F32 or x.dtype != F32 or not halo_wgrad_ok(x.shape, N):
@@ -492,7 +523,23 @@ def halo_wgrad(dy, x, gw, dy_planes=None, x_planes=None, bn=None, valid=None, sg
     assert gw.shape == (K, N, 3, 3, C) and gw.dtype == F32 and gw[0].is_contiguous(), gw.shape
     if gw.data_ptr() % 16 or gw.stride(0) % 4:
         return False
-    if dy_planes is not None:
+    bnb = None
+    if bn_bwd is not None:
+        dyo, xb, mk, cf, vr, dxp = bn_bwd
+        R = B * H * W
+        if not (dyo.is_contiguous() and xb.is_contiguous() and dyo.numel() == K * R * N and xb.numel() == K * R * N
+                and dyo.dtype == F32 and xb.dtype == F32):
+            return False
+        assert cf.shape == (K, N, 3) and cf.dtype == F32 and cf.is_contiguous(), cf.shape
+        assert dxp.shape == (K, 2, R, N) and dxp.dtype == BF16 and dxp.is_contiguous(), dxp.shape
+        if mk is not None:
+            assert mk.dtype == torch.uint8 and mk.is_contiguous() and mk.numel() == K * R * N // 8
+        if vr is not None:
+            vr = vr.to(torch.int32).contiguous()
+            assert vr.shape == (K,)
+        bnb = (_p(xb), _p(mk), _p(cf), _p(vr), _p(dxp))
+        dyp, dy_cs, dy_lo, dm = _p(dyo), R * N, 0, 2
+    elif dy_planes is not None:
         dyp, dy_cs, dy_lo = _planes_args(dy_planes, dy)
         dm = 0
     else:
@@ -522,10 +569,8 @@ def halo_wgrad(dy, x, gw, dy_planes=None, x_planes=None, bn=None, valid=None, sg
         valid = valid.to(torch.int32).contiguous()
         assert valid.shape == (K,)
         vimg = _p(valid)
-    if sgd is not None:
-        _arm_sgd(sgd)
     ok = _C.halo_wgrad(dyp, dy_cs, dy_lo, N, xp, x_cs, x_lo, C, coef, relu, valid_rows_p, _p(gw), gw.stride(0), part,
-                       K, B, H, W, C, N, xm, dm, _s(), vimg)
+                       K, B, H, W, C, N, xm, dm, _s(), vimg, _sgd_arg(sgd), bnb)
     if ok:
         planes_launches["wgrad_halo"] += 1
     return bool(ok)
@@ -1013,13 +1058,15 @@ def conv_halo_bn_dense_fwd(x, coef, relu: bool, valid_rows, w, out, w_planes=Non
 
 
 def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dpre, relu_mask=None, dx_out=None,
-           dx_planes: int = 0, pre_part=None):
+           dx_planes: int = 0, pre_part=None, coef_out=None):
     """`dx_out`: a channel slice of a wider gradient buffer (same strides as `x`) that dX is ADDED
     into (DenseNet block-buffer gradient); otherwise dX is returned contiguous. `dx_planes`
     (fp32, contiguous, no dx_out): 1 = also write dX's split planes, 2 = only the planes (dX is
     their fp32-typed alias); the planes [K, 2, R, C] are then returned as a third value.
     `pre_part`: [K, parts, 2, C] Σĝ / Σĝ·x̂ partials written by the dgrad that produced dy
-    (conv_dgrad(bnb=)) — the reduction pass over dy and x is skipped."""
+    (conv_dgrad(bnb=)) — the reduction pass over dy and x is skipped.
+    `coef_out` [K, C, 3] fp32: compute the backward coefficients (a, d, e) and dγ / dβ only, into
+    it — no dX is written (bn_bwd_apply_planes or a loader applies them later); returns None."""
     K, R, C = x.shape
     x, ldx = _pix_stride(x)
     assert x.stride(0) == R * ldx
@@ -1050,13 +1097,31 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
     assert dy.dtype == x.dtype == gamma.dtype
     if pre_part is not None:
         assert pre_part.dtype == F32 and pre_part.is_contiguous() and pre_part.shape == (K, (R + 31) // 32, 2, C)
+    if coef_out is not None:
+        assert coef_out.shape == (K, C, 3) and coef_out.dtype == F32 and coef_out.is_contiguous()
+        assert dx_out is None and not need_dpre
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
               _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx,
               int(dx_out is not None), _p(dxp), int(dx_planes != 2), _p(pre_part),
-              0 if pre_part is None else pre_part.shape[1])
+              0 if pre_part is None else pre_part.shape[1], _p(coef_out), 1 if coef_out is not None else 0)
+    if coef_out is not None:
+        return None
     if dx_planes:
         return dx, dpre, dxp
     return dx, dpre
+
+
+def bn_bwd_apply_planes(dy, x, relu_mask, coef, valid_rows, dxp) -> None:
+    """The apply stage of a BN backward whose coefficients bn_bwd(coef_out=) computed: dX's split
+    planes into `dxp` [K, 2, R, C] (dy, x [K, R, C] fp32 contiguous; `relu_mask` the ReLU bits or
+    None for no gate) — bn_bwd's own apply pass, for a consumer that cannot apply it itself."""
+    K, R, C = x.shape
+    assert dy.shape == x.shape and dy.is_contiguous() and x.is_contiguous() and dy.dtype == F32 == x.dtype
+    assert coef.shape == (K, C, 3) and dxp.shape == (K, 2, R, C) and dxp.is_contiguous()
+    ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
+    vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
+    _C.bn_bwd(_p(dy), _p(x), NULL, NULL, NULL, NULL, _p(vr), 0, K, R, C, int(relu_mask is not None), _p(dxp), NULL,
+              NULL, NULL, 0, _p(ws), _p(relu_mask), NULL, 1, _s(), C, 0, _p(dxp), 0, NULL, 0, _p(coef), 2)
 
 
 # ------------------------------------------------------------------------ layernorm

@@ -78,6 +78,11 @@ class RuntimeOptions:
     """With halo_wgrad: a conv whose BN(+ReLU) input is applied in its forward halo loader
     (bn_fused_halo) also applies it in its weight gradient's loader from the raw tensor, so training
     never writes that BN's normalised planes (off: the fused forward writes them for the wgrad)."""
+    bn_bwd_in_wgrad: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_BWD_IN_WGRAD", True))
+    """A training BN(+ReLU) whose input gradient feeds only a 3x3 stride-1 conv's backward (ResNet
+    BasicBlock bn1 / identity-block bn2, layers 1-3) computes its coefficients only: that conv's halo
+    weight gradient applies the BN backward in its dY loader and writes dX's planes for the dgrad
+    (ops.functional DeferredBNBwd; off: the BN backward's own apply pass writes them)."""
     dgrad_wt: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DGRAD_WT", True))
     """3x3 stride-1 plane dgrads run the forward tiles on transposed, flipped weight planes (built
     per launch; off: the k-major weight tiles)."""

@@ -88,6 +88,9 @@ class Session:
         self.dc = create_dataset_collection(cfg.dataset_name, cfg.dataset_kwargs, cfg.seed, self.device,
                                             self.compute_dtype,
                                             image_channels=stored_image_channels(cfg.model_name, spec))
+        if cfg.merge_validation_to_training_set:
+            # (before the partition: the clients' shards are drawn from the merged training split)
+            self.dc.merge_validation_into_train(cfg.seed)
         if practitioners is None:
             labels = self.dc.train.labels  # (graph: labels of the training nodes)
             practitioners = create_practitioners(cfg, labels)
@@ -97,7 +100,7 @@ class Session:
             for wid, p in enumerate(practitioners):
                 p.set_worker_id(wid)
             cfg.worker_number = len(practitioners)
-        if cfg.dataset_sampling == "iid" and self.dc.graph is None:
+        if cfg.dataset_sampling == "iid" and self.dc.graph is None and not cfg.merge_validation_to_training_set:
             # Validation phase for keep-best-model selection (reference aggregation_worker.py:28-35)
             self.dc.split_validation(cfg.seed)
             vparts = get_partition("iid", self.dc.validation_labels(), len(practitioners), seed=cfg.seed + 1)

@@ -216,6 +216,25 @@ def test_resnet18_fused_sgd_matches_flat_step(hip, tmp_path, monkeypatch):
     assert torch.equal(a.server.global_parameter, b.server.global_parameter)
 
 
+def test_resnet18_bn_bwd_in_wgrad_bitwise(hip, tmp_path):
+    """BN backward applied in the halo weight gradient's dY loader (OPTIONS.bn_bwd_in_wgrad,
+    ops.functional DeferredBNBwd): a 2-round ResNet-18 session (ragged last batches, fused SGD with
+    the dgrad's transposed weight planes built before the stepping wgrad) gives the global model of
+    the separate BN-backward apply pass bit for bit."""
+    from distributed_learning_simulator_amd.ops import functional as Fn
+
+    ov = {"round": 2, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
+          "learning_rate": 0.05}
+    Fn.bn_bwd_defer_count.update(wgrad=0, materialized=0)
+    with options.override(bn_bwd_in_wgrad=True):
+        a, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    # (l1: 4 BNs, l2 / l3: block 2's bn1 + bn2 each, per step)
+    assert Fn.bn_bwd_defer_count["wgrad"] > 0, Fn.bn_bwd_defer_count
+    with options.override(bn_bwd_in_wgrad=False):
+        b, _ = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    assert torch.equal(a.server.global_parameter, b.server.global_parameter)
+
+
 def test_transformer_imdb_bitwise_reproducible_and_matches_cpu(hip, tmp_path):
     """The reference's imdb Transformer (d_model 100, 5 heads: dh 20 on the MFMA attention, with
     attention-probability dropout): two GPU runs are bitwise equal (deterministic LN / bias /

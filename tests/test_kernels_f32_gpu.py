@@ -100,12 +100,12 @@ def test_conv_f32_every_variant(hip, case):
         _close(y, y_ref)
         dx = torch.empty_like(x)
         hip._C.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, w.stride(0), K, 1, B, OH, y.shape[3], Co, H,
-                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+                          W, Ci, k, k, s, p, v, 1, stream, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
         _close(dx, dx_ref)
     for v in range(hip._C.conv_tn_f32_num_variants()):
         gw = torch.zeros((K, Co, k, k, Ci), device=DEV)
         hip._C.conv_tn(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), M * Co, B * H * W * Ci, gw.stride(0), B, H, W, Ci,
-                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream, 0, 0, 0, 0, 0)
+                       OH, dy.shape[3], k, k, s, p, M, Co, k * k * Ci, K, v, 1, stream, 0, 0, 0, 0, 0, None)
         _close(gw, dw_ref)
 
 
@@ -1390,3 +1390,69 @@ def test_dgrad_acc_mask(hip, case):
         a = hip.conv_dgrad(dy, w, (H, H), 1, 1, w_split=ws, dy_planes=dyp, acc=g, acc_mask=mask, wt=wt)
         b = hip.conv_dgrad(dy, w, (H, H), 1, 1, w_split=ws, dy_planes=dyp, acc=dense, wt=wt)
         assert torch.equal(a, b), wt
+
+
+@pytest.mark.parametrize("case", [(2, 3, 32, 64, 64), (2, 2, 16, 128, 128), (3, 2, 8, 256, 256), (2, 2, 16, 64, 128)])
+@pytest.mark.parametrize("xmode", ["planes", "bn"])
+@pytest.mark.parametrize("gate", [True, False])
+def test_halo_wgrad_bn_bwd_loader(hip, case, xmode, gate):
+    """The halo weight gradient with the BatchNorm BACKWARD applied in its dY loader (dy mode 2,
+    ops.functional DeferredBNBwd): from the BN's output gradient, raw input, ReLU bits and the
+    coefficients bn_bwd(coef_out=) computed, it builds dX = a·(dy·relu') + e·x + d exactly as
+    bn_bwd_apply does — the dX planes it stores for the dgrad are bitwise the BN backward's own
+    (zeros past a client's valid rows, also in the images it skips), the weight gradient is bitwise
+    the one from those planes and within 1e-5 of fp64; the standalone apply stage
+    (bn_bwd_apply_planes) writes the same bits."""
+    K, B, H, C, N = case
+    torch.manual_seed(31)
+    R = B * H * H
+    dyo = _f(K, R, N)  # the BN output's gradient
+    xb = _f(K, R, N) * 1.5 + 0.25  # the BN's raw input (the conv output)
+    mean = xb.mean(dim=1).contiguous()
+    rstd = (1.0 / (xb.var(dim=1) + 1e-5).sqrt()).contiguous()
+    gamma = torch.rand(K, N, device=DEV) + 0.5
+    mask = torch.randint(0, 256, (K, R, N // 8), dtype=torch.uint8, device=DEV) if gate else None
+    valid = torch.tensor([B - 1] + [B] * (K - 1), dtype=torch.int32, device=DEV)
+    vr = (valid * (H * H)).contiguous()
+    # the BN backward's own passes: fp32 dX + its planes, dγ / dβ
+    g1, b1 = torch.empty(K, N, device=DEV), torch.empty(K, N, device=DEV)
+    dx, _, dxp_ref = hip.bn_bwd(dyo, xb, None, mean, rstd, gamma, vr, gate, g1, b1, False, relu_mask=mask,
+                                dx_planes=1)
+    # coefficients only, then the loader
+    coef = torch.empty((K, N, 3), device=DEV)
+    g2, b2 = torch.empty(K, N, device=DEV), torch.empty(K, N, device=DEV)
+    assert hip.bn_bwd(dyo, xb, None, mean, rstd, gamma, vr, gate, g2, b2, False, relu_mask=mask, coef_out=coef) is None
+    assert torch.equal(g1, g2) and torch.equal(b1, b2)
+    x = _f(K, B, H, H, C)
+    xkw, xo = {}, x
+    if xmode == "planes":
+        xkw["x_planes"] = hip.split_planes(x)
+    else:  # (the conv's input is itself a BN(+ReLU) applied in the x loader: x mode 2)
+        xr = x * 2.0 + 0.5
+        xcoef, _, _ = hip.bn_coef(xr.view(K, R, C), torch.rand(K, C, device=DEV) + 0.5,
+                                  torch.randn(K, C, device=DEV) * 0.3, vr)
+        xkw["bn"] = (xcoef, True, vr)
+        xo = xr
+        yp = torch.empty((K, 2, R, C), dtype=torch.bfloat16, device=DEV)
+        hip.bn_apply_only(xr.view(K, R, C), xcoef, vr, True, yp)
+        x = torch.empty((K, B, H, H, C), device=DEV)  # (shape carrier)
+        xplanes = yp.view(K, 2, B, H, H, C)
+    dxo = torch.empty((K, B, H, H, N), device=DEV)  # (shape carrier: the planes-only alias)
+    for skip in (None, valid):
+        dxp = torch.full((K, 2, R, N), 12345.0, dtype=torch.bfloat16, device=DEV)
+        gw = torch.empty((K, N, 3, 3, C), device=DEV)
+        assert hip.halo_wgrad(dxo, xo, gw, valid=skip, bn_bwd=(dyo, xb, mask, coef, vr, dxp), **xkw)
+        assert torch.equal(dxp, dxp_ref), "the loader's dX planes must be bn_bwd_apply's bits"
+        base = torch.empty_like(gw)
+        pl = {"x_planes": xplanes} if xmode == "bn" else {"x_planes": xkw["x_planes"]}
+        assert hip.halo_wgrad(dx.view(K, B, H, H, N), x, base, dy_planes=dxp_ref.view(K, 2, B, H, H, N), valid=skip,
+                              **pl)
+        assert torch.equal(gw, base), "same operand bits as the planes path"
+    xd = _d(x) if xmode == "planes" else None
+    if xd is None:
+        xd = (_d(xo) * _d(xcoef[..., 0]).view(K, 1, 1, 1, C) + _d(xcoef[..., 1]).view(K, 1, 1, 1, C)).clamp_min(0)
+        xd[0, B - 1] = 0
+    _close(gw, ref.conv_wgrad(_d(dx).view(K, B, H, H, N), xd, (K, N, 3, 3, C), 1, 1))
+    alone = torch.full((K, 2, R, N), 7.0, dtype=torch.bfloat16, device=DEV)
+    hip.bn_bwd_apply_planes(dyo, xb, mask, coef, vr, alone)
+    assert torch.equal(alone, dxp_ref)

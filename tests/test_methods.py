@@ -375,3 +375,27 @@ def test_per_client_hyper_parameter_artefacts(tmp_path):
         with open(os.path.join(tmp_path, f"worker_{c}", "hyper_parameter.json")) as f:
             h = json.load(f)
         assert h["learning_rate"] == 0.02 and h["epoch"] == 1 and h["batch_size"] == cfg.batch_size
+
+
+@pytest.mark.parametrize("cfg_name,extra", [
+    ("fed_avg/mnist.yaml", {"worker_number": 3}),
+    ("fed_avg/imdb.yaml", {"worker_number": 2, "dataset_kwargs.scale": 0.004, "dataset_kwargs.max_len": 32,
+                           "model_kwargs.max_len": 32}),
+])
+def test_merge_validation_to_training_set(cfg_name, extra, tmp_path):
+    """`merge_validation_to_training_set: true` (reference config.py:27): the Validation half of
+    the test split joins the training split before the partition — the clients' shards cover
+    n_train + n_test // 2 samples, some of them test-split samples — and no Validation phase is
+    left (no keep-best-model selection); the server tests on the other half."""
+    sess, res = _run(cfg_name, {**SMALL, **extra, "merge_validation_to_training_set": True}, tmp_path / "m")
+    base, _ = _run(cfg_name, {**SMALL, **extra}, tmp_path / "b")
+    dc, dcb = sess.dc, base.dc
+    n_val = dcb.validation_indices.numel()
+    assert dc.validation_indices is None and dcb.validation_indices is not None
+    assert dc.train.n == dcb.train.n + n_val
+    assert torch.equal(dc.test_indices, dcb.test_indices)
+    assert torch.equal(dc.train.labels[dcb.train.n:], dcb.test.labels[dcb.validation_indices])
+    shards = torch.cat([p.indices(dc.spec.name) for p in sess.practitioners.values()])
+    assert int(shards.max()) >= dcb.train.n  # merged samples are dealt to clients
+    assert not sess.worker._choose_model_by_validation
+    assert res["performance"]
