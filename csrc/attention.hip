@@ -289,11 +289,11 @@ bool attn_supported(int L, int DH) {
 
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
               int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds,
-              int heads_per_client, float drop_p, bf16_t* o_pl, long o_pl_cl) {
+              int heads_per_client, float drop_p) {
   if (use_mfma(L, DH))
     return attn_fwd_mfma(q, k, v, key_valid, o, lse, KBH, H, L, DH, f32, s, ldqkv, ldo, drop_seeds, heads_per_client,
-                         drop_p, o_pl, o_pl_cl);
-  if (ldqkv || ldo || drop_p > 0.f || o_pl) return false;  // packed layouts / dropout / planes: MFMA kernels only
+                         drop_p);
+  if (ldqkv || ldo || drop_p > 0.f) return false;  // packed layouts / dropout: MFMA kernels only
   if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));
@@ -307,12 +307,11 @@ bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid,
 
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
-              hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds, int heads_per_client, float drop_p,
-              bf16_t* dq_pl, bf16_t* dk_pl, bf16_t* dv_pl, long g_pl_cl) {
+              hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds, int heads_per_client, float drop_p) {
   if (use_mfma(L, DH))
     return attn_bwd_mfma(dout, q, k, v, o, lse, key_valid, dq, dk, dv, delta, KBH, H, L, DH, f32, s, ldqkv, ldo,
-                         drop_seeds, heads_per_client, drop_p, dq_pl, dk_pl, dv_pl, g_pl_cl);
-  if (ldqkv || ldo || drop_p > 0.f || dq_pl || dk_pl || dv_pl) return false;
+                         drop_seeds, heads_per_client, drop_p);
+  if (ldqkv || ldo || drop_p > 0.f) return false;
   if (!attn_supported(L, DH) || (2L * L * DH + 2L * L) * 4 > 160L * 1024) return false;
   const int rows = attn_rows(L);
   const dim3 grid((unsigned)KBH, cdiv(L, rows));

@@ -185,11 +185,11 @@ __device__ __forceinline__ void put_colrows(const Img<T>& m, const f32x16& v) {
 
 // global store of a transposed accumulator tile (lane column = matrix row `row`, tile rows =
 // 16 of the DH columns starting at d0): out[row][d0 + rows(e)]
-// pl_row (fp32 only, may be null): the same row of the output's split planes (hi; lo pl_lo
-// elements further) — written with the values, for the plane GEMM that reads this output
+// (writing the outputs' split planes here for the projections' plane GEMMs measured +0.4-0.5 s
+// per FedOBD Transformer round each for o and dqkv — their stores cost more than the plane GEMMs
+// gain at d 512, profiles/r5_c6_ab_tfm_planes.txt — and was removed)
 template <typename T, int DH>
-__device__ __forceinline__ void store_rowcols(T* out_row, int d0, const f32x16& v, float mul,
-                                              bf16_t* pl_row = nullptr, long pl_lo = 0) {
+__device__ __forceinline__ void store_rowcols(T* out_row, int d0, const f32x16& v, float mul) {
   const int h = (threadIdx.x & 63) >> 5;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -197,27 +197,8 @@ __device__ __forceinline__ void store_rowcols(T* out_row, int d0, const f32x16& 
     const int d = d0 + 8 * j + 4 * h;
     if (d < DH) {
       store_vec<4>(out_row + d, x);  // (DH % 4 == 0)
-      if (sizeof(T) == 4 && pl_row) {
-        uint32_t h0, l0, h1, l1;
-        split_pair(x[0], x[1], h0, l0);
-        split_pair(x[2], x[3], h1, l1);
-        *reinterpret_cast<uint2*>(pl_row + d) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(pl_row + pl_lo + d) = make_uint2(l0, l1);
-      }
     }
   }
-}
-
-// Output split planes [clients][2][per-client elements] of an output addressed by element
-// offsets (pl_cl = elements per client; a head belongs to client head / hpc)
-struct PlOut {
-  bf16_t* p;
-  long cl;
-  int hpc;
-};
-// the hi-plane pointer of the output row at element offset `off` of head `head` (null: no planes)
-__device__ __forceinline__ bf16_t* pl_row(const PlOut& po, long head, long off) {
-  return po.p ? po.p + (head / po.hpc) * po.cl + off : nullptr;
 }
 
 // attention-probability dropout of one score (client seed, head within the client, query, key)
@@ -242,8 +223,8 @@ template <typename T, int DH, int DP>
 __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__ q, const T* __restrict__ k,
                                                            const T* __restrict__ v, const int* __restrict__ key_valid,
                                                            T* __restrict__ o, float* __restrict__ lse, int L, int H,
-                                                           float scale, HeadLayout lq, HeadLayout lo, AttnDropArgs dr,
-                                                           PlOut opl) {
+                                                           float scale, HeadLayout lq, HeadLayout lo,
+                                                           AttnDropArgs dr) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
   constexpr int LDK = pad_ld(DP), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NP * RB * LDK], Vs[NP * RB * LDK];
@@ -308,8 +289,7 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
     const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
     for (int t = 0; t < DP / 32; ++t)
-      store_rowcols<T, DH>(o + obase + (long)qrow * lo.ld, t * 32, ot[t], inv,
-                           pl_row(opl, head, obase + (long)qrow * lo.ld), opl.cl);
+      store_rowcols<T, DH>(o + obase + (long)qrow * lo.ld, t * 32, ot[t], inv);
     if ((lane >> 5) == 0) lse[head * L + qrow] = l > 0.f ? m + __logf(l) : 0.f;
   }
 }
@@ -321,8 +301,7 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
                                                               const T* __restrict__ o, const float* __restrict__ lse,
                                                               const int* __restrict__ key_valid, T* __restrict__ dq,
                                                               float* __restrict__ delta, int L, int H, float scale,
-                                                              HeadLayout lq, HeadLayout lo, AttnDropArgs dr,
-                                                              PlOut gpl) {
+                                                              HeadLayout lq, HeadLayout lo, AttnDropArgs dr) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
   constexpr int LDK = pad_ld(DP), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[NP * RB * LDK], Vs[NP * RB * LDK];
@@ -391,24 +370,23 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
   if (qok) {
 #pragma unroll
     for (int t = 0; t < DP / 32; ++t)
-      store_rowcols<T, DH>(dq + base + (long)qrow * lq.ld, t * 32, dqt[t], 1.f,
-                           pl_row(gpl, head, base + (long)qrow * lq.ld), gpl.cl);
+      store_rowcols<T, DH>(dq + base + (long)qrow * lq.ld, t * 32, dqt[t], 1.f);
   }
 }
 
 // ------------------------------------------------------------------------------ dK, dV
-// RELOAD: the lane's K / V fragments are re-read (L2) and re-split for each query block instead of
-// held in registers for the whole kernel — at fp32 dh 64 they are 64 VGPRs, which keep the kernel
-// at one wave per SIMD (217 VGPRs + 64 AGPRs)
-template <typename T, int DH, int DP, bool RELOAD = false>
+// The lane's K / V fragments stay in registers for the whole kernel (at fp32 dh 64: 64 VGPRs, one
+// wave per SIMD). Re-reading them per query block instead (two waves per SIMD) measured 2.73 →
+// 2.23 ms per launch alone but 22.40 → 22.62 s per FedOBD stage-1 round beside the other
+// sub-cohort's GEMMs (profiles/r5_c10_ab_attn_dkv_reload.txt): removed.
+template <typename T, int DH, int DP>
 __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
                                                                const T* __restrict__ k, const T* __restrict__ v,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
                                                                const int* __restrict__ key_valid, T* __restrict__ dk,
                                                                T* __restrict__ dv, int L, int H, float scale,
-                                                               HeadLayout lq, HeadLayout lo, AttnDropArgs dr,
-                                                               PlOut kpl, PlOut vpl) {
+                                                               HeadLayout lq, HeadLayout lo, AttnDropArgs dr) {
   constexpr int NP = sizeof(T) == 4 ? 2 : 1;
   constexpr int LDK = pad_ld(DP), LDP = pad_ld(RB);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[NP * RB * LDK], Os[NP * RB * LDK];
@@ -424,15 +402,12 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   const Img<T> QI{Qs, LDK, RB * LDK}, OI{Os, LDK, RB * LDK};
   const Img<T> PI{Ps[wid], LDP, RB * LDP}, SI{Ss[wid], LDP, RB * LDP};
 
-  constexpr int NKF = RELOAD ? 1 : DP / 16;
-  Frag<T> kf[NKF], vf[NKF];
-  if constexpr (!RELOAD) {
+  Frag<T> kf[DP / 16], vf[DP / 16];
 #pragma unroll
-    for (int ks = 0; ks < DP / 16; ++ks) {
-      const int d = ks * 16 + 8 * h, n = kok ? min(8, max(0, DH - d)) : 0;
-      kf[ks] = frag_global<T>(k + base + (long)key * lq.ld + d, n);
-      vf[ks] = frag_global<T>(v + base + (long)key * lq.ld + d, n);
-    }
+  for (int ks = 0; ks < DP / 16; ++ks) {
+    const int d = ks * 16 + 8 * h, n = kok ? min(8, max(0, DH - d)) : 0;
+    kf[ks] = frag_global<T>(k + base + (long)key * lq.ld + d, n);
+    vf[ks] = frag_global<T>(v + base + (long)key * lq.ld + d, n);
   }
   f32x16 dkt[DP / 32], dvt[DP / 32];
 #pragma unroll
@@ -452,16 +427,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
     f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < DP / 16; ++ks) {
-      if constexpr (RELOAD) {
-        const int d = ks * 16 + 8 * h, n = kok ? min(8, max(0, DH - d)) : 0;
-        const Frag<T> kr = frag_global<T>(k + base + (long)key * lq.ld + d, n);
-        const Frag<T> vr = frag_global<T>(v + base + (long)key * lq.ld + d, n);
-        mma<T>(s, frag_rm<T>(QI, 0, ks * 16), kr);
-        mma<T>(dp, frag_rm<T>(OI, 0, ks * 16), vr);
-      } else {
-        mma<T>(s, frag_rm<T>(QI, 0, ks * 16), kf[ks]);   // S = Q·Kᵀ   [query][key]
-        mma<T>(dp, frag_rm<T>(OI, 0, ks * 16), vf[ks]);  // dP̃ = dO·Vᵀ [query][key]
-      }
+      mma<T>(s, frag_rm<T>(QI, 0, ks * 16), kf[ks]);   // S = Q·Kᵀ   [query][key]
+      mma<T>(dp, frag_rm<T>(OI, 0, ks * 16), vf[ks]);  // dP̃ = dO·Vᵀ [query][key]
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -487,10 +454,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   if (key < L) {
 #pragma unroll
     for (int t = 0; t < DP / 32; ++t) {
-      store_rowcols<T, DH>(dk + base + (long)key * lq.ld, t * 32, dkt[t], 1.f,
-                           pl_row(kpl, head, base + (long)key * lq.ld), kpl.cl);
-      store_rowcols<T, DH>(dv + base + (long)key * lq.ld, t * 32, dvt[t], 1.f,
-                           pl_row(vpl, head, base + (long)key * lq.ld), vpl.cl);
+      store_rowcols<T, DH>(dk + base + (long)key * lq.ld, t * 32, dkt[t], 1.f);
+      store_rowcols<T, DH>(dv + base + (long)key * lq.ld, t * 32, dvt[t], 1.f);
     }
   }
 }
@@ -550,48 +515,33 @@ static HeadLayout head_layout(int ld, int H, int L, int DH) {
 
 bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
                    int H, int L, int DH, int f32, hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds,
-                   int heads_per_client, float drop_p, bf16_t* o_pl, long o_pl_cl) {
+                   int heads_per_client, float drop_p) {
   if (!attn_mfma_supported(L, DH)) return false;
-  if (o_pl && (!f32 || o_pl_cl <= 0)) return false;
   const dim3 grid((unsigned)KBH, cdiv(L, 4 * RB));
   const float scale = 1.0f / sqrtf((float)DH);
   const HeadLayout lq = head_layout(ldqkv, H, L, DH), lo = head_layout(ldo, H, L, DH);
   const int hpc = heads_per_client > 0 ? heads_per_client : 1;
   const AttnDropArgs dr{drop_p > 0.f ? drop_seeds : nullptr, hpc, drop_p};
-  const PlOut opl{o_pl, o_pl_cl, hpc};
   DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_fwd_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s, CP(q),
-                                                 CP(k), CP(v), key_valid, MP(o), lse, L, H, scale, lq, lo, dr, opl)));
+                                                 CP(k), CP(v), key_valid, MP(o), lse, L, H, scale, lq, lo, dr)));
   return true;
 }
 
 bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                    const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
                    int f32, hipStream_t s, int ldqkv, int ldo, const uint32_t* drop_seeds, int heads_per_client,
-                   float drop_p, bf16_t* dq_pl, bf16_t* dk_pl, bf16_t* dv_pl, long g_pl_cl) {
+                   float drop_p) {
   if (!attn_mfma_supported(L, DH)) return false;
-  if ((dq_pl || dk_pl || dv_pl) && (!f32 || g_pl_cl <= 0)) return false;
   const dim3 grid((unsigned)KBH, cdiv(L, 4 * RB));
   const float scale = 1.0f / sqrtf((float)DH);
   const HeadLayout lq = head_layout(ldqkv, H, L, DH), lo = head_layout(ldo, H, L, DH);
   const int hpc = heads_per_client > 0 ? heads_per_client : 1;
   const AttnDropArgs dr{drop_p > 0.f ? drop_seeds : nullptr, hpc, drop_p};
-  const PlOut qpl{dq_pl, g_pl_cl, hpc}, kpl{dk_pl, g_pl_cl, hpc}, vpl{dv_pl, g_pl_cl, hpc};
   DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dq_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s,
                                                  CP(dout), CP(q), CP(k), CP(v), CP(o), lse, key_valid, MP(dq), delta,
-                                                 L, H, scale, lq, lo, dr, qpl)));
-  // DLS_ATTN_DKV_RELOAD=1 (fp32 dh > 32): K / V fragments re-read per query block, two waves per SIMD
-  // instead of one. Measured (bench/attn_bench.py, Transformer-base shape, 25 clients): backward
-  // 2.73 → 2.23 ms per launch in isolation, but the FedOBD stage-1 round 22.40 → 22.62 s, where the
-  // dK/dV kernel runs beside the other sub-cohort's GEMMs (profiles/r5_c10_ab_attn_dkv_reload.txt)
-  const bool reload = f32 && DH > 32 && native_option(g_opt_attn_dkv_reload, "DLS_ATTN_DKV_RELOAD", 0) != 0;
-  if (reload) {
-    DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dkv_mfma_kernel<TT, D, DPAD, true>), grid, dim3(WG), 0,
-                                                   s, CP(dout), CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk),
-                                                   MP(dv), L, H, scale, lq, lo, dr, kpl, vpl)));
-  } else {
-    DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dkv_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s,
-                                                   CP(dout), CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk), MP(dv),
-                                                   L, H, scale, lq, lo, dr, kpl, vpl)));
-  }
+                                                 L, H, scale, lq, lo, dr)));
+  DISPATCH_T(f32, MFMA_DH(DH, hipLaunchKernelGGL((attn_bwd_dkv_mfma_kernel<TT, D, DPAD>), grid, dim3(WG), 0, s,
+                                                 CP(dout), CP(q), CP(k), CP(v), lse, delta, key_valid, MP(dk), MP(dv),
+                                                 L, H, scale, lq, lo, dr)));
   return true;
 }

@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define DLS_CHECK(x)                                                                  \
+#define CHECK_HIP(x)                                                                  \
   do {                                                                                \
     hipError_t err__ = (x);                                                           \
     if (err__ != hipSuccess) {                                                        \

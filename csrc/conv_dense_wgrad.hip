@@ -254,18 +254,18 @@ bool dense_wgrad(const float* dy, long dy_cs, int ldy, const float* y, long y_cs
   p.ldy_x = ldy_x;
   p.valid_rows = valid_rows;
   const int grid = K * p.nchunks * p.G;
-#define DLS_DW(REC_)                                                                                 \
+#define DW_LAUNCH(REC_)                                                                                 \
   switch (cfg) {                                                                                     \
     case 0: hipLaunchKernelGGL((dense_wgrad_kernel<1, 8, 32, REC_>), dim3(grid), dim3(576), 0, s, p); break;  \
     case 1: hipLaunchKernelGGL((dense_wgrad_kernel<1, 16, 16, REC_>), dim3(grid), dim3(576), 0, s, p); break; \
     default: hipLaunchKernelGGL((dense_wgrad_kernel<2, 8, 8, REC_>), dim3(grid), dim3(576), 0, s, p); break;  \
   }
   if (bn_sc) {
-    DLS_DW(true)
+    DW_LAUNCH(true)
   } else {
-    DLS_DW(false)
+    DW_LAUNCH(false)
   }
-#undef DLS_DW
+#undef DW_LAUNCH
   const long total = (long)K * N * 9 * C;
   hipLaunchKernelGGL(dense_wgrad_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
   return true;

@@ -404,13 +404,10 @@ bool launch_nt_f32_variant(int v, const ConvNTParams& p, int K, int va, int vb, 
 
 int vw(int c) { return (c % 8 == 0) ? 8 : (c % 4 == 0) ? 4 : 1; }
 
-// DLS_F32_SMALLK: small-cohort tile rules, bit 0 the NT 64x64 rule, bit 1 the wgrad 64x64 rule.
-// Off by default: they win in isolation (kernel_bench at K = 4) but lose inside a round, where
-// the other sub-cohort stream fills the GPU and per-CU efficiency matters more than grid fill
-// (rank 0's share of an 8-rank round, 2 streams: off 743 ms, NT rule 757, wgrad rule 765)
-int small_k_rules() {
-  return native_option(g_opt_f32_smallk, "DLS_F32_SMALLK", 0);
-}
+// (small-cohort 64x64 tile rules for the NT and wgrad kernels won in isolation — kernel_bench at
+// K = 4 — but lost inside a round, where the other sub-cohort stream fills the GPU and per-CU
+// efficiency matters more than grid fill: rank 0's share of an 8-rank round, 2 streams, 743 ms
+// without, 757 / 765 ms with the NT / wgrad rule — removed)
 
 // --------------------------------------------------------------------------- TN (wgrad)
 template <int BMc, int BNr, int BKT, int WM, int WN, int VA, int VB, int NBUF>
@@ -676,9 +673,6 @@ int tn_f32_default_variant(int K, int Co, int R) {
   auto tiles = [&](int bm, int bn) { return (long)K * cdiv(Co, bm) * cdiv(R, bn); };
   if (Co <= 32 && R > 64) return 6;
   if (Co <= 32 || R <= 64) return 5;
-  // K <= 8 (8 ranks x 3 streams): the 64x64 tile beats the split-K 128 tiles on every ResNet-18
-  // layer (K = 4: l4a 143 vs 103, l2a 129 vs 94, l4 178 vs 157 TFLOP/s); at K = 13 it loses
-  if (K <= 8 && (small_k_rules() & 2)) return 5;
   // re-measured after the buffer-load loaders (kernel_bench --f32 --sweep, K = 33 / 100):
   // 1x1 shortcut convs (R <= 256) the 64x64 tile (l4sc 165 vs 97 TFLOP/s at K = 33); Co <= 64 the
   // 64x128 double-buffered tile; 3x3 layers with Co >= 256 and R >= 2048 the 256x128 tile (l3 / l4
@@ -752,13 +746,6 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     // waves per SIMD, v9: l1 dgrad 233-236 vs 205-222, strided-dgrad classes onto 64 channels
     // 157-179 vs 132-151, the 8-channel stem 118 vs 98-108; fwd equal)
     variant = p.N <= 64 ? 9 : 1;
-    // opt-in (DLS_F32_SMALLK bit 0, see small_k_rules): few clients per launch (K = 4-5) or short
-    // reductions → the 20-KB 64x64 tile. In isolation (kernel_bench --f32 --sweep, K = 4 / 13): l4 / l4a fwd
-    // and dgrad at K = 4 (<= 128 big tiles) 142-154 vs 95-105 TFLOP/s; 1x1 shortcut convs
-    // (R <= 128) 63-117 vs 41-107; stride-2 dgrad parity classes onto 64 channels 114-138 vs
-    // 91-125. At K >= 13 the big tiles win the 3x3 layers (l4 269 vs 198).
-    const long big = (long)K * cdiv(p.M, variant == 9 ? 256 : 128) * cdiv(p.N, variant == 9 ? 64 : 128);
-    if ((small_k_rules() & 1) && (big <= 192 || p.R <= 128 || (p.out_s > 1 && p.N <= 64))) variant = 7;
     if (p.N <= 32) variant = 10;
   }
   // variants without the requested vector widths fall back to the all-widths 64x64 tile

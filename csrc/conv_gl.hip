@@ -270,9 +270,9 @@ __global__ void __launch_bounds__(256) flip_t_kernel(const bf16_t* __restrict__ 
 const bf16_t* zero_page() {
   static bf16_t* z = nullptr;
   if (!z) {
-    DLS_CHECK(hipMalloc(&z, 4096));
-    DLS_CHECK(hipMemset(z, 0, 4096));
-    DLS_CHECK(hipDeviceSynchronize());
+    CHECK_HIP(hipMalloc(&z, 4096));
+    CHECK_HIP(hipMemset(z, 0, 4096));
+    CHECK_HIP(hipDeviceSynchronize());
   }
   return z;
 }

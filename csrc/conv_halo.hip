@@ -464,11 +464,9 @@ void launch_halo_bnf(const ConvNTParams& p, int K, hipStream_t s) {
                      dim3(WM * WN * 64), 0, s, p);
 }
 
-// two taps per pipeline step (DLS_HALO_TPS2 bit mask): 1 the 32² / 64-channel ResNet shape (headline
-// −2.6 %, profiles/r5_c12_ab_halo_tps2.txt), 2 the DenseNet growth convs (32-wide N tiles; measured
-// even: 9.45 / 9.48 vs 9.46 / 9.53 s per DenseNet-40 round, so off by default)
-static int halo_tps2() { return native_option(g_opt_halo_tps2, "DLS_HALO_TPS2", 1) & 1; }
-static int halo_tps2_dense() { return native_option(g_opt_halo_tps2, "DLS_HALO_TPS2", 1) & 2; }
+// two taps per pipeline step: the 32² / 64-channel ResNet shape (headline −2.6 %,
+// profiles/r5_c12_ab_halo_tps2.txt); the DenseNet growth convs (32-wide N tiles) measured even with
+// it (9.45 / 9.48 vs 9.46 / 9.53 s per DenseNet-40 round) and keep one tap per step
 
 int g_halo_mode = -1;  // -1 shape rule, 0 never, 1 whenever supported (tests / A-B)
 int g_halo_variant = -1;
@@ -521,32 +519,12 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
   if (p.bn_x != nullptr) {  // fused BN input: the default one-halo-buffer shapes only
     if (g_halo_variant >= 0 || cfg == 3) return false;
     switch (cfg) {
-      case 0:
-        if (halo_tps2())
-          launch_halo_bnf<1, 8, 32, 64, 4, 2, 2, 1, 2, 2>(p, K, s);
-        else
-          launch_halo_bnf<1, 8, 32, 64, 4, 2, 3>(p, K, s);
-        break;
+      case 0: launch_halo_bnf<1, 8, 32, 64, 4, 2, 2, 1, 2, 2>(p, K, s); break;
       case 1: launch_halo_bnf<1, 16, 16, 128, 4, 2, 2>(p, K, s); break;
       case 2: launch_halo_bnf<2, 8, 8, 128, 4, 2, 2>(p, K, s); break;
-      case 4:
-        if (halo_tps2_dense())
-          launch_halo_bnf<1, 8, 32, 32, 4, 1, 2, 2, 2>(p, K, s);
-        else
-          launch_halo_bnf<1, 8, 32, 32, 4, 1, 3, 2>(p, K, s);  // 62 KB
-        break;
-      case 5:
-        if (halo_tps2_dense())
-          launch_halo_bnf<1, 16, 16, 32, 4, 1, 2, 2, 2>(p, K, s);
-        else
-          launch_halo_bnf<1, 16, 16, 32, 4, 1, 3, 2>(p, K, s);  // 62 KB
-        break;
-      case 6:
-        if (halo_tps2_dense())
-          launch_halo_bnf<4, 8, 8, 32, 4, 1, 2, 2, 2>(p, K, s);
-        else
-          launch_halo_bnf<4, 8, 8, 32, 4, 1, 3, 2>(p, K, s);  // 78 KB
-        break;
+      case 4: launch_halo_bnf<1, 8, 32, 32, 4, 1, 3, 2>(p, K, s); break;   // 62 KB
+      case 5: launch_halo_bnf<1, 16, 16, 32, 4, 1, 3, 2>(p, K, s); break;  // 62 KB
+      case 6: launch_halo_bnf<4, 8, 8, 32, 4, 1, 3, 2>(p, K, s); break;    // 78 KB
       // (8 waves of 32 x 32 per tile: bitwise the same, no faster — r4_c14_dn_w*.log)
       default: return false;
     }
@@ -554,14 +532,13 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
   }
   const int v = g_halo_variant >= 0 ? g_halo_variant : (cfg == 2 ? 2 : 1);
   if (cfg > 3) return false;
-  if (cfg == 0 && (v == 3 || (v == 1 && halo_tps2()))) {  // 32² / 64 channels: two taps per step
+  if (cfg == 0 && (v == 1 || v == 3)) {  // 32² / 64 channels: two taps per step
     launch_halo<1, 8, 32, 64, 4, 2, 1, 2, 2>(p, K, s);      // 74 KB
     return true;
   }
   if (v > 2) return false;
   switch (cfg * 3 + v) {
     case 0: launch_halo<1, 8, 32, 64, 4, 1, 2, 3>(p, K, s); break;    // 120 KB, 4 waves
-    case 1: launch_halo<1, 8, 32, 64, 4, 2, 1, 3>(p, K, s); break;    // 73 KB, 8 waves
     case 2: launch_halo<1, 8, 32, 64, 4, 2, 2, 3>(p, K, s); break;    // 121 KB
     case 3: launch_halo<1, 16, 16, 128, 4, 2, 2, 3>(p, K, s); break;  // 144 KB
     case 4: launch_halo<1, 16, 16, 128, 4, 2, 1, 2>(p, K, s); break;  // 80 KB

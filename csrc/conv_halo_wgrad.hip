@@ -438,36 +438,36 @@ bool halo_wgrad(HaloWgradParams p, int xm, int dm, hipStream_t s) {
   p.G = halo_wgrad_G(cfg, p.B, p.H, p.W, p.C, p.N);
   if (p.G > 1 && p.part == nullptr) return false;
   const int grid = p.K * p.G * p.nblk * p.cblk;
-#define DLS_HW_LAUNCH_XD(TH, TW, U, XM, DM) \
+#define HW_LAUNCH_XD(TH, TW, U, XM, DM) \
   hipLaunchKernelGGL((halo_wgrad_kernel<TH, TW, XM, DM, U>), dim3(grid), dim3(768), 0, s, p)
-#define DLS_HW_LAUNCH1(TH, TW, U)                               \
+#define HW_LAUNCH1(TH, TW, U)                               \
   switch (xm * 3 + dm) {                                        \
-    case 0: DLS_HW_LAUNCH_XD(TH, TW, U, 0, 0); break;          \
-    case 1: DLS_HW_LAUNCH_XD(TH, TW, U, 0, 1); break;          \
-    case 2: DLS_HW_LAUNCH_XD(TH, TW, U, 0, 2); break;          \
-    case 3: DLS_HW_LAUNCH_XD(TH, TW, U, 1, 0); break;          \
-    case 4: DLS_HW_LAUNCH_XD(TH, TW, U, 1, 1); break;          \
-    case 5: DLS_HW_LAUNCH_XD(TH, TW, U, 1, 2); break;          \
-    case 6: DLS_HW_LAUNCH_XD(TH, TW, U, 2, 0); break;          \
-    case 7: DLS_HW_LAUNCH_XD(TH, TW, U, 2, 1); break;          \
-    default: DLS_HW_LAUNCH_XD(TH, TW, U, 2, 2); break;         \
+    case 0: HW_LAUNCH_XD(TH, TW, U, 0, 0); break;          \
+    case 1: HW_LAUNCH_XD(TH, TW, U, 0, 1); break;          \
+    case 2: HW_LAUNCH_XD(TH, TW, U, 0, 2); break;          \
+    case 3: HW_LAUNCH_XD(TH, TW, U, 1, 0); break;          \
+    case 4: HW_LAUNCH_XD(TH, TW, U, 1, 1); break;          \
+    case 5: HW_LAUNCH_XD(TH, TW, U, 1, 2); break;          \
+    case 6: HW_LAUNCH_XD(TH, TW, U, 2, 0); break;          \
+    case 7: HW_LAUNCH_XD(TH, TW, U, 2, 1); break;          \
+    default: HW_LAUNCH_XD(TH, TW, U, 2, 2); break;         \
   }
-#define DLS_HW_LAUNCH(TH, TW) \
+#define HW_LAUNCH(TH, TW) \
   if (unroll == 2) {          \
-    DLS_HW_LAUNCH1(TH, TW, 2) \
+    HW_LAUNCH1(TH, TW, 2) \
   } else {                    \
-    DLS_HW_LAUNCH1(TH, TW, 1) \
+    HW_LAUNCH1(TH, TW, 1) \
   }
   // (k-step unroll: 2 lets the compiler fetch the next step's fragments under this step's MFMAs)
   const int unroll = native_option(g_opt_halo_wgrad_unroll, "DLS_HALO_WGRAD_UNROLL", 1);
   if (cfg == 0) {
-    DLS_HW_LAUNCH(8, 16)
+    HW_LAUNCH(8, 16)
   } else {
-    DLS_HW_LAUNCH(8, 8)
+    HW_LAUNCH(8, 8)
   }
-#undef DLS_HW_LAUNCH
-#undef DLS_HW_LAUNCH1
-#undef DLS_HW_LAUNCH_XD
+#undef HW_LAUNCH
+#undef HW_LAUNCH1
+#undef HW_LAUNCH_XD
   if (p.G > 1) {
     const long total4 = (long)p.K * p.N * 9 * p.C / 4;
     hipLaunchKernelGGL(halo_wgrad_fold_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, p);

@@ -636,10 +636,8 @@ int tn_pl_default_variant(int K, int Co, int R) {
 // KREF 8 would cost l2 / l3 6-7 % in slab traffic (profiles/r3_kernel_bench_small_cohort_kref.log).
 // So 1-rank and 2-rank runs train bitwise alike; an 8-rank run's weight gradients differ from
 // them by summation order only. Co <= 64 (5 tiles per client: l1) takes 8 at any cohort size (236
-// vs 216 TFLOP/s at 50 clients). DLS_TN_KREF pins one KREF for every launch.
+// vs 216 TFLOP/s at 50 clients).
 static int tn_kref(int K, int Co) {
-  const int v = native_option(g_opt_tn_kref, "DLS_TN_KREF", 0);
-  if (v > 0) return v;
   return (K >= 16 && Co > 64) ? 32 : 8;
 }
 void tn_pl_split(int K, int Co, int R, int M, int variant, int& splitk, int& mps) {
@@ -697,22 +695,22 @@ bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s) {
   const int grid = (int)((long)K * cdiv(p.Co, t.bm) * cdiv(p.R, t.bn) * p.splitk);
   // (the SGD epilogue instantiation where the kernel itself stores: no split-K slabs)
   const bool sgd = p.sgd.theta != nullptr && p.splitk == 1;
-#define DLS_TN_PL(BM_, BN_, WM_, WN_, NST_, ILV_, NT_)                                                       \
+#define TN_PL_LAUNCH(BM_, BN_, WM_, WN_, NST_, ILV_, NT_)                                                       \
   if (sgd)                                                                                                 \
     hipLaunchKernelGGL((conv_tn_pl_kernel<BM_, BN_, WM_, WN_, NST_, ILV_, true>), dim3(grid), dim3(NT_), 0, s, p); \
   else                                                                                                     \
     hipLaunchKernelGGL((conv_tn_pl_kernel<BM_, BN_, WM_, WN_, NST_, ILV_>), dim3(grid), dim3(NT_), 0, s, p);
   switch (variant) {
-    case 0: DLS_TN_PL(128, 128, 2, 2, 2, false, 256) break;
-    case 1: DLS_TN_PL(64, 128, 2, 2, 2, false, 256) break;
-    case 2: DLS_TN_PL(128, 128, 2, 2, 3, true, 256) break;
-    case 3: DLS_TN_PL(64, 128, 2, 2, 3, true, 256) break;
-    case 4: DLS_TN_PL(256, 128, 4, 2, 2, false, 512) break;
-    case 5: DLS_TN_PL(128, 256, 2, 4, 2, false, 512) break;
-    case 6: DLS_TN_PL(256, 256, 2, 4, 2, false, 512) break;
+    case 0: TN_PL_LAUNCH(128, 128, 2, 2, 2, false, 256) break;
+    case 1: TN_PL_LAUNCH(64, 128, 2, 2, 2, false, 256) break;
+    case 2: TN_PL_LAUNCH(128, 128, 2, 2, 3, true, 256) break;
+    case 3: TN_PL_LAUNCH(64, 128, 2, 2, 3, true, 256) break;
+    case 4: TN_PL_LAUNCH(256, 128, 4, 2, 2, false, 512) break;
+    case 5: TN_PL_LAUNCH(128, 256, 2, 4, 2, false, 512) break;
+    case 6: TN_PL_LAUNCH(256, 256, 2, 4, 2, false, 512) break;
     default: return false;
   }
-#undef DLS_TN_PL
+#undef TN_PL_LAUNCH
   if (p.splitk > 1) tn_fold(p.part, p.dw, p.dw_cs, K, p.splitk, (long)p.Co * p.R, s, &p.sgd);
   return true;
 }

@@ -11,13 +11,11 @@ typedef uint16_t bf16_t;
 // set_native_option() — the Python RuntimeOptions (distributed_learning_simulator_amd/options.py)
 // — overrides it at any time between launches. Defined in elementwise.hip.
 constexpr int kOptUnset = -1000000;
-extern int g_opt_attn_mfma, g_opt_f32_smallk, g_opt_conv_gl, g_opt_pl_min_wg, g_opt_tn_kref, g_opt_bn_coef_groups;
+extern int g_opt_attn_mfma, g_opt_conv_gl, g_opt_pl_min_wg;
 extern int g_opt_halo_wgrad_unroll;  // conv_halo_wgrad.hip k-step unroll (1 or 2)
 // halo fwd / dgrad tiles past the valid samples skip their work (ConvNTParams::skip_valid; env
 // DLS_SKIP_INVALID, Python OPTIONS.skip_invalid)
 extern int g_opt_halo_skip;
-extern int g_opt_attn_dkv_reload;
-extern int g_opt_halo_tps2;  // conv_halo.hip: 32² / 64-channel convs with two taps per pipeline step
 int native_option(int& slot, const char* env, int dflt);
 bool set_native_option(const char* name, int value);  // false: unknown name
 
@@ -432,16 +430,15 @@ int conv_tn_f32_splitk(int K, int Co, int R, int M, int gco, int gc, int variant
 long bn_workspace_floats(int K, long R, int C);  // ws size for bn_fwd / bn_bwd
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
-            uint8_t* relu_mask, unsigned* counters, int f32, hipStream_t s,
+            uint8_t* relu_mask, int f32, hipStream_t s,
             int ldx = 0, const float* pre_part = nullptr,
             int pre_nparts = 0, bf16_t* yp = nullptr,
-            int y_f32 = 1, float* coef_out = nullptr, int apply = 1);  // yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; counters: optional [K] zeros (fused
-                                  // coefs); ldx: row stride of x / res (channel slice of a wider buffer), y
+            int y_f32 = 1, float* coef_out = nullptr, int apply = 1);  // yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; ldx: row stride of x / res (channel slice of a wider buffer), y
                                   // contiguous; pre_part: [K][pre_nparts][2C] Σx / Σx² partials from the
                                   // producing conv's epilogue (ConvNTParams::stats) — no statistics pass
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
-            float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, unsigned* counters, int f32,
+            float* dbeta, long dg_cs, float* ws, const uint8_t* relu_mask, int f32,
             hipStream_t s, int ldx = 0,
             int acc_dx = 0, bf16_t* dxp = nullptr,
             int dx_f32 = 1,  // dxp / dx_f32: split planes of dX (fp32, contiguous) with or without dX; relu_mask (from bn_fwd) replaces reading y for the ReLU gate; x / dx at row
@@ -574,25 +571,19 @@ bool attn_mfma_supported(int L, int DH);
 // key, drop_seeds[head / hpc]) >= p·2³², hpc = heads per client (B·H); MFMA kernels only
 bool attn_fwd_mfma(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH,
                    int H, int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0,
-                   const uint32_t* drop_seeds = nullptr, int heads_per_client = 1, float drop_p = 0.f,
-                   bf16_t* o_pl = nullptr, long o_pl_cl = 0);
-// o_pl / dq_pl / dk_pl / dv_pl (fp32, MFMA kernels only): also write the output's split planes
-// [clients][2][pl_cl] (hi, lo) at the output's own element offsets within a client (pl_cl =
-// elements per client of the output buffer; dq / dk / dv share the packed dqkv buffer's planes)
+                   const uint32_t* drop_seeds = nullptr, int heads_per_client = 1, float drop_p = 0.f);
 bool attn_bwd_mfma(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                    const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH,
                    int f32, hipStream_t s, int ldqkv = 0, int ldo = 0, const uint32_t* drop_seeds = nullptr,
-                   int heads_per_client = 1, float drop_p = 0.f, bf16_t* dq_pl = nullptr, bf16_t* dk_pl = nullptr,
-                   bf16_t* dv_pl = nullptr, long g_pl_cl = 0);
+                   int heads_per_client = 1, float drop_p = 0.f);
 bool attn_packed_supported(int L, int DH);
 bool attn_fwd(const void* q, const void* k, const void* v, const int* key_valid, void* o, float* lse, long KBH, int H,
               int L, int DH, int f32, hipStream_t s, int ldqkv = 0, int ldo = 0, const uint32_t* drop_seeds = nullptr,
-              int heads_per_client = 1, float drop_p = 0.f, bf16_t* o_pl = nullptr, long o_pl_cl = 0);
+              int heads_per_client = 1, float drop_p = 0.f);
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
               const int* key_valid, void* dq, void* dk, void* dv, float* delta, long KBH, int H, int L, int DH, int f32,
               hipStream_t s, int ldqkv = 0, int ldo = 0, const uint32_t* drop_seeds = nullptr,
-              int heads_per_client = 1, float drop_p = 0.f, bf16_t* dq_pl = nullptr, bf16_t* dk_pl = nullptr,
-              bf16_t* dv_pl = nullptr, long g_pl_cl = 0);
+              int heads_per_client = 1, float drop_p = 0.f);
 void spmm(const int* rowptr, const int* col, const float* val, const void* x, void* y, int K, int N, int Nx, int F,
           long x_cs, long y_cs, int f32, hipStream_t s);
 void gather_rows(const void* src, const int* idx, void* dst, long n, long row_bytes, hipStream_t s);

@@ -945,8 +945,8 @@ void gap_bwd(const void* dy, void* dx, int KB, int HW, int C, int f32, hipStream
 void ce_fwd_bwd(const void* logits, const int* labels, const int* valid, float* loss, float* correct, void* dlogits,
                 int K, int B, int NC, int f32, hipStream_t s, float* rowbuf) {
   if (!rowbuf) {
-    DLS_CHECK(hipMemsetAsync(loss, 0, sizeof(float) * K, s));
-    DLS_CHECK(hipMemsetAsync(correct, 0, sizeof(float) * K, s));
+    CHECK_HIP(hipMemsetAsync(loss, 0, sizeof(float) * K, s));
+    CHECK_HIP(hipMemsetAsync(correct, 0, sizeof(float) * K, s));
   }
   DISPATCH_T(f32, hipLaunchKernelGGL(ce_kernel<TT>, dim3(cdiv(B, 4), K), dim3(256), 0, s, CP(logits), labels, valid,
                                      loss, correct, MP(dlogits), B, NC, rowbuf));
@@ -1012,7 +1012,7 @@ void weighted_sum(const float* x, const double* w, double* out, int K, long P, l
 void mix_rows(const float* x, const float* w, void* out, int K, int M, long P, long ld, long ld_out, int f32,
               hipStream_t s) {
   if (K > MIX_KMAX || M <= 0) {  // the wrapper (ops/hip.py) routes larger K elsewhere
-    DLS_CHECK(hipErrorInvalidValue);
+    CHECK_HIP(hipErrorInvalidValue);
     return;
   }
   dim3 grid(grid_for(P / 4, 256, 2048), cdiv(M, MIX_M));
@@ -1033,7 +1033,7 @@ void dropout_mask(uint8_t* mask, int K, long P, float p, const uint32_t* seeds, 
 
 void block_sq_norms(const float* x, const int* block_ids, float* out, int K, long P, long ld, int nblocks,
                     hipStream_t s) {
-  DLS_CHECK(hipMemsetAsync(out, 0, sizeof(float) * K * nblocks, s));
+  CHECK_HIP(hipMemsetAsync(out, 0, sizeof(float) * K * nblocks, s));
   dim3 grid(grid_for(P / 16, 256, 1024), K);
   hipLaunchKernelGGL(block_sq_kernel, grid, dim3(256), 0, s, x, block_ids, out, P, ld, nblocks);
 }
@@ -1148,10 +1148,9 @@ void synth_images(const int64_t* idx, long n, long npix, int C, int Cout, const 
 }
 
 // ------------------------------------------------------------------ host launch knobs (dls.h)
-int g_opt_attn_mfma = kOptUnset, g_opt_f32_smallk = kOptUnset, g_opt_conv_gl = kOptUnset;
-int g_opt_pl_min_wg = kOptUnset, g_opt_tn_kref = kOptUnset, g_opt_bn_coef_groups = kOptUnset;
-int g_opt_halo_wgrad_unroll = kOptUnset, g_opt_halo_skip = kOptUnset, g_opt_attn_dkv_reload = kOptUnset,
-    g_opt_halo_tps2 = kOptUnset;
+int g_opt_attn_mfma = kOptUnset, g_opt_conv_gl = kOptUnset;
+int g_opt_pl_min_wg = kOptUnset;
+int g_opt_halo_wgrad_unroll = kOptUnset, g_opt_halo_skip = kOptUnset;
 
 int native_option(int& slot, const char* env, int dflt) {
   if (slot == kOptUnset) {
@@ -1166,11 +1165,9 @@ bool set_native_option(const char* name, int value) {
     const char* name;
     int* slot;
   };
-  const Entry table[] = {{"attn_mfma", &g_opt_attn_mfma},   {"f32_smallk", &g_opt_f32_smallk},
+  const Entry table[] = {{"attn_mfma", &g_opt_attn_mfma},
                          {"conv_gl", &g_opt_conv_gl},       {"pl_min_wg", &g_opt_pl_min_wg},
-                         {"tn_kref", &g_opt_tn_kref},       {"bn_coef_groups", &g_opt_bn_coef_groups},
-                         {"halo_wgrad_unroll", &g_opt_halo_wgrad_unroll}, {"halo_skip", &g_opt_halo_skip},
-                         {"attn_dkv_reload", &g_opt_attn_dkv_reload}, {"halo_tps2", &g_opt_halo_tps2}};
+                         {"halo_wgrad_unroll", &g_opt_halo_wgrad_unroll}, {"halo_skip", &g_opt_halo_skip}};
   for (const Entry& t : table)
     if (strcmp(t.name, name) == 0) {
       *t.slot = value;

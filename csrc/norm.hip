@@ -26,10 +26,6 @@ static int rows_per_block(long R, int K) {
 }
 
 // Arguments of the per-(client, channel) coefficient stage (see bn_coef_kernel for the math).
-// When `counters` is set, the reduction kernel computes the coefficients itself: the last of a
-// client's workgroups to publish its partial sums (agent-scope release → counter ticket →
-// agent-scope acquire) reduces them in fixed order and resets the ticket — one launch less per
-// BN pass and no separate tiny coefficient kernel.
 struct BNCoefArgs {
   const void* gamma;  // T (bf16 or fp32, the compute dtype)
   const void* beta;
@@ -43,7 +39,6 @@ struct BNCoefArgs {
   long dg_cs, g_cs;
   float eps;
   int rep, bwd;
-  unsigned* counters;  // [K], zero at launch; reset by the last workgroup of each client
 };
 
 template <typename T>
@@ -89,7 +84,6 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
   // lda / ldb: row strides of a and of b (channel-sliced views of a wider buffer, DenseNet);
   // yv is contiguous (row stride C)
   __shared__ float red[2][256 * V];
-  __shared__ int is_last;
   const int k = blockIdx.y;
   const int CT = C / V;
   const int tid = threadIdx.x;
@@ -180,34 +174,6 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
     }
     __syncthreads();
   }
-  if (MODE >= 2 || ca.counters == nullptr) return;
-  // ---- last-arriver coefficient stage (cdna_hip_programming.md Guideline 16 protocol)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's partials issued+done
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (ROCm 7.2: keep the wait after the release)
-    is_last = atomicAdd(&ca.counters[k], 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const int nvalid2 = valid_rows ? min(valid_rows[k], R) : R;
-  const float n = (float)max(nvalid2, 1);
-  const float* parts = ws + (long)k * gridDim.x * 2 * C;
-  for (int c = tid; c < C; c += blockDim.x) {
-    float a0 = 0.f, a1 = 0.f;
-    for (int b = 0; b < (int)gridDim.x; ++b) {  // fixed order: deterministic
-      a0 += parts[(long)b * 2 * C + c];
-      a1 += parts[(long)b * 2 * C + C + c];
-    }
-    bn_coef_math<T>(a0, a1, k, c, C, n, ca);
-  }
-  if (tid == 0) atomicExch(&ca.counters[k], 0u);
 }
 
 // Per-(client, channel) coefficients from the reduced sums (one tiny launch), so the apply
@@ -217,14 +183,10 @@ __global__ void __launch_bounds__(256) chan_reduce_kernel(const T* __restrict__ 
 //        dγ = Σgx̂, dβ = Σg written straight into the flat gradient buffer
 // grid (cdiv(C, 32), K), 1024 threads = 32 channels × 32 part-groups: the per-workgroup partial
 // sums of a client are reduced in a fixed order (deterministic) by 8 lanes per channel.
-// partial-sum rows reduced in parallel per channel: G = 8 (256-thread workgroups) by default,
-// DLS_BN_COEF_GROUPS=32 for the 1024-thread form. The coefficient kernel is tiny and sits on the
-// stream's critical path; a 1024-thread workgroup has to wait for a whole CU's wave slots while
-// the other sub-cohort stream's GEMM workgroups occupy them
-constexpr int COEF_GROUPS = 32;  // (upper bound: shared-memory sizing)
-static int coef_groups() {
-  return native_option(g_opt_bn_coef_groups, "DLS_BN_COEF_GROUPS", 8) == 32 ? 32 : 8;
-}
+// partial-sum rows reduced in parallel per channel: G = 8 (256-thread workgroups). The coefficient
+// kernel is tiny and sits on the stream's critical path; a 1024-thread form (G = 32) has to wait
+// for a whole CU's wave slots while the other sub-cohort stream's GEMM workgroups occupy them
+// (measured slower, profiles/r2_ab_bn_coef_groups.txt: removed)
 
 // DenseNet running channel sums: out[k·out_cs + j·ldo + c] = Σ_p part[k][p][j][c] in fp64 (j = Σx, Σx²;
 // c < g new channels) — the epilogue partials of one growth conv summed into the block's running
@@ -402,10 +364,7 @@ __global__ void __launch_bounds__(32 * G) bn_coef_kernel(const PT* __restrict__ 
 
 template <typename TT, typename PT, typename... A>
 void launch_coef(dim3 grid, hipStream_t s, A... args) {
-  if (coef_groups() == 32)
-    hipLaunchKernelGGL((bn_coef_kernel<TT, PT, 32>), grid, dim3(32 * 32), 0, s, args...);
-  else
-    hipLaunchKernelGGL((bn_coef_kernel<TT, PT, 8>), grid, dim3(32 * 8), 0, s, args...);
+  hipLaunchKernelGGL((bn_coef_kernel<TT, PT, 8>), grid, dim3(32 * 8), 0, s, args...);
 }
 
 // V fp32 values → their split-bf16 planes (hi = bf16(v), lo = bf16(v − hi), RNE): the operand form
@@ -810,7 +769,7 @@ long bn_workspace_floats(int K, long R, int C) {
 
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
-            uint8_t* rmask, unsigned* counters, int f32, hipStream_t s, int ldx, const float* pre_part,
+            uint8_t* rmask, int f32, hipStream_t s, int ldx, const float* pre_part,
             int pre_nparts, bf16_t* yp, int y_f32, float* coef_out, int apply) {
   if (ldx == 0) ldx = C;
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums. coef_out: the
@@ -822,7 +781,7 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
   dim3 grid(cdiv(R, rpb), K);
   const int nparts = pre_part ? pre_nparts : (int)grid.x;
   const int V = vw(std::gcd(C, ldx));
-  BNCoefArgs ca{gamma, beta, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, eps, rep, 0, counters};
+  BNCoefArgs ca{gamma, beta, nullptr, nullptr, mean, rstd, coef, nullptr, nullptr, 0L, g_cs, eps, rep, 0};
   if (V != 8) rmask = nullptr;  // bit masks need 8-channel vectors
   DISPATCH_T(f32, {
     if (!pre_part) {  // (else the producing conv's epilogue already wrote the partial sums)
@@ -838,7 +797,7 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
       launch_coef<TT, double>(dim3(cdiv(C, 32), K), s, (const double*)folds, nfold, CP(gamma), CP(beta), valid_rows,
                               (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
                               (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0, 0, 0L);
-    } else if (!counters || pre_part) {
+    } else {
       launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, part, nparts, CP(gamma), CP(beta), valid_rows,
                              (const float*)nullptr, (const float*)nullptr, mean, rstd, coef, (float*)nullptr,
                              (float*)nullptr, 0L, g_cs, K, R, C, eps, rep, 0, 0, 0L);
@@ -868,7 +827,7 @@ void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int
 
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, void* dx, void* dpre, float* dgamma,
-            float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, unsigned* counters, int f32, hipStream_t s,
+            float* dbeta, long dg_cs, float* ws, const uint8_t* rmask, int f32, hipStream_t s,
             int ldx, int acc_dx, bf16_t* dxp, int dx_f32, const float* pre_part, int pre_nparts, float* coef_ext,
             int stage) {
   // stage 0: coefficients + apply; 1: coefficients (and dγ, dβ) only, into coef_ext — a consumer
@@ -884,7 +843,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
   dim3 grid(cdiv(R, rpb), K);
   const int V = vw(std::gcd(C, ldx));
   if (V != 8) rmask = nullptr;
-  BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1, counters};
+  BNCoefArgs ca{gamma, nullptr, mean, rstd, nullptr, nullptr, coef, dgamma, dbeta, dg_cs, g_cs, 0.f, 1, 1};
   DISPATCH_T(f32, {
     if (stage == 2) {
     } else if (pre_part) {  // Σĝ / Σĝx̂ from the dgrad epilogue that produced dy: coefficients only
@@ -905,7 +864,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, con
       DISPATCH_V(V, hipLaunchKernelGGL((chan_reduce_kernel<TT, VV, 1>), grid, dim3(256), 0, s, CP(dy), CP(x), CP(y),
                                        mean, rstd, valid_rows, R, C, relu, part, (long)2 * C, rpb, rmask, ca, C, ldx));
     }
-    if (!counters && !pre_part && stage != 2)
+    if (!pre_part && stage != 2)
       launch_coef<TT, float>(dim3(cdiv(C, 32), K), s, (const float*)part, (int)grid.x, CP(gamma), (const TT*)nullptr,
                              valid_rows, mean, rstd, (float*)nullptr, (float*)nullptr, coef, dgamma, dbeta, dg_cs, g_cs, K,
                              R, C, 0.f, 1, 1, 0, 0L);
@@ -981,13 +940,11 @@ void col_sum(const void* x, float* out, long out_cs, int K, long rows, int C, in
                                                    out_cs, rpb, nullptr, BNCoefArgs{}, C, C)));
 }
 
-static int g_opt_ln_pairs = kOptUnset;
-
 void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd, long g_cs, int K,
             long rpc, int C, float eps, int rep, int f32, hipStream_t s, bf16_t* yp) {
   const long nrows = (long)K * rpc;
-  const bool pairs = f32 && native_option(g_opt_ln_pairs, "DLS_LN_PAIRS", 1) && (C == 512 || C == 1024) &&
-                     (rep == 1 || g_cs % 2 == 0);
+  // (column pairs per lane: 0.39 → 0.24 ms at 25 × 8192 × 512, profiles/r5_c25_ab_layernorm.txt)
+  const bool pairs = f32 && (C == 512 || C == 1024) && (rep == 1 || g_cs % 2 == 0);
   if (pairs) {
     const float* xf = static_cast<const float*>(x);
     if (C == 512)
@@ -1004,10 +961,7 @@ void ln_fwd(const void* x, const void* gamma, const void* beta, void* y, float* 
                                      CP(beta), MP(y), mean, rstd, g_cs, nrows, rpc, C, eps, rep, f32 ? yp : nullptr));
 }
 
-static int g_opt_ln_rpw = kOptUnset;
 static int ln_rows_per_wave(long rpc) {
-  const int v = native_option(g_opt_ln_rpw, "DLS_LN_RPW", 0);  // (A/B knob: rows per wave)
-  if (v > 0) return v;
   return rpc >= 4096 ? 128 : 16;  // (128: bench/ln_bench.py 0.33 -> 0.28 ms vs 64)
 }
 

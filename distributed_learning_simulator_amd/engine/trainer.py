@@ -103,6 +103,8 @@ class _StepGraph:
         self.samples = torch.zeros_like(self.loss)
         self.graph = None
         self.eager_steps = 0
+        self.full = True  # (the full cohort's step: never evicted for a ragged one)
+        self.key = None  # (its CohortTrainer._graphs key)
 
 
 def _nullctx():
@@ -491,26 +493,36 @@ class CohortTrainer:
             sg.samples[a:b] += vf
             self.optimizer_step(b - a, lr, active, first, row0=a, fused=fused)
 
-    def _step_graph(self, n: int, parts) -> _StepGraph:
+    def _step_graph(self, n: int, parts, full: bool = True, keep=()) -> _StepGraph | None:
         """The step graph of an n-row cohort split into `parts` (created empty; captured on its
         second use). Each captured graph owns a private pool sized for its step; n varies with
-        failures / last waves / uneven rank shares / ragged epoch ends, so only the most recent
-        `max_graphs` are kept (a dropped graph's pool returns to the driver before the next
-        capture)."""
+        failures / last waves / uneven rank shares / ragged epoch ends, so at most `max_graphs`
+        are kept (a dropped graph's pool returns to the driver before the next capture), least
+        recently used first out — except that a ragged step (`full` False) never evicts a
+        full-cohort graph nor a graph in `keep` (the ones this round already uses): then it gets
+        None, and the caller runs it on a graph of more rows (the extra rows masked)."""
         B = self.hyper.batch_size
         key = (n, B, tuple(parts))
         sg = self._graphs.get(key)
-        if sg is None:
-            while len(self._graphs) >= self.max_graphs:
-                old = self._graphs.pop(next(iter(self._graphs)))
-                old.graph = None
-                del old
-                with DEVICE_LOCK:
-                    torch.cuda.synchronize(self.device)
-                    torch.cuda.empty_cache()
-            sg = self._graphs[key] = _StepGraph(n, B, self.device)
-        else:  # (most recently used last: the full-cohort graph is not the one evicted)
+        if sg is not None:  # (most recently used last)
             self._graphs[key] = self._graphs.pop(key)
+            return sg
+        while len(self._graphs) >= max(self.max_graphs, 1):
+            victim = next((k for k, g in self._graphs.items() if all(g is not u for u in keep)
+                           and (full or not g.full)), None)
+            if victim is None:
+                if full:  # (the caller's own round holds every graph: the oldest goes)
+                    victim = next(iter(self._graphs))
+                else:
+                    return None
+            old = self._graphs.pop(victim)
+            old.graph = None
+            del old
+            with DEVICE_LOCK:
+                torch.cuda.synchronize(self.device)
+                torch.cuda.empty_cache()
+        sg = self._graphs[key] = _StepGraph(n, B, self.device)
+        sg.full, sg.key = full, key
         return sg
 
     def _run_step_graph(self, sg: _StepGraph, parts, ds) -> None:
@@ -580,10 +592,20 @@ class CohortTrainer:
                 if n > 0:
                     sg = used.get(n)
                     if sg is None:
-                        sg = used[n] = self._step_graph(n, parts if n == K else self._sub_cohorts(n))
-                        sg.loss.zero_()
-                        sg.correct.zero_()
-                        sg.samples.zero_()
+                        sg = self._step_graph(n, parts if n == K else self._sub_cohorts(n), full=n == K,
+                                              keep=tuple(used.values()))
+                        if sg is None:
+                            # (the graph budget holds the full cohort's and this round's ragged
+                            # graphs: the smallest of them with >= n rows runs it, rows past n
+                            # inactive — their slot rows carry no batch)
+                            n = min(m for m in used if m >= n)
+                            sg = used[n]
+                        else:
+                            used[n] = sg
+                            sg.loss.zero_()
+                            sg.correct.zero_()
+                            sg.samples.zero_()
+                    self._graphs[sg.key] = self._graphs.pop(sg.key)  # (most recently used last)
                     sg.slot.copy_(schedule.packed[s, :n])
                     self._run_step_graph(sg, parts if n == K else self._sub_cohorts(n), ds)
                 if s + 1 == schedule.epoch_end[e]:

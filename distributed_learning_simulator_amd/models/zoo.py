@@ -13,7 +13,6 @@ import math
 import torch
 
 from ..engine.params import ParamLayout
-from ..options import OPTIONS
 from ..ops import functional as Fn
 from .layers import (AvgPool, BatchNorm, Conv2d, Embedding, conv_bn, Flatten, LayerNorm, Linear,
                      MaxPool, Module, ReLU, RunCtx, Seq)
@@ -191,12 +190,11 @@ class ResNetNet(Module):
         # downsample block follows (its convs read planes; its shortcut is a conv too), fp32 only
         # before the pooling head, both otherwise (planes for the convs, fp32 for the identity
         # shortcut's residual add)
-        # (OPTIONS.block_out_planes = False: every block output in both forms, the A/B switch)
         blocks = [b for s in self.stages for b in s.children]
         for i, b in enumerate(blocks):
             nxt = blocks[i + 1] if i + 1 < len(blocks) else None
             op = 0 if nxt is None else 2 if nxt.down is not None else 1
-            x = b.forward(x, ctx, out_planes=op if OPTIONS.block_out_planes else 1)
+            x = b.forward(x, ctx, out_planes=op)
         x = Fn.global_avg_pool(x)
         return self.fc.forward(x, ctx)
 
@@ -306,9 +304,7 @@ class MultiheadAttention(Module):
             ad = {"drop_p": attn_drop, "drop_seeds": attn_seeds if attn_seeds is not None else ctx.dropout_seeds()}
         if Fn.packed_attention_ok(qkv, L, D // self.h):
             # heads read / written in place in the projections' row layouts (no permute copies)
-            # o (and dqkv in the backward) come with split planes for the projections' plane GEMMs
-            planes = getattr(ctx.P, "split", None) is not None
-            o = Fn.attention_packed(qkv, key_valid, self.h, planes=planes, **ad)
+            o = Fn.attention_packed(qkv, key_valid, self.h, **ad)
             return self.out_proj.forward(o, ctx, residual=residual, **drop)
         qkv = qkv.reshape(K, B, L, 3, self.h, D // self.h)
         qkv = qkv.permute(3, 0, 1, 4, 2, 5)  # 3,K,B,H,L,dh
@@ -353,7 +349,7 @@ class TransformerEncoderLayer(Module):
         sa = ctx.dropout_seeds() if p else None  # (the attention's site first: same order as unfused)
         # each residual input has two readers — a projection and the residual add of a later one — and
         # the later one hands its gradient to the first one's dgrad epilogue (no autograd add pass)
-        fuse = ctx.training and OPTIONS.linear_res_link
+        fuse = ctx.training
         l1 = Fn.ResidualLink() if fuse else None
         l2 = Fn.ResidualLink() if fuse else None
         # the LayerNorm outputs feed linear1 / the next layer's in_proj (split planes: the LDS-DMA

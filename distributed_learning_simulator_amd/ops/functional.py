@@ -114,7 +114,7 @@ class BNBwdLink:
 # planes carries them as attribute `_dls_planes` ([K, 2, *shape[1:]], ops.hip.planes_buffer
 # layout); `_dls_planes_only` marks a tensor whose fp32 bytes ARE those planes (the producer
 # wrote nothing else) — only a planes-reading GEMM may consume it. OPTIONS.planes = False
-# disables them (OPTIONS.ln_planes: the LayerNorm ones).
+# disables them.
 
 
 def _planes_of(t):
@@ -224,8 +224,7 @@ class _Conv(torch.autograd.Function):
         big = be is not ref and max(x[0].numel(), y_numel) * x.element_size() >= (1 << 31)
         if stats is not None:
             stats.dy_planes_ok = stats.dy_planes_ok and be.planes_fit(y_numel)
-        want_stats = stats is not None and be is not ref and x.dtype == torch.float32 and OPTIONS.bn_epilogue_stats \
-            and not big
+        want_stats = stats is not None and be is not ref and x.dtype == torch.float32 and not big
         y = None
         ctx.bn_src = None
         defer = getattr(x, "_dls_bn_defer", None)
@@ -237,7 +236,7 @@ class _Conv(torch.autograd.Function):
                                     device=x.device) if want_stats else None)
                 # the weight gradient applies the BN in its own loader too (halo wgrad x mode 2): then
                 # the normalised planes are never written, only the ReLU bits the BN backward reads
-                bn_wgrad = (defer.write_out and gw is not None and OPTIONS.halo_wgrad and OPTIONS.halo_wgrad_bn
+                bn_wgrad = (defer.write_out and gw is not None and OPTIONS.halo_wgrad
                             and x.shape[-1] == ci and be.halo_wgrad_ok(x.shape, w.shape[1]))
                 y = be.conv_halo_bn_fwd(defer.x.view(x.shape), defer.coef, defer.relu, defer.valid_rows, w, w_split,
                                         stats=part, stats_valid=stats.valid if want_stats else None,
@@ -277,7 +276,7 @@ class _Conv(torch.autograd.Function):
         # (valid samples: the BatchNorm around this conv zeroes the rows past them, so the halo wgrad
         # skips those images' tiles)
         ctx.valid = stats.valid if (stats is not None and OPTIONS.skip_invalid) else None
-        ctx.dgrad_wt = OPTIONS.dgrad_wt and be is not ref
+        ctx.dgrad_wt = be is not ref
         ctx.save_for_backward(x, w)
         ctx.gw, ctx.gb, ctx.stride, ctx.pad, ctx.ci = gw, gb, stride, pad, ci
         ctx.link = link
@@ -488,7 +487,7 @@ class _Linear(torch.autograd.Function):
         if not native:
             w_split = x_planes = None
             out_planes = dx_planes = False
-        if not OPTIONS.tfm_planes & 1:
+        if not OPTIONS.tfm_planes:
             out_planes = dx_planes = False
         ws = {"w_split": w_split} if w_split is not None else {}
         xp = {"x_planes": x_planes} if x_planes is not None else {}
@@ -505,7 +504,7 @@ class _Linear(torch.autograd.Function):
         ctx.mask_dy, ctx.gate_input, ctx.has_res = mask_dy, gate_input, residual is not None
         ctx.drop_p, ctx.premasked, ctx.gate_scale = drop_p, premasked, gate_scale
         ctx.native, ctx.dx_planes, ctx.shape = native, dx_planes, shp
-        ctx.drop_planes = bool(OPTIONS.tfm_planes & 4)
+        ctx.drop_planes = bool(OPTIONS.tfm_planes)
         ctx.sgd = sgd if (native and gw is not None) else None  # (the plane weight gradient may step W)
         yo = y.view(*shp[:-1], y.shape[-1])
         if yp is not None:
@@ -544,7 +543,7 @@ class _Linear(torch.autograd.Function):
             if ctx.native and ctx.drop_planes:
                 # (the bias gradient comes from the dropout pass's column sums: dY is written
                 # only as planes, and no separate column-sum pass reads it)
-                cs = ctx.gb is not None and ctx.gw is not None and Fo % 2 == 0 and OPTIONS.dropout_colsum
+                cs = ctx.gb is not None and ctx.gw is not None and Fo % 2 == 0
                 # planes only when both GEMMs that read dY take the plane path (else they read fp32 dY)
                 pl_only = (ctx.x_planes is not None and be.planes_ok(Fo, Fi) and Fo % 8 == 0
                            and ctx.ws.get("w_split") is not None)
@@ -704,7 +703,6 @@ class _BN(torch.autograd.Function):
         ctx.bnb = bnb
         ctx.planes_on = OPTIONS.planes  # (the backward's dX-planes decision follows the forward's)
         ctx.bwd_in_wgrad = OPTIONS.bn_bwd_in_wgrad
-        ctx.residual_mask = OPTIONS.residual_mask
         yo = y.reshape(x.shape)
         if yp is not None:
             _tag_planes(yo, yp.view((K, 2) + tuple(x.shape[1:])), planes >= 2)
@@ -744,7 +742,7 @@ class _BN(torch.autograd.Function):
             # identity shortcut (ResidualLink): its gradient dy·relu' goes to the block's first conv
             # as factors (MaskedGrad) — the backward writes no dpre tensor
             masked = (ctx.has_res and ctx.link is not None and ctx.relu and ctx.relu_mask is not None
-                      and ctx.residual_mask and C % 8 == 0)
+                      and C % 8 == 0)
             if (dxm == 2 and ctx.bwd_in_wgrad and not (ctx.has_res and not masked) and C % 64 == 0
                     and (ctx.relu_mask is not None or not ctx.relu) and x3.is_contiguous()):
                 # coefficients only: the producing conv's halo weight gradient applies them in its
@@ -801,7 +799,7 @@ class _LN(torch.autograd.Function):
     def forward(ctx, x, token, gamma, beta, ggamma, gbeta, planes=False):
         be = _be(x)
         yp = None
-        if (planes and OPTIONS.planes and OPTIONS.ln_planes and be is not ref and x.dtype == torch.float32
+        if (planes and OPTIONS.planes and be is not ref and x.dtype == torch.float32
                 and be.planes_fit(x[0].numel())):
             y, mean, rstd, yp = be.ln_fwd(x, gamma, beta, planes=True)
         else:
@@ -979,26 +977,19 @@ class _AttnPacked(torch.autograd.Function):
     MFMA kernels read / write the heads in place (no permute copies either way)."""
 
     @staticmethod
-    def forward(ctx, qkv, key_valid, H, drop_p=0.0, drop_seeds=None, planes=False):
+    def forward(ctx, qkv, key_valid, H, drop_p=0.0, drop_seeds=None):
         be = _be(qkv)
         K, B, L, D3 = qkv.shape
         D = D3 // 3
         dr = {"drop_p": drop_p, "drop_seeds": drop_seeds} if drop_p else {}
-        planes = bool(planes and be is not ref and qkv.dtype == torch.float32 and OPTIONS.planes)
-        fwd_planes, ctx.planes = planes and bool(OPTIONS.tfm_planes & 2), planes and bool(OPTIONS.tfm_planes & 8)
-        opl = None
         if be is ref:
             t = qkv.reshape(K, B, L, 3, H, D // H).permute(3, 0, 1, 4, 2, 5)
             o, lse = ref.attn_fwd(t[0], t[1], t[2], key_valid, **dr)
             o = o.permute(0, 1, 3, 2, 4).reshape(K, B, L, D)
-        elif fwd_planes:
-            o, lse, opl = be.attn_fwd_packed(qkv, H, key_valid, out_planes=True, **dr)
         else:
             o, lse = be.attn_fwd_packed(qkv, H, key_valid, **dr)
         ctx.save_for_backward(qkv, o, lse)
         ctx.key_valid, ctx.H, ctx.dr = key_valid, H, dr
-        if opl is not None:
-            _tag_planes(o, opl, False)
         return o
 
     @staticmethod
@@ -1014,18 +1005,14 @@ class _AttnPacked(torch.autograd.Function):
             dop = do.reshape(K, B, L, H, D // H).permute(0, 1, 3, 2, 4)
             dq, dk, dv = ref.attn_bwd(dop, t[0], t[1], t[2], op, lse, ctx.key_valid, **ctx.dr)
             dqkv = torch.stack([dq, dk, dv]).permute(1, 2, 4, 0, 3, 5).reshape(K, B, L, D3)
-        elif ctx.planes:
-            dqkv, gpl = be.attn_bwd_packed(do.contiguous(), qkv, o, lse, H, ctx.key_valid, out_planes=True, **ctx.dr)
-            _tag_planes(dqkv, gpl, False)
         else:
             dqkv = be.attn_bwd_packed(do.contiguous(), qkv, o, lse, H, ctx.key_valid, **ctx.dr)
-        return dqkv, None, None, None, None, None
+        return dqkv, None, None, None, None
 
 
-def attention_packed(qkv, key_valid, H: int, drop_p: float = 0.0, drop_seeds=None, planes: bool = False):
-    """`planes` (fp32 native): o and, in the backward, dqkv also carry their split planes for the
-    projections' plane GEMMs (out_proj forward / weight gradient; QKV dgrad / weight gradient)."""
-    return _AttnPacked.apply(qkv, key_valid, H, drop_p, drop_seeds, planes)
+def attention_packed(qkv, key_valid, H: int, drop_p: float = 0.0, drop_seeds=None):
+    """Attention over the QKV projection's packed rows (no permute copies; MFMA kernels)."""
+    return _AttnPacked.apply(qkv, key_valid, H, drop_p, drop_seeds)
 
 
 def packed_attention_ok(t: torch.Tensor, L: int, DH: int) -> bool:

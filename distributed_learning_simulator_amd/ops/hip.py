@@ -136,26 +136,6 @@ def _workspace(numel: int, device) -> torch.Tensor:
     return _grown(_ws_cache, key, numel, device)
 
 
-_ctr_cache: dict = {}
-# OPTIONS.bn_fused_coef: fused BN coefficients (csrc/norm.hip, last-arriver stage) instead of the
-# separate coefficient kernel. Off by default: measured SLOWER on MI355X — every workgroup's
-# agent-scope release (buffer_wbl2) writes back its XCD's dirty L2 lines: FedAvg ResNet-18 round
-# 2.45 -> 2.91 s at 100 clients, 462 -> 529 ms at the 8-rank per-rank load
-
-
-def _bn_counters(K: int, device):
-    """Per-(device, stream) zeroed ticket counters of the fused BN coefficient stage; every
-    launch leaves them zero again. Sized once, generously, so graph capture never allocates."""
-    if not OPTIONS.bn_fused_coef:
-        return None
-    key = (device, torch.cuda.current_stream().cuda_stream)
-    t = _ctr_cache.get(key)
-    if t is None or t.numel() < K:
-        t = torch.zeros(max(K, 1 << 14), dtype=torch.int32, device=device)
-        _ctr_cache[key] = t
-    return t
-
-
 # ----------------------------------------------------------------------------- conv
 # NT-GEMM tile configuration: -1 = per-shape heuristic (csrc/conv_nt.hip); the kernel
 # microbenchmark (bench/kernel_bench.py) sets explicit variant ids to sweep them.
@@ -772,7 +752,7 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
         mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
     assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
-              eps, rep, _p(ws), _p(mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx, _p(pre_stats),
+              eps, rep, _p(ws), _p(mask), _f32(x), _s(), ldx, _p(pre_stats),
               0 if pre_stats is None else pre_stats.shape[1], _p(yp), int(planes != 2), NULL, 1)
     out = (y, mean, rstd, mask) if with_mask else (y, mean, rstd)
     return out + (yp,) if planes else out
@@ -796,7 +776,7 @@ def bn_coef(x, gamma, beta, valid_rows=None, eps=1e-5, pre_stats=None):
         assert pre_stats.dtype == torch.float32 and pre_stats.is_contiguous()
         assert pre_stats.shape[0] == K and pre_stats.shape[2:] == (2, C), pre_stats.shape
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), NULL, NULL, _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, 0, eps, rep, _p(ws),
-              NULL, _p(_bn_counters(K, x.device)), 1, _s(), ldx, _p(pre_stats),
+              NULL, 1, _s(), ldx, _p(pre_stats),
               0 if pre_stats is None else pre_stats.shape[1], NULL, 1, _p(coef), 0)
     return coef, mean, rstd
 
@@ -1101,7 +1081,7 @@ def bn_bwd(dy, x, y, mean, rstd, gamma, valid_rows, relu, ggamma, gbeta, need_dp
         assert coef_out.shape == (K, C, 3) and coef_out.dtype == F32 and coef_out.is_contiguous()
         assert dx_out is None and not need_dpre
     _C.bn_bwd(_p(dy), _p(x), _p(y), _p(mean), _p(rstd), _p(gamma), _p(vr), g_cs, K, R, C, int(relu), _p(dx), _p(dpre),
-              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _p(_bn_counters(K, x.device)), _f32(x), _s(), ldx,
+              _p(ggamma), _p(gbeta), dg_cs, _p(ws), _p(relu_mask), _f32(x), _s(), ldx,
               int(dx_out is not None), _p(dxp), int(dx_planes != 2), _p(pre_part),
               0 if pre_part is None else pre_part.shape[1], _p(coef_out), 1 if coef_out is not None else 0)
     if coef_out is not None:
@@ -1121,7 +1101,7 @@ def bn_bwd_apply_planes(dy, x, relu_mask, coef, valid_rows, dxp) -> None:
     ws = _workspace(_C.bn_workspace_floats(K, R, C), x.device)
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
     _C.bn_bwd(_p(dy), _p(x), NULL, NULL, NULL, NULL, _p(vr), 0, K, R, C, int(relu_mask is not None), _p(dxp), NULL,
-              NULL, NULL, 0, _p(ws), _p(relu_mask), NULL, 1, _s(), C, 0, _p(dxp), 0, NULL, 0, _p(coef), 2)
+              NULL, NULL, 0, _p(ws), _p(relu_mask), 1, _s(), C, 0, _p(dxp), 0, NULL, 0, _p(coef), 2)
 
 
 # ------------------------------------------------------------------------ layernorm
@@ -1324,7 +1304,7 @@ def attn_fwd(q, k, v, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     lse = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
     sp, dp_ = _attn_drop(drop_p, drop_seeds, q.shape[0], q)
     ok = _C.attn_fwd(_p(q), _p(k), _p(v), _p(kv), _p(o), _p(lse), KBH, H, L, DH, _f32(q), _s(), 0, 0, sp,
-                     KBH // q.shape[0], dp_, NULL, 0)
+                     KBH // q.shape[0], dp_)
     if not ok:
         raise NotImplementedError(f"attention kernel: L={L} dh={DH} drop_p={drop_p} not supported")
     return o, lse
@@ -1338,7 +1318,7 @@ def attn_bwd(do, q, k, v, o, lse, key_valid=None, drop_p: float = 0.0, drop_seed
     delta = torch.empty(q.shape[:-1], dtype=torch.float32, device=q.device)
     sp, dp_ = _attn_drop(drop_p, drop_seeds, q.shape[0], q)
     ok = _C.attn_bwd(_p(do), _p(q), _p(k), _p(v), _p(o), _p(lse.contiguous()), _p(kv), _p(dq), _p(dk), _p(dv),
-                     _p(delta), KBH, H, L, DH, _f32(q), _s(), 0, 0, sp, KBH // q.shape[0], dp_, NULL, NULL, NULL, 0)
+                     _p(delta), KBH, H, L, DH, _f32(q), _s(), 0, 0, sp, KBH // q.shape[0], dp_)
     if not ok:
         raise NotImplementedError(f"attention kernel: L={L} dh={DH} drop_p={drop_p} not supported")
     return dq, dk, dv
@@ -1348,11 +1328,10 @@ def attn_packed_supported(L: int, DH: int) -> bool:
     return bool(_C.attn_packed_supported(L, DH))
 
 
-def attn_fwd_packed(qkv, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds=None, out_planes: bool = False):
+def attn_fwd_packed(qkv, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
     """Attention straight from the QKV projection's output rows qkv [K, B, L, 3·D] (q | k | v
     column blocks, heads of dh = D/H inside each): returns o [K, B, L, D] — the out projection's
-    input layout — and lse [K, B, H, L]. No permute / contiguous copies. `out_planes` (fp32):
-    the kernel also writes o's split planes [K, 2, B, L, D], returned third."""
+    input layout — and lse [K, B, H, L]. No permute / contiguous copies."""
     K, B, L, D3 = qkv.shape
     D = D3 // 3
     DH = D // H
@@ -1364,17 +1343,14 @@ def attn_fwd_packed(qkv, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds
     base = _p(qkv)
     es = qkv.element_size()
     sp, dp_ = _attn_drop(drop_p, drop_seeds, K, qkv)
-    opl = torch.empty((K, 2, B, L, D), dtype=BF16, device=qkv.device) if (out_planes and _f32(qkv)) else None
     ok = _C.attn_fwd(base, base + D * es, base + 2 * D * es, _p(kv), _p(o), _p(lse), K * B * H, H, L, DH,
-                     _f32(qkv), _s(), D3, D, sp, B * H, dp_, _p(opl), B * L * D)
+                     _f32(qkv), _s(), D3, D, sp, B * H, dp_)
     assert ok
-    return (o, lse, opl) if out_planes else (o, lse)
+    return o, lse
 
 
-def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds=None,
-                    out_planes: bool = False):
-    """dqkv [K, B, L, 3·D] (the QKV projection's gradient layout) from do / o [K, B, L, D].
-    `out_planes` (fp32): also dqkv's split planes [K, 2, B, L, 3·D] (returns (dqkv, planes))."""
+def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None, drop_p: float = 0.0, drop_seeds=None):
+    """dqkv [K, B, L, 3·D] (the QKV projection's gradient layout) from do / o [K, B, L, D]."""
     K, B, L, D3 = qkv.shape
     D = D3 // 3
     DH = D // H
@@ -1384,14 +1360,10 @@ def attn_bwd_packed(do, qkv, o, lse, H: int, key_valid=None, drop_p: float = 0.0
     delta = torch.empty((K, B, H, L), dtype=torch.float32, device=qkv.device)
     b, g, es = _p(qkv), _p(dqkv), qkv.element_size()
     sp, dp_ = _attn_drop(drop_p, drop_seeds, K, qkv)
-    gpl = torch.empty((K, 2, B, L, D3), dtype=BF16, device=qkv.device) if (out_planes and _f32(qkv)) else None
-    gp = _p(gpl)
-    pe = 2 if gpl is not None else 0  # (bytes per plane element)
     ok = _C.attn_bwd(_p(do), b, b + D * es, b + 2 * D * es, _p(o), _p(lse.contiguous()), _p(kv), g, g + D * es,
-                     g + 2 * D * es, _p(delta), K * B * H, H, L, DH, _f32(qkv), _s(), D3, D, sp, B * H, dp_,
-                     gp, gp + D * pe if gp else NULL, gp + 2 * D * pe if gp else NULL, B * L * D3)
+                     g + 2 * D * es, _p(delta), K * B * H, H, L, DH, _f32(qkv), _s(), D3, D, sp, B * H, dp_)
     assert ok
-    return (dqkv, gpl) if out_planes else dqkv
+    return dqkv
 
 
 # -------------------------------------------------------------- synthetic data

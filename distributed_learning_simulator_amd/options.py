@@ -40,29 +40,15 @@ class RuntimeOptions:
     planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_PLANES", True))
     """BatchNorms emit bf16 (hi, lo) planes for the LDS-DMA plane / halo GEMMs (off: every conv
     splits its operand in registers)."""
-    ln_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_LN_PLANES", True))
-    """LayerNorm outputs carry planes for the Transformer's plane linears."""
     fused_sgd: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_FUSED_SGD", True))
     """SGD steps of the weights whose plane / halo wgrad kernels can apply them (csrc/sgd_epi.h)
     run in those kernels; the flat step covers the rest (engine.params.FusedSGD)."""
-    linear_res_link: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_LINEAR_RES_LINK", True))
-    """Transformer residual inputs: the residual add's gradient goes to the other reader's dgrad
-    epilogue (Fn.linear res_link / acc_link) instead of an autograd add pass."""
-    tfm_planes: int = dataclasses.field(default_factory=lambda: _env_int("DLS_TFM_PLANES", 5))
-    """Transformer split-plane producers (bit mask): 1 = the FFN hidden activation and its
-    gradient (linear1 / linear2 epilogues), 2 = the attention output (forward kernel), 4 = the
-    dropout backward of the residual-branch linears (out_proj / linear2), 8 = dqkv (attention
-    backward kernels). Default 5: the attention planes (2, 8) measured +0.4-0.5 s per FedOBD
-    stage-1 round each (their plane stores cost more than the plane GEMMs gain at d 512,
-    profiles/r5_c6_ab_tfm_planes.txt)."""
-    dropout_colsum: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DROPOUT_COLSUM", True))
-    """The dropout backward of out_proj / linear2 also writes the column sums of its output (their
-    bias gradients) and then writes dY only as planes (off: fp32 dY + planes, and a column-sum pass)."""
-    block_out_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BLOCK_OUT_PLANES", True))
-    """ResNet block outputs written only in the forms their readers take (off: fp32 + planes)."""
+    tfm_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_TFM_PLANES", True))
+    """Transformer split-plane producers: the FFN hidden activation and its gradient (linear1 /
+    linear2 epilogues) and the dropout backward of the residual-branch linears (out_proj /
+    linear2) write planes for the plane GEMMs (off: fp32 only). (Attention outputs writing planes
+    measured +0.4-0.5 s per FedOBD stage-1 round each, profiles/r5_c6_ab_tfm_planes.txt: removed.)"""
     # --- BatchNorm fusions
-    bn_epilogue_stats: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_EPILOGUE_STATS", True))
-    """BN forward statistics from the producing conv's epilogue (off: BN's own statistics pass)."""
     bn_bwd_parts: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_BWD_PARTS", True))
     """BN backward partial sums from the consuming conv's dgrad epilogue (off: own reduction)."""
     bn_fused_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_HALO", True))
@@ -74,22 +60,11 @@ class RuntimeOptions:
     halo_wgrad: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_HALO_WGRAD", True))
     """3x3 stride-1 weight gradients of 64-512-channel convs (ResNet layers 1-3) on the LDS-halo
     kernel (csrc/conv_halo_wgrad.hip; off: the implicit-GEMM TN kernel)."""
-    halo_wgrad_bn: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_HALO_WGRAD_BN", True))
-    """With halo_wgrad: a conv whose BN(+ReLU) input is applied in its forward halo loader
-    (bn_fused_halo) also applies it in its weight gradient's loader from the raw tensor, so training
-    never writes that BN's normalised planes (off: the fused forward writes them for the wgrad)."""
     bn_bwd_in_wgrad: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_BWD_IN_WGRAD", True))
     """A training BN(+ReLU) whose input gradient feeds only a 3x3 stride-1 conv's backward (ResNet
     BasicBlock bn1 / identity-block bn2, layers 1-3) computes its coefficients only: that conv's halo
     weight gradient applies the BN backward in its dY loader and writes dX's planes for the dgrad
     (ops.functional DeferredBNBwd; off: the BN backward's own apply pass writes them)."""
-    dgrad_wt: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DGRAD_WT", True))
-    """3x3 stride-1 plane dgrads run the forward tiles on transposed, flipped weight planes (built
-    per launch; off: the k-major weight tiles)."""
-    residual_mask: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_RESIDUAL_MASK", True))
-    """A ResNet identity shortcut's gradient (dy·relu' of the block output) is read by the first
-    conv's dgrad epilogue from the output gradient and the ReLU bits, instead of being written
-    by the BatchNorm backward and read back (off: the BN backward writes it)."""
     dense_wgrad_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_WGRAD_HALO", True))
     """DenseNet growth-conv weight gradients on the LDS-halo kernel (the normalised prefix staged
     once per pixel tile for all nine taps; off: the implicit-GEMM TN kernel)."""
@@ -105,8 +80,6 @@ class RuntimeOptions:
     """DenseNet blocks (fused growth convs) sum each channel's statistics once, from the producing
     conv's epilogue, into running fp64 sums the BN coefficients read (off: a statistics pass over
     the prefix per layer)."""
-    bn_fused_coef: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_COEF", False))
-    """BN coefficients in a last-arriver stage of the statistics kernel (measured slower: off)."""
     # --- reductions
     deterministic: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DETERMINISTIC", True))
     """Split-K weight gradients and column sums folded in a fixed order (off: fp32 atomics)."""
@@ -137,7 +110,7 @@ class RuntimeOptions:
     3.51 vs 3.18 s per vote step)."""
     # --- native launch knobs (csrc/, forwarded to the extension; None = the kernel's own default)
     native: dict = dataclasses.field(default_factory=dict)
-    """e.g. {"tn_kref": 8, "pl_min_wg": 0, "conv_gl": 0, "f32_smallk": 1, "attn_mfma": 0}."""
+    """e.g. {"pl_min_wg": 0, "conv_gl": 0, "attn_mfma": 0, "halo_wgrad_unroll": 2}."""
 
 
 OPTIONS = RuntimeOptions()

@@ -22,16 +22,16 @@ def test_session_applies_runtime_options(tmp_path):
     """A run's `runtime_options:` mapping reaches the engine (trainer stream count) while the session
     builds and runs, and does not leak into the process afterwards (options scoped to the
     run)."""
-    before = options.OPTIONS.streams, options.OPTIONS.block_out_planes
+    before = options.OPTIONS.streams, options.OPTIONS.ragged_steps
     cfg = config_from_dict({"distributed_algorithm": "fed_avg", "dataset_name": "MNIST", "model_name": "LeNet5",
                             "worker_number": 2, "round": 1, "epoch": 1, "dataset_kwargs": {"scale": 0.01},
                             "save_dir": str(tmp_path), "log_level": "WARNING",
-                            "runtime_options": {"streams": 3, "block_out_planes": False}})
+                            "runtime_options": {"streams": 3, "ragged_steps": False}})
     sess = Session(cfg, comm=Comm())
     assert sess.trainer.num_streams == 3
-    assert (options.OPTIONS.streams, options.OPTIONS.block_out_planes) == before
+    assert (options.OPTIONS.streams, options.OPTIONS.ragged_steps) == before
     sess.run()
-    assert (options.OPTIONS.streams, options.OPTIONS.block_out_planes) == before
+    assert (options.OPTIONS.streams, options.OPTIONS.ragged_steps) == before
 
 
 def test_scoped_options_refuse_conflicting_concurrent_runs():

@@ -3,6 +3,7 @@ epoch's last steps the clients that still have a batch form a row prefix, and th
 only that prefix. Every client trains exactly the same batches either way, so the round's result
 equals the full-cohort run (up to the fp64 aggregation order)."""
 
+import pytest
 import torch
 
 from distributed_learning_simulator_amd import options
@@ -62,3 +63,45 @@ def test_schedule_active_prefix():
     assert sch.steps == 3 and sch.active_rows == [3, 2, 1]
     sch = tr.build_schedule([torch.arange(3), torch.arange(10)], epochs=1, seed=0)
     assert sch.active_rows == [2, 2, 2]  # (rows 1 active alone: not a prefix)
+
+
+@pytest.mark.gpu
+def test_ragged_step_graphs_bounded_gpu(tmp_path):
+    """Graph-replayed ragged steps (the image models' HIP-graph path) with strongly uneven
+    Dirichlet shards: more distinct ragged row counts per epoch than the graph budget holds. The
+    full cohort's graph is never evicted for a ragged one; once the budget is full, a new ragged
+    count runs on this round's smallest graph with more rows (extra rows masked) — so the cache
+    never exceeds max_graphs — and the round equals the full-cohort run (ragged_steps off)."""
+    assert torch.cuda.is_available()
+    from distributed_learning_simulator_amd.parallel.comm import init_distributed
+
+    assert init_distributed().device.type == "cuda"
+    cfg = dict(CFG, dataset_sampling="dirichlet_non_iid", dataset_sampling_kwargs={"alpha": 0.3}, worker_number=8,
+               round=2, epoch=2, batch_size=8, dataset_kwargs={"scale": 0.03})
+    fallbacks = []
+    orig = CohortTrainer._step_graph
+
+    def spy(self, n, parts, full=True, keep=()):
+        sg = orig(self, n, parts, full=full, keep=keep)
+        if sg is None:
+            fallbacks.append(n)
+        assert len(self._graphs) <= max(self.max_graphs, 1)
+        return sg
+
+    out = {}
+    for ragged in (True, False):
+        CohortTrainer._step_graph = spy
+        try:
+            with options.override(ragged_steps=ragged, graphs=True, max_graphs=3):
+                sess = Session(config_from_dict(dict(cfg, save_dir=str(tmp_path / str(ragged)))),
+                               comm=Comm(device=torch.device("cuda")))
+                assert sess.trainer._graphs_enabled()
+                res = sess.run()
+        finally:
+            CohortTrainer._step_graph = orig
+        out[ragged] = (sess.server.global_parameter.clone(), res)
+    assert fallbacks, "the uneven shards must overflow the ragged graph budget"
+    (g_on, r_on), (g_off, r_off) = out[True], out[False]
+    assert torch.allclose(g_on, g_off, rtol=1e-5, atol=1e-6), (g_on - g_off).abs().max()
+    for k in r_off["performance"]:
+        assert abs(r_on["performance"][k]["test_loss"] - r_off["performance"][k]["test_loss"]) < 1e-4
