@@ -134,8 +134,11 @@ __device__ __forceinline__ long hbase(const HeadLayout& hl, long head, int H) {
   return (head / H) * hl.s_kb + (head % H) * hl.s_h;
 }
 
-// stage rows [r0, r0+RB) of a head matrix (row stride ld, DH real columns) into an image of DP
-// padded columns (zero rows past L, zero columns past DH)
+// Staging rows [r0, r0+RB) of a head matrix (row stride ld, DH real columns) into an image of DP
+// padded columns (zero rows past L, zero columns past DH): `stage` in one go, or split in two so a
+// block's global loads can be issued into registers while the previous block's MFMAs run (DP ≤ 64:
+// one 8-column chunk per thread at most): stage_load fills the thread's chunk, stage_store splits
+// it into the image.
 template <typename T, int DH, int DP>
 __device__ __forceinline__ void stage(const T* __restrict__ src, int ld, int r0, int L, const Img<T>& m) {
   for (int c = threadIdx.x; c < RB * DP / 8; c += WG) {
@@ -143,6 +146,36 @@ __device__ __forceinline__ void stage(const T* __restrict__ src, int ld, int r0,
     const int n = r0 + r < L ? min(8, max(0, DH - d)) : 0;
     float x[8];
     load8n(src + (long)(r0 + r) * ld + d, n, x);
+    union {
+      uint4 v;
+      bf16_t e[8];
+    } hh, ll;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (sizeof(T) == 4)
+        split2(x[i], hh.e[i], ll.e[i]);
+      else
+        hh.e[i] = f2bf(x[i]);  // exact: x came from bf16
+    }
+    *reinterpret_cast<uint4*>(m.p + r * m.ld + d) = hh.v;
+    if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(m.p + m.ps + r * m.ld + d) = ll.v;
+  }
+}
+template <typename T, int DH, int DP>
+__device__ __forceinline__ void stage_load(const T* __restrict__ src, int ld, int r0, int L, float (&x)[8]) {
+  static_assert(RB * DP / 8 <= WG, "one chunk per thread");
+  const int c = threadIdx.x;
+  if (c < RB * DP / 8) {
+    const int r = c / (DP / 8), d = (c % (DP / 8)) * 8;
+    const int n = r0 + r < L ? min(8, max(0, DH - d)) : 0;
+    load8n(src + (long)(r0 + r) * ld + d, n, x);
+  }
+}
+template <typename T, int DP>
+__device__ __forceinline__ void stage_store(const float (&x)[8], const Img<T>& m) {
+  const int c = threadIdx.x;
+  if (c < RB * DP / 8) {
+    const int r = c / (DP / 8), d = (c % (DP / 8)) * 8;
     union {
       uint4 v;
       bf16_t e[8];
@@ -248,6 +281,7 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
 #pragma unroll
   for (int t = 0; t < DP / 32; ++t) ot[t] = f32x16{};
   float m = -INFINITY, l = 0.f;
+  // (no register prefetch of the next block here: it costs this kernel a wave per SIMD, 3 → 2)
   for (int k0 = 0; k0 < nk; k0 += RB) {
     stage<T, DH, DP>(k + base, lq.ld, k0, nk, KI);
     stage<T, DH, DP>(v + base, lq.ld, k0, nk, VI);
@@ -342,10 +376,19 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
   f32x16 dqt[DP / 32];
 #pragma unroll
   for (int t = 0; t < DP / 32; ++t) dqt[t] = f32x16{};
+  float kx[8], vx[8];
+  if (nk > 0) {
+    stage_load<T, DH, DP>(k + base, lq.ld, 0, nk, kx);
+    stage_load<T, DH, DP>(v + base, lq.ld, 0, nk, vx);
+  }
   for (int k0 = 0; k0 < nk; k0 += RB) {
-    stage<T, DH, DP>(k + base, lq.ld, k0, nk, KI);
-    stage<T, DH, DP>(v + base, lq.ld, k0, nk, VI);
+    stage_store<T, DP>(kx, KI);
+    stage_store<T, DP>(vx, VI);
     __syncthreads();
+    if (k0 + RB < nk) {
+      stage_load<T, DH, DP>(k + base, lq.ld, k0 + RB, nk, kx);
+      stage_load<T, DH, DP>(v + base, lq.ld, k0 + RB, nk, vx);
+    }
     f32x16 st = f32x16{}, dpt = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < DP / 16; ++ks) {
@@ -415,15 +458,28 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   // a workgroup whose keys are all padding still writes their zero gradients (no early exit:
   // every wave must reach every barrier)
   const bool any = blockIdx.y * (4 * RB) < nk;
-  for (int q0 = 0; any && q0 < L; q0 += RB) {
-    stage<T, DH, DP>(q + base, lq.ld, q0, L, QI);
-    stage<T, DH, DP>(dout + obase, lo.ld, q0, L, OI);
+  // (the next query block's Q / dO rows, lse and δ are loaded into registers under this block's
+  // MFMAs: the staging's global-load latency leaves the loop's critical path)
+  float qx[8], ox[8], lq_r = 0.f, dq_r = 0.f;
+  auto load_qblock = [&](int q0) {
+    stage_load<T, DH, DP>(q + base, lq.ld, q0, L, qx);
+    stage_load<T, DH, DP>(dout + obase, lo.ld, q0, L, ox);
     if (threadIdx.x < RB) {
       const bool ok = q0 + threadIdx.x < L;
-      Lq[threadIdx.x] = ok ? lse[head * L + q0 + threadIdx.x] : 0.f;
-      Dq[threadIdx.x] = ok ? delta[head * L + q0 + threadIdx.x] : 0.f;
+      lq_r = ok ? lse[head * L + q0 + threadIdx.x] : 0.f;
+      dq_r = ok ? delta[head * L + q0 + threadIdx.x] : 0.f;
+    }
+  };
+  if (any) load_qblock(0);
+  for (int q0 = 0; any && q0 < L; q0 += RB) {
+    stage_store<T, DP>(qx, QI);
+    stage_store<T, DP>(ox, OI);
+    if (threadIdx.x < RB) {
+      Lq[threadIdx.x] = lq_r;
+      Dq[threadIdx.x] = dq_r;
     }
     __syncthreads();
+    if (q0 + RB < L) load_qblock(q0 + RB);
     f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < DP / 16; ++ks) {
