@@ -442,15 +442,15 @@ conv_halo_kernel(ConvNTParams p) {
   nt_f32_epilogue<TM, TN, NW, (TM * TN <= 2 ? 2 : -1), false>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
 }
 
-template <int IMG, int TH, int TW, int BN, int WM, int WN, int HB, int NBS, int TPS = 1>
+template <int IMG, int TH, int TW, int BN, int WM, int WN, int HB, int NBS, int TPS = 1, int MINW = 1>
 void launch_halo(const ConvNTParams& p, int K, hipStream_t s) {
   const int tilesM = IMG == 1 ? p.B * (p.OH / TH) : p.B / IMG;
   const int grid = K * tilesM * cdiv(p.N, BN);
   if (p.b_kmajor)
-    hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, true, 1, HB, NBS, 0, TPS>), dim3(grid),
+    hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, true, MINW, HB, NBS, 0, TPS>), dim3(grid),
                        dim3(WM * WN * 64), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, false, 1, HB, NBS, 0, TPS>), dim3(grid),
+    hipLaunchKernelGGL((conv_halo_kernel<IMG, TH, TW, BN, WM, WN, false, MINW, HB, NBS, 0, TPS>), dim3(grid),
                        dim3(WM * WN * 64), 0, s, p);
 }
 
@@ -530,6 +530,9 @@ bool conv_halo(const ConvNTParams& p, int K, hipStream_t s) {
     }
     return true;
   }
+  // (measured at 32² / 64 channels and removed: 16 waves with two halo buffers, one workgroup per
+  // CU, +42 % forward; 4-row blocks with three workgroups per CU, +15 %,
+  // profiles/r6_c9_halo_l1_variant5_rejected.log)
   const int v = g_halo_variant >= 0 ? g_halo_variant : (cfg == 2 ? 2 : 1);
   if (cfg > 3) return false;
   if (cfg == 0 && (v == 1 || v == 3)) {  // 32² / 64 channels: two taps per step
