@@ -50,7 +50,15 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int BM, int BN, int WM, int WN, bool BKM, int NST, int MINW, bool ILV, int PKT>
+// conv_nt_pl_kernel<…, PIX>: pixel-major GEMM rows (ConvNTParams::pix). Row m is image m % B at
+// pixel m / B, so a tile covers a few pixels of every image and each 32-row group (B % 32 == 0)
+// one pixel. The K walk visits only the box of taps that lands inside the image for some row of
+// the tile, and each wave skips the MFMAs (and A fragment reads) of its groups whose pixels the
+// stage's tap misses. A skipped tap's rows are all out of the image, i.e. zeros: the sums are the
+// ones the full walk forms, term for term. On 4x4 images with 3x3 taps the walk keeps 30 of 36
+// taps per 256-row tile at B = 64 (every tap of a one-pixel tile past B = 256) and the MFMAs 100
+// of 144.
+template <int BM, int BN, int WM, int WN, bool BKM, int NST, int MINW, bool ILV, int PKT, bool PIX = false>
 __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTParams p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -77,7 +85,16 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int client = bid / per_client;
   const int t = bid - client * per_client;
-  const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BN;
+  int mt = t / tilesN;
+  if constexpr (PIX) {
+    // one-pixel tiles (B % BM == 0): the tiles of every pixel of one image chunk are consecutive, so
+    // they run together on one XCD and the input rows their taps share are read from its L2
+    if (p.B % BM == 0) {
+      const int npix = p.OH * p.OW;
+      mt = (mt % npix) * (p.B / BM) + mt / npix;
+    }
+  }
+  const int m0 = mt * BM, n0 = (t % tilesN) * BN;
 
   // ---- operand windows (hi plane .. end of lo plane) as buffer resources
   const long a_img = (long)p.B * p.H * p.W * p.ldx;  // elements of one plane of a client's image
@@ -95,10 +112,18 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
   for (int i = 0; i < AI; ++i) {
     const int m = m0 + (i * NW + wid) * RI + lane / CR;
     if (m < p.M) {
-      const uint32_t b = fdiv((uint32_t)m, p.fd_ohw);
-      const uint32_t rem = (uint32_t)m - b * (uint32_t)(p.OH * p.OW);
-      const uint32_t oh = fdiv(rem, p.fd_ow);
-      const uint32_t ow = rem - oh * (uint32_t)p.OW;
+      uint32_t b, oh, ow;
+      if constexpr (PIX) {
+        const uint32_t px = fdiv((uint32_t)m, p.fd_pb);
+        b = (uint32_t)m - px * (uint32_t)p.B;
+        oh = fdiv(px, p.fd_ow);
+        ow = px - oh * (uint32_t)p.OW;
+      } else {
+        b = fdiv((uint32_t)m, p.fd_ohw);
+        const uint32_t rem = (uint32_t)m - b * (uint32_t)(p.OH * p.OW);
+        oh = fdiv(rem, p.fd_ow);
+        ow = rem - oh * (uint32_t)p.OW;
+      }
       a_ih[i] = (int)oh * p.stride - p.pad;
       a_iw[i] = (int)ow * p.stride - p.pad_w;
       a_off[i] = (((int)b * p.H + a_ih[i]) * p.W + a_iw[i]) * p.ldx + lc * 8;
@@ -129,12 +154,29 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
     }
   }
 
+  // PIX: the taps (kh, kw) that land inside the image for some row in rows [r0, r1] form a box
+  // (the rows' pixels are a contiguous run in row-major pixel order); empty when r0 > r1
+  struct TapBox {
+    int h0, h1, w0, w1;
+  };
+  auto tap_box = [&](int r0, int r1) -> TapBox {
+    if (r0 > r1) return TapBox{1, 0, 1, 0};
+    const int p0 = r0 / p.B, p1 = r1 / p.B;
+    const int oh0 = p0 / p.OW, oh1 = p1 / p.OW;
+    const int ow0 = oh0 == oh1 ? p0 - oh0 * p.OW : 0, ow1 = oh0 == oh1 ? p1 - oh1 * p.OW : p.OW - 1;
+    return TapBox{max(0, p.pad - oh1 * p.stride), min(p.KH - 1, p.H - 1 + p.pad - oh0 * p.stride),
+                  max(0, p.pad_w - ow1 * p.stride), min(p.KW - 1, p.W - 1 + p.pad_w - ow0 * p.stride)};
+  };
+  TapBox tb{0, p.KH - 1, 0, p.KW - 1};
+  if constexpr (PIX) tb = tap_box(m0, min(m0 + BM, p.M) - 1);
+
   // K-tile walk: taps (kh, kw) × 32-channel chunks kc of the GEMM's A image (C % 32 == 0).
   // prep() fixes the scalar part of the next stage's source offsets and advances the walk;
   // piece(n, buf) issues that stage's n-th DMA (n < G: A hi / lo per A instruction, then B hi /
   // lo per B instruction). A stage past the last K tile is issued with every lane out of window
   // (zeros into a buffer nobody reads again), so the loop needs no branch around its DMAs.
-  int kc = 0, kh = 0, kw = 0, k_next = 0;
+  // (PIX: the walk covers the tile's tap box only; k_next, the row-major B offset, follows it)
+  int kc = 0, kh = tb.h0, kw = tb.w0, k_next = (tb.h0 * p.KW + tb.w0) * p.C;
   int s_toff = 0, s_boff = 0, s_kh = 0, s_kw = 0;
   bool s_live = false;
   auto prep = [&](bool live) {
@@ -152,9 +194,10 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
     kc += PKT;
     if (kc == p.C) {
       kc = 0;
-      if (++kw == p.KW) {
-        kw = 0;
+      if (++kw > tb.w1) {
+        kw = tb.w0;
         ++kh;
+        if constexpr (PIX) k_next = (kh * p.KW + kw) * p.C;
       }
     }
   };
@@ -187,15 +230,31 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
   // compute(buf, nb): the MFMAs of stage buf; with ILV the next stage's G DMAs (into buffer nb)
   // are spread over the MFMA triples (piece n after triple n·NTRI/G) instead of issued as one
   // burst after the barrier, so the DMA issue overlaps the matrix pipe
+  // PIX: each 32-row group's tap box; the stage being computed is at tap (c_kh, c_kw)
+  TapBox gb[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    gb[i] = TapBox{0, p.KH - 1, 0, p.KW - 1};
+    if constexpr (PIX) gb[i] = tap_box(m0 + wm0 + i * 32, min(m0 + wm0 + i * 32 + 32, p.M) - 1);
+  }
+  int c_kc = 0, c_kh = tb.h0, c_kw = tb.w0;
+  auto group_on = [&](int i) -> bool {
+    if constexpr (!PIX) return true;
+    return c_kh >= gb[i].h0 && c_kh <= gb[i].h1 && c_kw >= gb[i].w0 && c_kw <= gb[i].w1;
+  };
   auto compute = [&](int buf, int nb) {
     const unsigned char* As = smem + buf * STAGE;
     const unsigned char* Bs = As + 2 * A_PL;
+    bool on[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) on[i] = group_on(i);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int ch = ((ks * 2 + h) ^ rsw) * 16;
       bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
+        if (PIX && !on[i]) continue;
         const unsigned char* a = As + (wm0 + i * 32 + (lane & 31)) * (PKT * 2) + ch;
         ah[i] = *reinterpret_cast<const bf16x8*>(a);
         al[i] = *reinterpret_cast<const bf16x8*>(a + A_PL);
@@ -216,13 +275,15 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
         }
       }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        if (PIX && !on[i]) continue;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
           if constexpr (ILV) {
+            static_assert(!ILV || !PIX, "the interleaved DMAs must issue with every triple");
             const int tri = (ks * TM + i) * TN + j;
 #pragma unroll
             for (int n = 0; n < G; ++n)
@@ -233,13 +294,24 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
               }
           }
         }
+      }
+    }
+    if constexpr (PIX) {  // (the computed stage's walk position, one stage behind prep's)
+      c_kc += PKT;
+      if (c_kc == p.C) {
+        c_kc = 0;
+        if (++c_kw > tb.w1) {
+          c_kw = tb.w0;
+          ++c_kh;
+        }
+      }
     }
   };
 
   // ---- main loop: NST-stage LDS ring. Stage kt+NST-1 is issued after the barrier that retires
   // every wave's reads of its buffer (compute(kt-1)); stage kt is waited for by a counted vmcnt
   // that leaves the younger stage in flight (NST = 3)
-  const int nk = p.R / PKT;
+  const int nk = PIX ? (tb.h1 - tb.h0 + 1) * (tb.w1 - tb.w0 + 1) * (p.C / PKT) : p.R / PKT;
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st) {
     prep(st < nk);
@@ -259,17 +331,17 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
   }
   wait_vm<0>();
 
-  nt_f32_epilogue<TM, TN, NW>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
+  nt_f32_epilogue<TM, TN, NW, -1, true, PIX>(p, acc, smem, client, m0, n0, wm0, wn0, wid, lane);
 }
 
-template <int BM, int BN, int WM, int WN, int NST, bool ILV = false, int PKT = 32, int MINW = 1>
+template <int BM, int BN, int WM, int WN, int NST, bool ILV = false, int PKT = 32, int MINW = 1, bool PIX = false>
 void launch_pl(const ConvNTParams& p, int K, bool bkm, hipStream_t s) {
   const int grid = K * cdiv(p.M, BM) * cdiv(p.N, BN);
   if (bkm)
-    hipLaunchKernelGGL((conv_nt_pl_kernel<BM, BN, WM, WN, true, NST, MINW, ILV, PKT>), dim3(grid),
+    hipLaunchKernelGGL((conv_nt_pl_kernel<BM, BN, WM, WN, true, NST, MINW, ILV, PKT, PIX>), dim3(grid),
                        dim3(WM * WN * 64), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_nt_pl_kernel<BM, BN, WM, WN, false, NST, MINW, ILV, PKT>), dim3(grid),
+    hipLaunchKernelGGL((conv_nt_pl_kernel<BM, BN, WM, WN, false, NST, MINW, ILV, PKT, PIX>), dim3(grid),
                        dim3(WM * WN * 64), 0, s, p);
 }
 
@@ -306,13 +378,33 @@ int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
   return 1;
 }
 
-bool conv_nt_pl(const ConvNTParams& p, int K, int variant, hipStream_t s) {
-  if (!conv_nt_pl_supported(p)) return false;
-  const long ab = (p.x_lo + (long)p.B * p.H * p.W * p.ldx) * 2;
-  const long wb = (p.ws_plane + (p.b_kmajor ? (long)p.C * p.wKH * p.wKW * p.N : (long)p.N * p.R)) * 2;
+// pixel-major rows with tap skipping (conv_nt_pl_kernel PIX) for stride-1 convs on small images,
+// where the image border holds a large share of the tap-pixels: 3x3 on 4x4 (ResNet-18 l4) keeps 100
+// of 144. Measured (bench/pix_bench.py, profiles/r6_c10_pix_bench.log): the 256x256 tile gains on l4
+// (fwd / dgrad 1.03 / 1.06x at 50 clients, eval fwd 1.09x); the 128x128 tile of small cohorts loses
+// (0.87 / 0.94x at 7 clients: a 2-pixel tile's tap box is mostly the full 3x3) and so do the strided
+// forwards (l4a 0.97x, eval 0.91x), which keep the plain walk. Not for the sub-pixel dgrad classes,
+// compact shortcut gradients or dropout (their epilogues index GEMM rows). conv_pix = 0 turns it off
+static bool pix_ok(const ConvNTParams& p, int variant) {
+  return native_option(g_opt_conv_pix, "DLS_CONV_PIX", 1) != 0 && variant == 3 && p.stride == 1 &&
+         p.OH * p.OW <= 64 && p.KH * p.KW > 1 && (p.pad > 0 || p.pad_w > 0) && p.out_s <= 1 && !p.acc_compact &&
+         !(p.drop_p > 0.f) && p.M == p.B * p.OH * p.OW;
+}
+
+bool conv_nt_pl(const ConvNTParams& p0, int K, int variant, hipStream_t s) {
+  if (!conv_nt_pl_supported(p0)) return false;
+  const long ab = (p0.x_lo + (long)p0.B * p0.H * p0.W * p0.ldx) * 2;
+  const long wb = (p0.ws_plane + (p0.b_kmajor ? (long)p0.C * p0.wKH * p0.wKW * p0.N : (long)p0.N * p0.R)) * 2;
   if (ab >= (long)OOB_OFF || wb >= (long)OOB_OFF) return false;
-  if (variant < 0) variant = conv_nt_pl_default_variant(p, K);
-  const bool bkm = p.b_kmajor != 0;
+  if (variant < 0) variant = conv_nt_pl_default_variant(p0, K);
+  const bool bkm = p0.b_kmajor != 0;
+  ConvNTParams p = p0;
+  p.pix = pix_ok(p0, variant) ? 1 : 0;
+  if (p.pix) {
+    p.fd_pb = make_fastdiv((uint32_t)p.B);
+    launch_pl<256, 256, 2, 4, 2, false, 32, 1, true>(p, K, bkm, s);
+    return true;
+  }
   switch (variant) {
     case 0: launch_pl<256, 128, 4, 2, 2>(p, K, bkm, s); break;  // 96 KB, 8 waves
     case 1: launch_pl<128, 128, 2, 2, 2>(p, K, bkm, s); break;  // 64 KB, 2 blocks/CU
@@ -347,7 +439,11 @@ struct KmSwz {  // k-major image of W-element rows: segment key of k-row kr
 // SGD: the direct-store epilogue applies the optimiser step (SgdEpi) instead of storing dW — its
 // own instantiation, so the plain kernels compile as if it did not exist (the merged branch cost
 // the 128x128 tile 96 → 178 VGPRs and +59 % time in the ResNet-50 sign-SGD profile)
-template <int BMc, int BNr, int WM, int WN, int NST, bool ILV, bool SGD = false>
+// PIX (ConvTNParams::pix; C % BNr == 0, so the workgroup's columns share one tap (kh, kw)): the
+// pixel reduction walks K tiles of (output pixel, 32 images) over only the pixels whose tap input
+// lies inside the image — a box — instead of 32 consecutive GEMM rows over every pixel; the
+// deterministic split-K cuts that walk into splitk equal runs
+template <int BMc, int BNr, int WM, int WN, int NST, bool ILV, bool SGD = false, bool PIX = false>
 __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BMc / (WM * 32), TN = BNr / (WN * 32);
@@ -371,8 +467,27 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p)
   const int split = t % p.splitk;
   t /= p.splitk;
   const int co0 = (t / tilesN) * BMc, r0 = (t % tilesN) * BNr;
-  const int mbeg = split * p.m_per_split;
-  const int mend = min(p.M, mbeg + p.m_per_split);
+  const int mbeg = PIX ? 0 : split * p.m_per_split;
+  const int mend = PIX ? p.M : min(p.M, mbeg + p.m_per_split);
+  // PIX walk: this tile's tap, the box of output pixels it lands inside for, nbc 32-image chunks per
+  // pixel, and this split's run [t_beg, t_end) of the nv·nbc K tiles
+  int x_kh = 0, x_kw = 0, x_oh0 = 0, x_ow0 = 0, x_nw = 1, x_nbc = 1, t_beg = 0, t_end = 0;
+  if constexpr (PIX) {
+    const int tap = r0 / p.C;
+    x_kh = tap / p.KW;
+    x_kw = tap - x_kh * p.KW;
+    int oh1 = p.OH - 1, ow1 = p.OW - 1;
+    while (x_oh0 < p.OH && x_oh0 * p.stride - p.pad + x_kh < 0) ++x_oh0;
+    while (oh1 >= 0 && oh1 * p.stride - p.pad + x_kh > p.H - 1) --oh1;
+    while (x_ow0 < p.OW && x_ow0 * p.stride - p.pad + x_kw < 0) ++x_ow0;
+    while (ow1 >= 0 && ow1 * p.stride - p.pad + x_kw > p.W - 1) --ow1;
+    x_nw = max(ow1 - x_ow0 + 1, 1);
+    const int nv = max(oh1 - x_oh0 + 1, 0) * max(ow1 - x_ow0 + 1, 0);
+    x_nbc = (p.B + PK - 1) / PK;
+    const int T = nv * x_nbc, tps = (T + p.splitk - 1) / p.splitk;
+    t_beg = min(T, split * tps);
+    t_end = min(T, t_beg + tps);
+  }
 
   const auto ar = make_rsrc(p.dy + (long)client * p.dy_cs, (uint32_t)((p.dy_lo + (long)p.M * p.ldy) * 2));
   const uint32_t a_lo = (uint32_t)(p.dy_lo * 2);
@@ -386,7 +501,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p)
     const int kr = (i * NW + wid) * RPA + lane / CPA;
     const int co = co0 + ((lane % CPA) ^ (KmSwz<BMc>::f(kr) << 2)) * 8;
     a_kr[i] = co < p.Co ? kr : (1 << 29);  // a column past Co never loads
-    a_off[i] = (mbeg + kr) * p.ldy + co;
+    a_off[i] = PIX ? kr * p.OH * p.OW * p.ldy + co : (mbeg + kr) * p.ldy + co;  // (PIX: image kr of the chunk)
   }
   // ---- B (im2col X) loader: fixed column chunk → fixed (kh, kw, c); pixel walk per k-row
   constexpr int S = PK;  // pixels per K tile
@@ -410,6 +525,10 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p)
       c = rr - kw * p.C;
     }
     b_kr[i] = r < p.R ? kr : (1 << 29);
+    if constexpr (PIX) {  // (image kr of the chunk, channel c; the pixel part is per stage)
+      b_off[i] = kr * p.H * p.W * p.ldx + c;
+      continue;
+    }
     const uint32_t m = mbeg + kr;
     const uint32_t b = fdiv(m, p.fd_ohw);
     const uint32_t rem = m - b * p.OH * p.OW;
@@ -427,7 +546,26 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p)
   int s_m0 = 0;
   int sa_off[AI], sb_off[BI];
   bool sb_ok[BI];
+  // PIX stage state: the scalar offsets of (pixel, first image) in dY and X, the images left
+  int t_j = 0, t_bc = 0, s_pa = 0, s_pb = 0, s_left = 0;
+  if constexpr (PIX) {
+    t_j = t_beg / x_nbc;
+    t_bc = t_beg - t_j * x_nbc;
+  }
   auto prep = [&](bool live) {
+    if constexpr (PIX) {
+      s_live = live;
+      const int jh = t_j / x_nw, oh = x_oh0 + jh, ow = x_ow0 + (t_j - jh * x_nw);
+      const int b0 = t_bc * PK;
+      s_left = p.B - b0;
+      s_pa = (b0 * p.OH * p.OW + oh * p.OW + ow) * p.ldy;
+      s_pb = ((b0 * p.H + oh * p.stride - p.pad + x_kh) * p.W + ow * p.stride - p.pad + x_kw) * p.ldx;
+      if (++t_bc == x_nbc) {
+        t_bc = 0;
+        ++t_j;
+      }
+      return;
+    }
     s_live = live;
     s_m0 = k_rows;
 #pragma unroll
@@ -459,6 +597,20 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p)
   auto piece = [&](int n, int buf) {
     unsigned char* As = smem + buf * STAGE;
     unsigned char* Bs = As + 2 * A_PL;
+    if constexpr (PIX) {
+      if (n < 2 * AI) {
+        const int i = n >> 1;
+        const bool ok = s_live && a_kr[i] < s_left;
+        const uint32_t off = (uint32_t)(a_off[i] + s_pa) * 2u + ((n & 1) ? a_lo : 0u);
+        dma16(ar, As + (n & 1) * A_PL + (i * NW + wid) * 1024, ok ? off : OOB_OFF);
+      } else {
+        const int i = (n - 2 * AI) >> 1;
+        const bool ok = s_live && b_kr[i] < s_left;
+        const uint32_t off = (uint32_t)(b_off[i] + s_pb) * 2u + ((n & 1) ? b_lo : 0u);
+        dma16(br, Bs + (n & 1) * B_PL + (i * NW + wid) * 1024, ok ? off : OOB_OFF);
+      }
+      return;
+    }
     if (n < 2 * AI) {
       const int i = n >> 1;
       const bool ok = s_live && s_m0 + a_kr[i] < mend;
@@ -522,7 +674,7 @@ __global__ void __launch_bounds__(WM* WN * 64) conv_tn_pl_kernel(ConvTNParams p)
     }
   };
 
-  const int nk = (mend - mbeg + PK - 1) / PK;
+  const int nk = PIX ? t_end - t_beg : (mend - mbeg + PK - 1) / PK;
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st) {
     prep(st < nk);
@@ -695,12 +847,24 @@ bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s) {
   const int grid = (int)((long)K * cdiv(p.Co, t.bm) * cdiv(p.R, t.bn) * p.splitk);
   // (the SGD epilogue instantiation where the kernel itself stores: no split-K slabs)
   const bool sgd = p.sgd.theta != nullptr && p.splitk == 1;
-#define TN_PL_LAUNCH(BM_, BN_, WM_, WN_, NST_, ILV_, NT_)                                                       \
+  // the pixel walk (PIX) on small images, the 128x128 and 256x256 tiles: l4 / l4a / l3a wgrad 1.31 /
+  // 1.13 / 1.06x at 50 clients, l4 1.08x at 7 (bench/pix_bench.py, profiles/r6_c10_pix_bench.log)
+  p.pix = native_option(g_opt_conv_pix, "DLS_CONV_PIX", 1) != 0 && (variant == 0 || variant == 6) &&
+          p.C % t.bn == 0 && p.OH * p.OW <= 64 && p.KH * p.KW > 1 && p.pad > 0 && p.R == p.KH * p.KW * p.C &&
+          p.M == p.B * p.OH * p.OW;
+#define TN_PL_LAUNCH_X(BM_, BN_, WM_, WN_, NST_, ILV_, NT_, PIX_)                                                 \
   if (sgd)                                                                                                 \
-    hipLaunchKernelGGL((conv_tn_pl_kernel<BM_, BN_, WM_, WN_, NST_, ILV_, true>), dim3(grid), dim3(NT_), 0, s, p); \
+    hipLaunchKernelGGL((conv_tn_pl_kernel<BM_, BN_, WM_, WN_, NST_, ILV_, true, PIX_>), dim3(grid), dim3(NT_), 0, s, p); \
   else                                                                                                     \
-    hipLaunchKernelGGL((conv_tn_pl_kernel<BM_, BN_, WM_, WN_, NST_, ILV_>), dim3(grid), dim3(NT_), 0, s, p);
-  switch (variant) {
+    hipLaunchKernelGGL((conv_tn_pl_kernel<BM_, BN_, WM_, WN_, NST_, ILV_, false, PIX_>), dim3(grid), dim3(NT_), 0, s, p);
+#define TN_PL_LAUNCH(BM_, BN_, WM_, WN_, NST_, ILV_, NT_) TN_PL_LAUNCH_X(BM_, BN_, WM_, WN_, NST_, ILV_, NT_, false)
+  if (p.pix) {
+    if (variant == 0) {
+      TN_PL_LAUNCH_X(128, 128, 2, 2, 2, false, 256, true)
+    } else {
+      TN_PL_LAUNCH_X(256, 256, 2, 4, 2, false, 512, true)
+    }
+  } else switch (variant) {
     case 0: TN_PL_LAUNCH(128, 128, 2, 2, 2, false, 256) break;
     case 1: TN_PL_LAUNCH(64, 128, 2, 2, 2, false, 256) break;
     case 2: TN_PL_LAUNCH(128, 128, 2, 2, 3, true, 256) break;
@@ -711,6 +875,7 @@ bool conv_tn_pl(ConvTNParams p, int K, int variant, hipStream_t s) {
     default: return false;
   }
 #undef TN_PL_LAUNCH
+#undef TN_PL_LAUNCH_X
   if (p.splitk > 1) tn_fold(p.part, p.dw, p.dw_cs, K, p.splitk, (long)p.Co * p.R, s, &p.sgd);
   return true;
 }

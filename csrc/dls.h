@@ -16,6 +16,7 @@ extern int g_opt_halo_wgrad_unroll;  // conv_halo_wgrad.hip k-step unroll (1 or 
 // halo fwd / dgrad tiles past the valid samples skip their work (ConvNTParams::skip_valid; env
 // DLS_SKIP_INVALID, Python OPTIONS.skip_invalid)
 extern int g_opt_halo_skip;
+extern int g_opt_conv_pix;  // conv_pl.hip pixel-major tap skipping on small images (1 on)
 int native_option(int& slot, const char* env, int dflt);
 bool set_native_option(const char* name, int value);  // false: unknown name
 
@@ -144,6 +145,12 @@ struct ConvNTParams {
   // the plane GEMMs that read this output (Transformer h, linear dgrads)
   bf16_t* yp;
   long yp_cs, yp_lo;
+  // pixel-major GEMM rows (conv_pl.hip, set by conv_nt_pl for small images): GEMM row m is image
+  // m % B at pixel m / B — a 32-row group then holds one pixel, so the K walk visits only the taps
+  // that land inside the image for some row of the tile and a wave skips the MFMAs of groups
+  // whose pixel the tap misses (4x4 images, 3x3 taps: 100 of 144 tap-pixels are inside)
+  int pix;
+  FastDiv fd_pb;
 };
 
 // BN-backward partial request handed to conv_dgrad (see ConvNTParams::bnb)
@@ -288,6 +295,9 @@ struct ConvTNParams {
   // elements after them (0 = fp32 tensors); client strides dy_cs / x_cs in bf16 elements
   long dy_lo, x_lo;
   SgdEpi sgd;  // (pre-split launches only: step the weights instead of storing dW)
+  // (conv_pl.hip, set by conv_tn_pl for small images) the pixel reduction walks (pixel, 32-image
+  // chunk) pairs over only the pixels the workgroup's tap lands inside the image for
+  int pix;
 };
 
 // Large-tile conv GEMM fed by the LDS-DMA (conv_gl.hip): K loop over a tap table × 64-channel

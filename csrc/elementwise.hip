@@ -1151,6 +1151,7 @@ void synth_images(const int64_t* idx, long n, long npix, int C, int Cout, const 
 int g_opt_attn_mfma = kOptUnset, g_opt_conv_gl = kOptUnset;
 int g_opt_pl_min_wg = kOptUnset;
 int g_opt_halo_wgrad_unroll = kOptUnset, g_opt_halo_skip = kOptUnset;
+int g_opt_conv_pix = kOptUnset;
 
 int native_option(int& slot, const char* env, int dflt) {
   if (slot == kOptUnset) {
@@ -1167,7 +1168,8 @@ bool set_native_option(const char* name, int value) {
   };
   const Entry table[] = {{"attn_mfma", &g_opt_attn_mfma},
                          {"conv_gl", &g_opt_conv_gl},       {"pl_min_wg", &g_opt_pl_min_wg},
-                         {"halo_wgrad_unroll", &g_opt_halo_wgrad_unroll}, {"halo_skip", &g_opt_halo_skip}};
+                         {"halo_wgrad_unroll", &g_opt_halo_wgrad_unroll}, {"halo_skip", &g_opt_halo_skip},
+                         {"conv_pix", &g_opt_conv_pix}};
   for (const Entry& t : table)
     if (strcmp(t.name, name) == 0) {
       *t.slot = value;

@@ -15,7 +15,9 @@
 // YP: the output-planes stores (ConvNTParams::yp) are compiled in — off for the halo convs,
 // whose occupancy the two extra registers would cost (l1 halo dgrad: 128 → 130 VGPRs, 4 → 3
 // waves/SIMD, +45 % time measured)
-template <int TM, int TN, int NW, int PF = -1, bool YP = true>
+// PIX: pixel-major GEMM rows (ConvNTParams::pix): row m is image m % B at pixel m / B; the
+// valid-row limits (statistics, BN partials) are compared on the output row
+template <int TM, int TN, int NW, int PF = -1, bool YP = true, bool PIX = false>
 __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&acc)[TM][TN], unsigned char* smem,
                                                 int client, int m0, int n0, int wm0, int wn0, int wid, int lane) {
   constexpr int SW = TN * 32 + 4;  // slab row (fp32), 16-B aligned
@@ -83,8 +85,12 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
     const float4 v = *reinterpret_cast<const float4*>(ok ? base + off : base);
     return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  // GEMM row → output row (sub-pixel dgrad classes write every out_s-th pixel)
+  // GEMM row → output row (sub-pixel dgrad classes write every out_s-th pixel; pixel-major rows)
   auto row_of = [&](int m) -> long {
+    if constexpr (PIX) {
+      const uint32_t px = fdiv((uint32_t)m, p.fd_pb);
+      return (long)((uint32_t)m - px * (uint32_t)p.B) * (p.OH * p.OW) + px;
+    }
     if (p.out_s > 1) {
       const uint32_t b = fdiv(m, p.fd_ohw);
       const uint32_t rem = m - b * p.OH * p.OW;
@@ -92,6 +98,11 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
       const uint32_t ow = rem - oh * p.OW;
       return ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
     }
+    return m;
+  };
+  // the row the valid-row limits count (the GEMM row itself unless rows are pixel-major)
+  auto vrow = [&](int m) -> long {
+    if constexpr (PIX) return row_of(m);
     return m;
   };
   __syncthreads();
@@ -110,7 +121,7 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
           const int m = g0 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
           float v = acc[i][j][e] + bvals[j];
           if (p.relu) v = fmaxf(v, 0.f);
-          if (m < stat_rows) {
+          if (vrow(m) < stat_rows) {
             s0 += v;
             s1 = fmaf(v, v, s1);
           }
@@ -144,10 +155,10 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
         if (accp) av[t % NS] = ld4(accp, (p.acc_compact ? (long)m : row) * p.ldy + n, ok);
         if (amask) amv[t % NS] = abits(row, n, ok);
         if (bnb) {
-          const bool okb = ok && m < bnb_rows;
+          const bool okb = ok && vrow(m) < bnb_rows;
           xv[t % NS] = ld4(bx_base, row * p.bnb_xld + n, okb);
           if (bm_base) {
-            const uint32_t mb = *(okb ? bm_base + (long)m * (p.N >> 3) + (n >> 3) : bm_base);
+            const uint32_t mb = *(okb ? bm_base + vrow(m) * (p.N >> 3) + (n >> 3) : bm_base);
             mv[t % NS] = okb ? (mb >> (n & 4)) : 0u;
           } else if (by_base) {
             const float4 yv = ld4(by_base, row * p.ldy + n, okb);
@@ -254,14 +265,7 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
         const int r = qd / (TN * 8), cc = (qd % (TN * 8)) * 4;
         const int m = m0 + wm0 + i * 32 + r, n = n0 + wn0 + cc;
         if (m >= p.M || n >= p.N) continue;
-        long row = m;
-        if (p.out_s > 1) {
-          const uint32_t b = fdiv(m, p.fd_ohw);
-          const uint32_t rem = m - b * p.OH * p.OW;
-          const uint32_t oh = fdiv(rem, p.fd_ow);
-          const uint32_t ow = rem - oh * p.OW;
-          row = ((long)b * p.out_H + oh * p.out_s + p.out_ph) * p.out_W + ow * p.out_s + p.out_pw;
-        }
+        const long row = row_of(m);
         float* dst = y + row * p.ldy + n;
         const float* src = slab + r * SW + cc;
         const long arow = p.acc_compact ? (long)m : row;  // (compact acc: the class-grid row)
@@ -284,12 +288,12 @@ __device__ __forceinline__ void nt_f32_epilogue(const ConvNTParams& p, f32x16 (&
           }
           *reinterpret_cast<float4*>(dst) = v;
           if (YP && ypl) store_pl4(row * p.ldy + n, v);
-          if (bnb && m < bnb_rows) {  // ĝ = dX·relu', x̂ = (x − μ)·rstd of the BN whose dY this is
+          if (bnb && vrow(m) < bnb_rows) {  // ĝ = dX·relu', x̂ = (x − μ)·rstd of the BN whose dY this is
             const float4 xv =
                 *reinterpret_cast<const float4*>(p.bnb_x + ((long)client * p.M + row) * p.bnb_xld + n);
             uint32_t mb = 0xFu;
             if (p.bnb_mask) {
-              mb = p.bnb_mask[((long)client * p.M + m) * (p.N >> 3) + (n >> 3)] >> (n & 4);
+              mb = p.bnb_mask[((long)client * p.M + vrow(m)) * (p.N >> 3) + (n >> 3)] >> (n & 4);
             } else if (p.bnb_y) {
               const float4 yv = *reinterpret_cast<const float4*>(p.bnb_y + (long)client * p.y_cs + row * p.ldy + n);
               mb = (yv.x > 0.f ? 1u : 0u) | (yv.y > 0.f ? 2u : 0u) | (yv.z > 0.f ? 4u : 0u) | (yv.w > 0.f ? 8u : 0u);

@@ -1434,3 +1434,86 @@ def test_halo_wgrad_bn_bwd_loader(hip, case, xmode, gate):
     alone = torch.full((K, 2, R, N), 7.0, dtype=torch.bfloat16, device=DEV)
     hip.bn_bwd_apply_planes(dyo, xb, mask, coef, vr, alone)
     assert torch.equal(alone, dxp_ref)
+
+
+@pytest.mark.parametrize("case", [
+    # K, B, H (= W), Ci, Co, stride: ResNet-18 l4 (4x4), a batch that is no multiple of 32 (groups
+    # straddle pixels), the strided l4a forward (8x8 -> 4x4) and a 7x7 image
+    (2, 64, 4, 128, 128, 1),
+    (2, 40, 4, 256, 512, 1),
+    (2, 33, 8, 128, 128, 2),
+    (2, 8, 7, 64, 128, 1),
+])
+def test_conv_pixel_major_tap_skip(hip, case):
+    """Pixel-major GEMM rows with tap skipping on small images (csrc/conv_pl.hip PIX, native option
+    conv_pix): forward (with BN statistics over the valid samples) and dgrad (with a residual
+    gradient and BN-backward partials) are bitwise the plain walk's — a skipped tap only ever added
+    zeros — on the 128x128 and 256x256 tiles; the weight gradient's pixel walk (other summation
+    order) is within 1e-5 of the fp64 oracle and reproducible."""
+    K, B, H, Ci, Co, s = case
+    torch.manual_seed(B + H)
+    x = _f(K, B, H, H, Ci)
+    w = _f(K, Co, 3, 3, Ci, scale=0.2)
+    ws = _wsplit(hip, w)
+    xp = hip.split_planes(x)
+    OH = (H + 2 - 3) // s + 1
+    M = B * OH * OH
+    valid = torch.tensor([B, max(1, B - 5)], dtype=torch.int32, device=DEV)
+    dy = _f(K, B, OH, OH, Co)
+    dyp = hip.split_planes(dy)
+    acc = _f(K, B, H, H, Ci)
+    # BN-backward partials of the BN whose dY the stride-1 dgrad is (x its input)
+    x3 = x.reshape(K, B * H * H, Ci)
+    vr = (valid * H * H).to(torch.int32)
+    _, mean, rstd, mask = hip.bn_fwd(x3, torch.ones(K, Ci, device=DEV), torch.zeros(K, Ci, device=DEV), vr, True,
+                                     None, with_mask=True)
+    y_exp = ref.conv_fwd(_d(x), _d(w), s, 1)
+    dx_exp = ref.conv_dgrad(_d(dy), _d(w), (H, H), s, 1) + _d(acc)
+    gw_exp = ref.conv_wgrad(_d(dy), _d(x), (K, Co, 3, 3, Ci), s, 1)
+    outs = {}
+    try:
+        for pix in (0, 1):
+            hip._C.set_native_option("conv_pix", pix)
+            for v in (1, 3):
+                hip._C.conv_nt_pl_set_variant(v)
+                st = torch.full((K, hip.conv_stats_parts(M), 2, Co), float("nan"), device=DEV)
+                y = hip.conv_fwd(x, w, s, 1, w_split=ws, x_planes=xp, stats=st, stats_valid=valid)
+                assert torch.isfinite(st).all()
+                r = {"y": y, "st": st}
+                if s == 1:
+                    part = torch.full((K, hip.conv_stats_parts(B * H * H), 2, Ci), float("nan"), device=DEV)
+                    r["dx"] = hip.conv_dgrad(dy, w, (H, H), 1, 1, acc=acc, w_split=ws, dy_planes=dyp,
+                                             bnb=(part, x3, mask, mean, rstd, vr, None))
+                    assert torch.isfinite(part).all()
+                    r["part"] = part
+                outs[(pix, v)] = r
+            for tv in (0, 6):
+                hip._C.conv_tn_pl_set_variant(tv)
+                ga = torch.full((K, Co, 3, 3, Ci), 5.0, device=DEV)
+                hip.conv_wgrad(dy, x, ga, s, 1, dy_planes=dyp, x_planes=xp)
+                _close(ga, gw_exp)
+                gb = torch.full_like(ga, -5.0)
+                hip.conv_wgrad(dy, x, gb, s, 1, dy_planes=dyp, x_planes=xp)
+                assert torch.equal(ga, gb), f"pix {pix} tn variant {tv} not reproducible"
+    finally:
+        hip._C.set_native_option("conv_pix", 1)
+        hip._C.conv_nt_pl_set_variant(-1)
+        hip._C.conv_tn_pl_set_variant(-1)
+    y3 = y_exp.reshape(K, M, Co)
+    xh = (_d(x3) - _d(mean)[:, None]) * _d(rstd)[:, None]
+    gd = dx_exp.reshape(K, B * H * H, Ci) * (xh > 0).double()
+    for (pix, v), r in outs.items():
+        base = outs[(0, v)]
+        assert torch.equal(r["y"], base["y"]), f"pix {pix} variant {v} fwd differs"
+        _close(r["y"], y_exp)
+        for kk in range(K):
+            rows = int(valid[kk]) * OH * OH
+            _close(r["st"][kk, :, 0].double().sum(0), y3[kk, :rows].sum(0))
+            _close(r["st"][kk, :, 1].double().sum(0), (y3[kk, :rows] ** 2).sum(0))
+        if s == 1:
+            assert torch.equal(r["dx"], base["dx"]), f"pix {pix} variant {v} dgrad differs"
+            _close(r["dx"], dx_exp)
+            for kk in range(K):
+                rows = int(vr[kk])
+                _close(r["part"][kk, :, 0].double().sum(0), gd[kk, :rows].sum(0))
+                _close(r["part"][kk, :, 1].double().sum(0), (gd[kk, :rows] * xh[kk, :rows]).sum(0))
