@@ -53,8 +53,19 @@ def main():
         gw = torch.empty((K, C, 3, 3, C), device="cuda")
         coef = torch.stack([torch.rand(K, C, device="cuda") + 0.5, torch.randn(K, C, device="cuda")], -1).contiguous()
         flop = 2.0 * K * B * H * H * C * C * 9
+        # the BN backward in the dY loader (dy mode 2): dy_out, the BN's raw input, ReLU bits, (a, d, e)
+        R = B * H * H
+        dyo = torch.randn(K, R, C, device="cuda")
+        xbn = torch.randn(K, R, C, device="cuda")
+        mk = torch.randint(0, 256, (K, R * C // 8), dtype=torch.uint8, device="cuda")
+        cf3 = torch.randn(K, C, 3, device="cuda").contiguous()
+        dxp = torch.empty((K, 2, R, C), dtype=torch.bfloat16, device="cuda")
+        bnb = (dyo, xbn, mk, cf3, None, dxp)
         runs = {
             "tn_planes": lambda: hip.conv_wgrad(dy, x, gw, 1, 1, dy_planes=dyp, x_planes=xp),
+            "bn_bwd_apply_pass": lambda: hip.bn_bwd_apply_planes(dyo, xbn, mk, cf3, None, dxp),
+            "halo_xplanes_dm2": lambda: hip.halo_wgrad(dy, x, gw, x_planes=xp, bn_bwd=bnb),
+            "halo_bn_dm2": lambda: hip.halo_wgrad(dy, x, gw, bn=(coef, True, None), bn_bwd=bnb),
             "halo_planes": lambda: hip.halo_wgrad(dy, x, gw, dy_planes=dyp, x_planes=xp),
             "halo_f32": lambda: hip.halo_wgrad(dy, x, gw),
             "halo_bn_dyplanes": lambda: hip.halo_wgrad(dy, x, gw, dy_planes=dyp, bn=(coef, True, None)),
@@ -62,7 +73,7 @@ def main():
         for small in [int(v) for v in args.unroll.split(",")]:
             with options.override(native={"halo_wgrad_unroll": small}):
                 for rn, fn in runs.items():
-                    if (rn == "tn_planes" and small != 1) or (args.runs and rn not in args.runs.split(",")):
+                    if (rn in ("tn_planes", "bn_bwd_apply_pass") and small != 1) or (args.runs and rn not in args.runs.split(",")):
                         continue
                     t = timeit(fn, args.iters)
                     print(json.dumps({"layer": name, "K": K, "run": rn, "unroll": small if rn != "tn_planes" else None,

@@ -372,9 +372,17 @@ static int pl_min_wg() {
   return native_option(g_opt_pl_min_wg, "DLS_PL_MIN_WG", 256);
 }
 
+// Evaluation-sized launches (GTG-Shapley utility: 8192 images per model, M >= 128 K rows per
+// client; bench/eval_tiles_bench.py, profiles/r6_c11_eval_tiles.log): N = 256 also takes the
+// 256x256 tile (l3a 3.63 vs 4.06 ms, l3sc 1.01 vs 1.06) and the 3x3 N = 128 conv the 3-stage
+// interleaved 256x128 tile (l2a 2.36 vs 2.53; the 1x1 shortcut keeps 128x128, 0.84 vs 0.97)
 int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
   if (p.N <= 64) return 2;
   if (p.N >= 512) return (long)K * cdiv(p.M, 256) * cdiv(p.N, 256) < pl_min_wg() ? 1 : 3;
+  if (p.M >= (1 << 17)) {
+    if (p.N >= 256) return 3;
+    if (p.KH * p.KW > 1) return 4;
+  }
   return 1;
 }
 
