@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--nt-variants", default="", help="also time fwd / dgrad on these conv_nt_pl variants")
+    ap.add_argument("--tn-variants", default="", help="also time the wgrad on these conv_tn_pl variants")
     args = ap.parse_args()
     from distributed_learning_simulator_amd.ops import build
 
@@ -100,6 +101,14 @@ def main():
                                       args.iters) * 1e3, 3)]
             finally:
                 hip._C.conv_nt_pl_set_variant(-1)
+        tn = {}
+        for v in [int(a) for a in args.tn_variants.split(",") if a]:
+            hip._C.conv_tn_pl_set_variant(v)
+            try:
+                tn[v] = round(timeit(lambda: hip.conv_wgrad(dy, x, gw, s, pad, dy_planes=dyp, x_planes=xp),
+                                     args.iters) * 1e3, 3)
+            finally:
+                hip._C.conv_tn_pl_set_variant(-1)
         for key, t in (("fwd", t_f), ("dgrad", t_d), ("wgrad", t_w)):
             tot[key] += t * n
         flops_tot += 3 * flops * n
@@ -108,7 +117,8 @@ def main():
                           "dgrad_ms": round(t_d * 1e3, 3), "dgrad_tflops": round(flops / t_d / 1e12, 1),
                           "wgrad_ms": round(t_w * 1e3, 3), "wgrad_tflops": round(flops / t_w / 1e12, 1),
                           "weighted_ms": round((t_f + t_d + t_w) * n * 1e3, 2),
-                          **({"nt_variants_fwd_dgrad_ms": nt} if nt else {})}), flush=True)
+                          **({"nt_variants_fwd_dgrad_ms": nt} if nt else {}),
+                          **({"tn_variants_wgrad_ms": tn} if tn else {})}), flush=True)
         del x, w, dy, gw, wpl, xp, dyp
         torch.cuda.empty_cache()
     ms = sum(tot.values()) * 1e3

@@ -389,8 +389,9 @@ long chan_sums_f64_ws(int R, int C);
 void chan_sums_f64(const float* x, long x_cs, int ldx, int K, int R, int C, const int* valid, double* ws, double* out,
                    long out_cs, int ldo, hipStream_t s);
 // BN apply with precomputed (scale, shift) coefficients (bn_fwd coef_out) → split planes (+ ReLU bits)
+// and / or the fp32 output y
 void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
-                   bf16_t* yp, uint8_t* rmask, hipStream_t s);
+                   bf16_t* yp, uint8_t* rmask, hipStream_t s, float* y = nullptr);
 bool conv_halo_bn_fwd(const float* x, long x_cs, const float* coef, int relu, const int* valid_rows,
                       const bf16_t* wsplit, long ws_cs, long ws_plane, int rep, float* y, long y_cs, int K, int B,
                       int H, int W, int C, int N, float* stats, const int* stats_valid, hipStream_t s,
@@ -443,7 +444,8 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
             uint8_t* relu_mask, int f32, hipStream_t s,
             int ldx = 0, const float* pre_part = nullptr,
             int pre_nparts = 0, bf16_t* yp = nullptr,
-            int y_f32 = 1, float* coef_out = nullptr, int apply = 1);  // yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; ldx: row stride of x / res (channel slice of a wider buffer), y
+            int y_f32 = 1, float* coef_out = nullptr, int apply = 1,
+            const float* res_coef = nullptr);  // res_coef [K][C][2]: res is a second BN's raw input, applied here; yp / y_f32: split planes of y (fp32 only) with or without y; relu_mask: optional [K][R][C/8] bits out; ldx: row stride of x / res (channel slice of a wider buffer), y
                                   // contiguous; pre_part: [K][pre_nparts][2C] Σx / Σx² partials from the
                                   // producing conv's epilogue (ConvNTParams::stats) — no statistics pass
 void bn_bwd(const void* dy, const void* x, const void* y, const float* mean, const float* rstd, const void* gamma,

@@ -402,8 +402,11 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
                                                        T* __restrict__ y, const int* __restrict__ valid_rows,
                                                        const float* __restrict__ coef, int R, int C, int relu,
                                                        int rpb, uint8_t* __restrict__ rmask, int ldx,
-                                                       bf16_t* __restrict__ yp, int y_f32) {
-  // x / res rows at stride ldx (channel slice of a wider buffer), y contiguous
+                                                       bf16_t* __restrict__ yp, int y_f32,
+                                                       const float* __restrict__ res_coef) {
+  // x / res rows at stride ldx (channel slice of a wider buffer), y contiguous. res_coef [K][C][2]:
+  // res is the RAW input of a second BatchNorm (no ReLU, same valid rows) whose apply is folded
+  // in here — out += res_scale·res + res_shift, the bits of applying it first (ResNet downsample)
   const int k = blockIdx.y;
   const int CT = C / V;
   const int nvalid = valid_rows ? min(valid_rows[k], R) : R;
@@ -415,11 +418,13 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
     const int cc = threadIdx.x % ctn, rl = threadIdx.x / ctn;
     if (rl >= RT) continue;
     const int c0 = (cg + cc) * V;
-    float sc[V], sh[V];
+    float sc[V], sh[V], rsc[V], rsh[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       sc[j] = coef[2 * ((long)k * C + c0 + j)];
       sh[j] = coef[2 * ((long)k * C + c0 + j) + 1];
+      rsc[j] = res_coef ? res_coef[2 * ((long)k * C + c0 + j)] : 0.f;
+      rsh[j] = res_coef ? res_coef[2 * ((long)k * C + c0 + j) + 1] : 0.f;
     }
     for (int r = r0 + rl; r < r1; r += RT) {
       const long off = base + (long)r * C + c0;
@@ -433,8 +438,13 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const T* __restrict__ x, 
         if (res) {
           float rv[V];
           load_vec<V>(res + offx, rv);
+          if (res_coef) {
 #pragma unroll
-          for (int j = 0; j < V; ++j) out[j] += rv[j];
+            for (int j = 0; j < V; ++j) out[j] += fmaf(rv[j], rsc[j], rsh[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) out[j] += rv[j];
+          }
         }
         if (relu) {
 #pragma unroll
@@ -770,7 +780,7 @@ long bn_workspace_floats(int K, long R, int C) {
 void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res, void* y, float* mean, float* rstd,
             const int* valid_rows, long g_cs, int K, int R, int C, int relu, float eps, int rep, float* ws,
             uint8_t* rmask, int f32, hipStream_t s, int ldx, const float* pre_part,
-            int pre_nparts, bf16_t* yp, int y_f32, float* coef_out, int apply) {
+            int pre_nparts, bf16_t* yp, int y_f32, float* coef_out, int apply, const float* res_coef) {
   if (ldx == 0) ldx = C;
   // ws layout: [K][3C] coefficients, then [K][parts][2C] per-workgroup partial sums. coef_out: the
   // (scale, shift) pairs go there instead and outlive this call (apply = 0: the consumer conv
@@ -805,23 +815,23 @@ void bn_fwd(const void* x, const void* gamma, const void* beta, const void* res,
     if (apply) {
       DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_kernel<TT, VV>), grid, dim3(256), 0, s, CP(x), CP(res), MP(y),
                                        valid_rows, coef, R, C, relu, rpb, rmask, ldx, f32 ? yp : nullptr,
-                                       f32 ? y_f32 : 1));
+                                       f32 ? y_f32 : 1, res_coef));
     }
   });
 }
 
 void bn_apply_only(const float* x, const float* coef, const int* valid_rows, int K, int R, int C, int relu,
-                   bf16_t* yp, uint8_t* rmask, hipStream_t s) {
+                   bf16_t* yp, uint8_t* rmask, hipStream_t s, float* y) {
   // the apply pass of bn_fwd with coefficients computed earlier (bn_coef): planes (+ ReLU bits)
-  // only — what a deferred BN materialises when its consumer cannot apply it itself
+  // and / or the fp32 output y — what a deferred BN materialises when its consumer cannot apply it
   const int rpb = rows_per_block(R, K);
   dim3 grid(cdiv(R, rpb), K);
   if (C % 8 == 0) {
-    hipLaunchKernelGGL((bn_apply_kernel<float, 8>), grid, dim3(256), 0, s, x, (const float*)nullptr, (float*)nullptr,
-                       valid_rows, coef, R, C, relu, rpb, rmask, C, yp, 0);
+    hipLaunchKernelGGL((bn_apply_kernel<float, 8>), grid, dim3(256), 0, s, x, (const float*)nullptr, y,
+                       valid_rows, coef, R, C, relu, rpb, rmask, C, yp, y ? 1 : 0, (const float*)nullptr);
   } else {
-    hipLaunchKernelGGL((bn_apply_kernel<float, 1>), grid, dim3(256), 0, s, x, (const float*)nullptr, (float*)nullptr,
-                       valid_rows, coef, R, C, relu, rpb, (uint8_t*)nullptr, C, yp, 0);
+    hipLaunchKernelGGL((bn_apply_kernel<float, 1>), grid, dim3(256), 0, s, x, (const float*)nullptr, y,
+                       valid_rows, coef, R, C, relu, rpb, (uint8_t*)nullptr, C, yp, y ? 1 : 0, (const float*)nullptr);
   }
 }
 

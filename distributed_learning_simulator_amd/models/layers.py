@@ -159,12 +159,13 @@ class BatchNorm(Module):
     def forward(self, x, ctx, residual=None, relu=None, link=None, stats=None, planes: int = 0):
         """`planes`: the output's consumers are split-plane convs (Fn.batch_norm): 1 = they and
         fp32 readers, 2 = split-plane convs only. Effective while the weights' planes are live
-        (training steps with BoundParams.split); otherwise the output is plain fp32."""
+        (training steps with BoundParams.split); otherwise the output is plain fp32. 4: the output
+        is read only as the next BatchNorm's residual, which folds this apply into its own."""
         P = ctx.P
         rps = 1
         for d in x.shape[2:-1]:
             rps *= d
-        if getattr(P, "split", None) is None or self.c % 32:
+        if (getattr(P, "split", None) is None or self.c % 32) and planes != 4:
             planes = 0
         return Fn.batch_norm(x, ctx.token, P.w(self.gamma), P.w(self.beta), P.g(self.gamma), P.g(self.beta),
                              ctx.valid_rows(rps), self.relu if relu is None else relu, residual, link=link,

@@ -98,9 +98,10 @@ def _residual_link(block, x, ctx):
 
 def _down(seq: Seq, x, ctx, donor=None):
     """Downsample shortcut Seq(Conv2d 1x1, BatchNorm) with epilogue statistics; `donor`: the
-    shortcut conv's input gradient goes to the block's first conv (Fn.ResidualLink)."""
+    shortcut conv's input gradient goes to the block's first conv (Fn.ResidualLink). Its BN output
+    is read only as the block's last BN's residual, which applies it (batch_norm planes=4)."""
     conv, bn = seq.children
-    return conv_bn(conv, bn, x, ctx, conv_donor=donor)
+    return conv_bn(conv, bn, x, ctx, conv_donor=donor, planes=4)
 
 
 class BasicBlock(Module):

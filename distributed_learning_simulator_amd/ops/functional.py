@@ -156,6 +156,33 @@ class DeferredBN:
             self.pending = False
 
 
+# downsample BN applies folded into the next BN ("folded") or run as their own pass ("materialized")
+res_fold_count = {"folded": 0, "materialized": 0}
+
+
+class DeferredRes:
+    """A BatchNorm output without ReLU whose one reader is the next BatchNorm, as its residual — a
+    ResNet downsample shortcut's BN (batch_norm planes=4): the statistics and (scale, shift) are
+    computed, the output is never written, and the reader folds the apply into its own
+    (hip.bn_fwd res_coef: act(bn2(x) + scale·x_ds + shift), the bits of applying it first). The
+    backward needs no output (no ReLU). Anything else that needs the values calls materialize(),
+    the ordinary apply pass into the same tensor."""
+
+    __slots__ = ("x", "coef", "valid_rows", "y", "pending")
+
+    def __init__(self, x, coef, valid_rows, y):
+        self.x, self.coef, self.valid_rows, self.y = x, coef, valid_rows, y
+        self.pending = True
+
+    def materialize(self):
+        if self.pending:
+            from . import hip
+
+            hip.bn_apply_only(self.x, self.coef, self.valid_rows, False, None, y=self.y)
+            self.pending = False
+            res_fold_count["materialized"] += 1
+
+
 # deferred BN backward applies (DeferredBNBwd) taken by a halo weight gradient's loader ("wgrad")
 # or run as their own pass ("materialized"): tests, reports
 bn_bwd_defer_count = {"wgrad": 0, "materialized": 0}
@@ -661,6 +688,18 @@ class _BN(torch.autograd.Function):
         mask = None
         yp = None
         bnb = None
+        res_coef = None
+        fold = getattr(residual, "_dls_res_fold", None) if residual is not None else None
+        if fold is not None and fold.pending:
+            # a downsample BN's apply folded into this one (DeferredRes), or materialised first
+            if (be is not ref and x.dtype == torch.float32 and fold.valid_rows is valid_rows
+                    and fold.x.shape == x3.shape and x3.is_contiguous()):
+                r3, res_coef = fold.x, fold.coef
+                fold.pending = False
+                res_fold_count["folded"] += 1
+            else:
+                fold.materialize()
+        fold_out = None
         if be is ref:
             y, mean, rstd = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3)
         else:  # native: 1-bit ReLU mask so the backward need not re-read y
@@ -673,7 +712,16 @@ class _BN(torch.autograd.Function):
             C8 = C % 8 == 0
             if planes == 3 and not (OPTIONS.bn_fused_halo and residual is None and C8 and x3.is_contiguous()):
                 planes = 2  # (no deferral: apply now, planes only)
-            if planes == 3:
+            if planes == 4 and not (OPTIONS.bn_res_fold and residual is None and not relu and x3.is_contiguous()):
+                planes = 0  # (no fold: apply now, fp32)
+            if planes == 4:
+                # the reader (the next BN, as its residual) applies it (DeferredRes)
+                coef, mean, rstd = be.bn_coef(x3, gamma, beta, valid_rows, pre_stats=pre)
+                y = torch.empty((K, x3.shape[1], C), dtype=x.dtype, device=x.device)
+                fold_out = DeferredRes(x3, coef, valid_rows, y)
+                defer = None
+                planes = 0
+            elif planes == 3:
                 # deferred apply (DeferredBN): statistics + coefficients now; the consuming 3x3 conv
                 # applies them in its halo loader, or materialises the planes / ReLU bits first
                 coef, mean, rstd = be.bn_coef(x3, gamma, beta, valid_rows, pre_stats=pre)
@@ -682,7 +730,8 @@ class _BN(torch.autograd.Function):
                 defer = DeferredBN(x3, coef, relu, valid_rows, yp, mask, write_out=wm)
             else:
                 defer = None
-                out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=wm, pre_stats=pre, planes=planes)
+                out = be.bn_fwd(x3, gamma, beta, valid_rows, relu, r3, with_mask=wm, pre_stats=pre, planes=planes,
+                                res_coef=res_coef)
                 y, mean, rstd = out[:3]
                 mask = out[3] if wm else None
                 if planes:
@@ -709,6 +758,8 @@ class _BN(torch.autograd.Function):
         ctx.defer = None
         if be is not ref and planes == 3:
             yo._dls_bn_defer = ctx.defer = defer
+        if fold_out is not None:
+            yo._dls_res_fold = fold_out
         if bnb is not None:
             yo._dls_bnb = bnb
         return yo
@@ -789,7 +840,9 @@ def batch_norm(x, token, gamma, beta, ggamma, gbeta, valid_rows=None, relu=False
     """`planes` (fp32 native): 1 = the output also carries its split planes (`_dls_planes`) for
     the conv(s) that read it, 2 = the output is ONLY planes — for outputs read by nothing but
     split-plane convs (e.g. a ResNet block's inner BN), 3 = as 2 with the apply pass deferred to
-    the ONE conv that reads it (DeferredBN: a 3x3 stride-1 halo conv applies it while staging)."""
+    the ONE conv that reads it (DeferredBN: a 3x3 stride-1 halo conv applies it while staging);
+    4 (no ReLU): the output's one reader is the next BatchNorm, as its residual, which folds this
+    apply into its own (DeferredRes: a ResNet downsample shortcut)."""
     return _BN.apply(x, token, gamma, beta, ggamma, gbeta, valid_rows, relu, residual, link, stats, planes)
 
 

@@ -715,14 +715,18 @@ def planes_buffer(shape, device):
 
 
 def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5, with_mask=False, pre_stats=None,
-           planes: int = 0):
+           planes: int = 0, res_coef=None):
     """Returns (y, mean, rstd); with_mask=True (ReLU, C % 8 == 0) also returns the 1-bit ReLU
     mask [K, R, C/8] uint8 that bn_bwd can read instead of y. `x` (and `residual`) may be
     channel slices of a wider buffer ([K, R, C] at row stride ld); y is contiguous.
     `pre_stats`: [K, parts, 2, C] Σx / Σx² partials written by the producing conv's epilogue
     (conv_fwd(stats=)) — the statistics pass over x is skipped.
     `planes` (fp32): 1 = also write y's split planes, 2 = write only the planes (y is then their
-    fp32-typed alias, see planes_buffer); the planes [K, 2, R, C] are returned last."""
+    fp32-typed alias, see planes_buffer); the planes [K, 2, R, C] are returned last.
+    `res_coef` [K, C, 2] (fp32, with `residual`): the residual is the RAW input of a second
+    BatchNorm without ReLU (same valid rows) whose (scale, shift) pairs bn_coef computed — its
+    apply is folded into this one (y = act(bn(x) + scale·res + shift), the bits of applying it
+    first)."""
     K, R, C = x.shape
     x, ldx = _pix_stride(x)
     assert x.stride(0) == R * ldx, "client stride of a strided BN input must be R*ld"
@@ -751,9 +755,11 @@ def bn_fwd(x, gamma, beta, valid_rows=None, relu=False, residual=None, eps=1e-5,
     if with_mask and relu and C % 8 == 0 and ldx % 8 == 0:
         mask = torch.empty((K, R, C // 8), dtype=torch.uint8, device=x.device)
     assert gamma.dtype == x.dtype and (residual is None or residual.dtype == x.dtype)
+    if res_coef is not None:
+        assert residual is not None and x.dtype == F32 and res_coef.shape == (K, C, 2) and res_coef.is_contiguous()
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), _p(residual), _p(y), _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, int(relu),
               eps, rep, _p(ws), _p(mask), _f32(x), _s(), ldx, _p(pre_stats),
-              0 if pre_stats is None else pre_stats.shape[1], _p(yp), int(planes != 2), NULL, 1)
+              0 if pre_stats is None else pre_stats.shape[1], _p(yp), int(planes != 2), NULL, 1, _p(res_coef))
     out = (y, mean, rstd, mask) if with_mask else (y, mean, rstd)
     return out + (yp,) if planes else out
 
@@ -777,7 +783,7 @@ def bn_coef(x, gamma, beta, valid_rows=None, eps=1e-5, pre_stats=None):
         assert pre_stats.shape[0] == K and pre_stats.shape[2:] == (2, C), pre_stats.shape
     _C.bn_fwd(_p(x), _p(gamma), _p(beta), NULL, NULL, _p(mean), _p(rstd), _p(vr), g_cs, K, R, C, 0, eps, rep, _p(ws),
               NULL, 1, _s(), ldx, _p(pre_stats),
-              0 if pre_stats is None else pre_stats.shape[1], NULL, 1, _p(coef), 0)
+              0 if pre_stats is None else pre_stats.shape[1], NULL, 1, _p(coef), 0, NULL)
     return coef, mean, rstd
 
 
@@ -828,15 +834,17 @@ def halo_bn_ok(shape, w) -> bool:
             and bool(_C.conv_halo_bn_supported(B, H, W, C, w.shape[1])))
 
 
-def bn_apply_only(x, coef, valid_rows, relu: bool, yp, mask=None):
-    """Materialise a deferred BN: relu?(coef-scaled x) → split planes yp [K, 2, R, C] (+ ReLU bits)."""
+def bn_apply_only(x, coef, valid_rows, relu: bool, yp, mask=None, y=None):
+    """Materialise a deferred BN: relu?(coef-scaled x) → split planes yp [K, 2, R, C] (+ ReLU bits)
+    and / or the fp32 output `y` [K, R, C] (bn_fwd's bits either way)."""
     K, R, C = x.shape
     assert x.dtype == F32 and x.is_contiguous() and coef.shape == (K, C, 2)
-    assert yp.shape == (K, 2, R, C) and yp.dtype == BF16 and yp.is_contiguous()
+    assert yp is None or (yp.shape == (K, 2, R, C) and yp.dtype == BF16 and yp.is_contiguous())
+    assert y is None or (y.shape == (K, R, C) and y.dtype == F32 and y.is_contiguous())
     if mask is not None:
         assert mask.shape == (K, R, C // 8) and C % 8 == 0
     vr = valid_rows.to(torch.int32).contiguous() if valid_rows is not None else None
-    _C.bn_apply_only(_p(x), _p(coef), _p(vr), K, R, C, int(relu), _p(yp), _p(mask), _s())
+    _C.bn_apply_only(_p(x), _p(coef), _p(vr), K, R, C, int(relu), _p(yp), _p(mask), _s(), _p(y))
 
 
 def conv_halo_bn_fwd(x, coef, relu: bool, valid_rows, w, w_split, stats=None, stats_valid=None, yp=None, mask=None):

@@ -54,6 +54,9 @@ class RuntimeOptions:
     bn_fused_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_FUSED_HALO", True))
     """A BN(+ReLU) whose only reader is a 3x3 stride-1 conv (ResNet BasicBlock bn1) is applied in
     that conv's halo loader (ops.functional DeferredBN; off: BN apply pass + plane conv)."""
+    bn_res_fold: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_BN_RES_FOLD", True))
+    """A ResNet downsample shortcut's BN is applied inside the block's last BN apply, which reads
+    its raw input as the residual (ops.functional DeferredRes; off: its own apply pass)."""
     dense_bn_halo: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_DENSE_BN_HALO", True))
     """DenseNet growth convs apply their BN + ReLU in the halo loader over the block buffer's
     channel prefix (off: BN apply pass + implicit-GEMM conv)."""

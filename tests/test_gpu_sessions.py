@@ -235,6 +235,24 @@ def test_resnet18_bn_bwd_in_wgrad_bitwise(hip, tmp_path):
     assert torch.equal(a.server.global_parameter, b.server.global_parameter)
 
 
+def test_resnet18_downsample_bn_fold_bitwise(hip, tmp_path):
+    """A downsample shortcut's BN applied inside the block's last BN (OPTIONS.bn_res_fold,
+    ops.functional DeferredRes): a 2-round ResNet-18 session (ragged last batches) and its test
+    evaluation give the unfolded run's global model and metrics bit for bit."""
+    ov = {"round": 2, "epoch": 1, "worker_number": 4, "model_name": "ResNet18", "dataset_kwargs.scale": 0.01,
+          "learning_rate": 0.05}
+    from distributed_learning_simulator_amd.ops import functional as Fn
+
+    Fn.res_fold_count.update(folded=0, materialized=0)
+    with options.override(bn_res_fold=True):
+        a, ra = _run("fed_avg/cifar10.yaml", ov, tmp_path / "a", "cuda")
+    assert Fn.res_fold_count["folded"] > 0 and Fn.res_fold_count["materialized"] == 0, Fn.res_fold_count
+    with options.override(bn_res_fold=False):
+        b, rb = _run("fed_avg/cifar10.yaml", ov, tmp_path / "b", "cuda")
+    assert torch.equal(a.server.global_parameter, b.server.global_parameter)
+    assert _losses(ra) == _losses(rb)
+
+
 def test_transformer_imdb_bitwise_reproducible_and_matches_cpu(hip, tmp_path):
     """The reference's imdb Transformer (d_model 100, 5 heads: dh 20 on the MFMA attention, with
     attention-probability dropout): two GPU runs are bitwise equal (deterministic LN / bias /

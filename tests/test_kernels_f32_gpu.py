@@ -1517,3 +1517,27 @@ def test_conv_pixel_major_tap_skip(hip, case):
                 rows = int(vr[kk])
                 _close(r["part"][kk, :, 0].double().sum(0), gd[kk, :rows].sum(0))
                 _close(r["part"][kk, :, 1].double().sum(0), (gd[kk, :rows] * xh[kk, :rows]).sum(0))
+
+
+@pytest.mark.parametrize("relu,valid", [(True, True), (False, False)])
+def test_bn_fwd_folded_residual_bn(hip, relu, valid):
+    """bn_fwd with `res_coef`: the residual is a second BN's raw input whose apply is folded in
+    (ResNet downsample, ops.functional DeferredRes) — bitwise the apply-first result (y, ReLU bits,
+    planes), and bn_apply_only(y=) materialises that second BN's output with bn_fwd's bits."""
+    torch.manual_seed(3)
+    K, R, C = 3, 517, 64
+    x = _f(K, R, C) * 2 + 0.5
+    xd = _f(K, R, C) * 3 - 0.2
+    g, b = torch.rand(K, C, device=DEV) + 0.5, _f(K, C)
+    gd, bd = torch.rand(K, C, device=DEV) + 0.5, _f(K, C)
+    vr = torch.tensor([R, R - 100, 7], dtype=torch.int32, device=DEV) if valid else None
+    yd, _, _ = hip.bn_fwd(xd, gd, bd, vr, False, None)
+    coef, _, _ = hip.bn_coef(xd, gd, bd, vr)
+    ym = torch.full_like(yd, float("nan"))
+    hip.bn_apply_only(xd, coef, vr, False, None, y=ym)
+    assert torch.equal(ym, yd)
+    ref_out = hip.bn_fwd(x, g, b, vr, relu, yd, with_mask=True, planes=1)
+    out = hip.bn_fwd(x, g, b, vr, relu, xd, with_mask=True, planes=1, res_coef=coef)
+    for u, v in zip(out, ref_out):
+        if u is not None or v is not None:
+            assert torch.equal(u, v)
