@@ -135,10 +135,11 @@ __device__ __forceinline__ long hbase(const HeadLayout& hl, long head, int H) {
 }
 
 // Staging rows [r0, r0+RB) of a head matrix (row stride ld, DH real columns) into an image of DP
-// padded columns (zero rows past L, zero columns past DH): `stage` in one go, or split in two so a
-// block's global loads can be issued into registers while the previous block's MFMAs run (DP ≤ 64:
-// one 8-column chunk per thread at most): stage_load fills the thread's chunk, stage_store splits
-// it into the image.
+// padded columns (zero rows past L, zero columns past DH): `stage` in one go, or split in two
+// (DP ≤ 64: one 8-column chunk per thread at most): stage_load fills the thread's chunk,
+// stage_store splits it into the image. (Issuing the next block's stage_load under the current
+// block's MFMAs cost the backward kernels the registers of their second / third workgroup per CU,
+// which hides that latency better: profiles/r6_c13_attn_occupancy.log)
 template <typename T, int DH, int DP>
 __device__ __forceinline__ void stage(const T* __restrict__ src, int ld, int r0, int L, const Img<T>& m) {
   for (int c = threadIdx.x; c < RB * DP / 8; c += WG) {
@@ -329,8 +330,9 @@ __global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__
 }
 
 // ------------------------------------------------------------------------------ dQ
+// three workgroups per CU, the key block loaded at its step (as the dK/dV kernel: 1.93 → 1.85 ms)
 template <typename T, int DH, int DP>
-__global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
+__global__ void __launch_bounds__(WG, 3) attn_bwd_dq_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
                                                               const T* __restrict__ k, const T* __restrict__ v,
                                                               const T* __restrict__ o, const float* __restrict__ lse,
                                                               const int* __restrict__ key_valid, T* __restrict__ dq,
@@ -377,18 +379,12 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
 #pragma unroll
   for (int t = 0; t < DP / 32; ++t) dqt[t] = f32x16{};
   float kx[8], vx[8];
-  if (nk > 0) {
-    stage_load<T, DH, DP>(k + base, lq.ld, 0, nk, kx);
-    stage_load<T, DH, DP>(v + base, lq.ld, 0, nk, vx);
-  }
   for (int k0 = 0; k0 < nk; k0 += RB) {
+    stage_load<T, DH, DP>(k + base, lq.ld, k0, nk, kx);
+    stage_load<T, DH, DP>(v + base, lq.ld, k0, nk, vx);
     stage_store<T, DP>(kx, KI);
     stage_store<T, DP>(vx, VI);
     __syncthreads();
-    if (k0 + RB < nk) {
-      stage_load<T, DH, DP>(k + base, lq.ld, k0 + RB, nk, kx);
-      stage_load<T, DH, DP>(v + base, lq.ld, k0 + RB, nk, vx);
-    }
     f32x16 st = f32x16{}, dpt = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < DP / 16; ++ks) {
@@ -422,8 +418,12 @@ __global__ void __launch_bounds__(WG) attn_bwd_dq_mfma_kernel(const T* __restric
 // wave per SIMD). Re-reading them per query block instead (two waves per SIMD) measured 2.73 →
 // 2.23 ms per launch alone but 22.40 → 22.62 s per FedOBD stage-1 round beside the other
 // sub-cohort's GEMMs (profiles/r5_c10_ab_attn_dkv_reload.txt): removed.
+// two workgroups per CU (≤ 256 registers per lane, a few spilled): with one, every barrier of the
+// 3-barrier query-block step stalled its CU. The query block is loaded at its step, not a step
+// ahead — the other workgroup covers the load, and the look-ahead registers would spill more
+// (2.56 → 1.92 ms per backward at 25 clients × 64 × 8 heads × 128², profiles/r6_c13_attn_occupancy.log)
 template <typename T, int DH, int DP>
-__global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
+__global__ void __launch_bounds__(WG, 2) attn_bwd_dkv_mfma_kernel(const T* __restrict__ dout, const T* __restrict__ q,
                                                                const T* __restrict__ k, const T* __restrict__ v,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
@@ -458,8 +458,6 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
   // a workgroup whose keys are all padding still writes their zero gradients (no early exit:
   // every wave must reach every barrier)
   const bool any = blockIdx.y * (4 * RB) < nk;
-  // (the next query block's Q / dO rows, lse and δ are loaded into registers under this block's
-  // MFMAs: the staging's global-load latency leaves the loop's critical path)
   float qx[8], ox[8], lq_r = 0.f, dq_r = 0.f;
   auto load_qblock = [&](int q0) {
     stage_load<T, DH, DP>(q + base, lq.ld, q0, L, qx);
@@ -470,8 +468,8 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
       dq_r = ok ? delta[head * L + q0 + threadIdx.x] : 0.f;
     }
   };
-  if (any) load_qblock(0);
   for (int q0 = 0; any && q0 < L; q0 += RB) {
+    load_qblock(q0);
     stage_store<T, DP>(qx, QI);
     stage_store<T, DP>(ox, OI);
     if (threadIdx.x < RB) {
@@ -479,7 +477,6 @@ __global__ void __launch_bounds__(WG) attn_bwd_dkv_mfma_kernel(const T* __restri
       Dq[threadIdx.x] = dq_r;
     }
     __syncthreads();
-    if (q0 + RB < L) load_qblock(q0 + RB);
     f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < DP / 16; ++ks) {
