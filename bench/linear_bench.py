@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--sweep", action="store_true", help="every conv_nt_pl / conv_tn_pl variant")
     ap.add_argument("--only", default="")
+    ap.add_argument("--f32-variants", default="", help="fp32-operand paths (register-staged split): conv_nt_f32 variants")
+    ap.add_argument("--tn-f32-variants", default="", help="fp32-operand weight gradient: conv_tn_f32 variants")
     args = ap.parse_args()
     from distributed_learning_simulator_amd.ops import hip
 
@@ -85,6 +87,26 @@ def main():
         t = timeit(lambda: hip.linear_fwd(x, w, b), args.iters)
         print(json.dumps({"layer": name, "op": "fwd_f32_split_in_loader", "K": K, "ms": round(t * 1e3, 4),
                           "tflops": round(flop / t / 1e12, 1)}), flush=True)
+        # the Transformer's fp32-operand users (attention output into out_proj, dqkv into in_proj):
+        # x / dY fp32 split in the loader, the weight from its planes
+        for v in [int(a) for a in args.f32_variants.split(",") if a]:
+            hip.nt_f32_variant = v
+            try:
+                for op, fn in (("fwd_f32", lambda: hip.linear_fwd(x, w, b, w_split=ws)),
+                               ("dgrad_f32", lambda: hip.linear_dgrad(dy, w, w_split=ws))):
+                    t = timeit(fn, args.iters)
+                    print(json.dumps({"layer": name, "op": op, "nt_f32_variant": v, "ms": round(t * 1e3, 4),
+                                      "tflops": round(flop / t / 1e12, 1)}), flush=True)
+            finally:
+                hip.nt_f32_variant = -1
+        for v in [int(a) for a in args.tn_f32_variants.split(",") if a]:
+            hip.tn_f32_variant = v
+            try:
+                t = timeit(lambda: hip.linear_wgrad(dy, x, gw, None), args.iters)
+                print(json.dumps({"layer": name, "op": "wgrad_f32", "tn_f32_variant": v, "ms": round(t * 1e3, 4),
+                                  "tflops": round(flop / t / 1e12, 1)}), flush=True)
+            finally:
+                hip.tn_f32_variant = -1
         del x, w, dy, xp, dyp, gw, gb
         torch.cuda.empty_cache()
 

@@ -681,6 +681,9 @@ int tn_f32_default_variant(int K, int Co, int R) {
   if (R <= 256 && Co > 64) return 5;
   if (Co <= 64) return 1;
   if (Co >= 256 && R >= 2048) return 3;
+  // (the Transformer in_proj weight gradient, Co 1536 x R 512: 1.16 vs 1.24 ms for 128x128,
+  // profiles/r6_c14_linear_f32_variants.log)
+  if (Co >= 1024 && R >= 512) return 3;
   return 0;
 }
 
@@ -747,6 +750,11 @@ void conv_nt_f32(const ConvNTParams& p, int K, int variant, hipStream_t s) {
     // 157-179 vs 132-151, the 8-channel stem 118 vs 98-108; fwd equal)
     variant = p.N <= 64 ? 9 : 1;
     if (p.N <= 32) variant = 10;
+    // linear-shaped GEMMs (1x1, no im2col: the Transformer's fp32-operand out_proj forward and
+    // in_proj dgrad) on the 128x128 tile at 3 waves per SIMD as well: out_proj fwd 0.44 → 0.38 ms,
+    // in_proj fwd / dgrad 1.25 / 1.10 → 1.09 / 1.02 (bench/linear_bench.py --f32-variants,
+    // profiles/r6_c14_linear_f32_variants.log)
+    if (p.N > 64 && p.KH * p.KW == 1) variant = 8;
   }
   // variants without the requested vector widths fall back to the all-widths 64x64 tile
   const bool v88 = va == 8 && vb == 8;
