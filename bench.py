@@ -149,7 +149,9 @@ def main() -> None:
         # one stderr line per round keeps long runs visibly alive (gpurun's silence watchdog)
         if comm.rank == 0:
             row = sess.metrics[-1] if sess.metrics else {}
-            print(f"[bench] {tag} round {row.get('round')} {row.get('wall_s', 0):.2f}s", file=sys.stderr, flush=True)
+            retries = torch.cuda.memory_stats().get("num_alloc_retries", 0) if torch.cuda.is_available() else 0
+            print(f"[bench] {tag} round {row.get('round')} {row.get('wall_s', 0):.2f}s (allocator retries {retries})",
+                  file=sys.stderr, flush=True)
 
     def barrier_sync():
         if comm.world > 1:
@@ -245,6 +247,12 @@ def main() -> None:
         }
         if stage2 is not None:
             out["stage2"] = stage2
+        if torch.cuda.is_available():
+            # device memory of this rank: peak allocated, and how often the caching allocator had to
+            # free its cache and retry an allocation (a synchronising stall)
+            ms = torch.cuda.memory_stats()
+            out["memory"] = {"peak_allocated_gb": round(ms.get("allocated_bytes.all.peak", 0) / 2**30, 2),
+                             "alloc_retries": int(ms.get("num_alloc_retries", 0))}
         if "extra" in wl:
             out.update(wl["extra"](sess, elapsed / args.steps))
         print(json.dumps(out), flush=True)
