@@ -253,8 +253,10 @@ __device__ __forceinline__ int crow(int e) { return (e & 3) + 8 * (e >> 2) + 4 *
 constexpr int pad_ld(int n) { return n + 8; }  // 16-B padded rows: conflict-free ds_read_b128
 
 // ------------------------------------------------------------------------------ forward
+// four workgroups per CU (127 VGPRs at dh 64, none spilled; the fp32 dh-48 build would spill at
+// four and keeps three)
 template <typename T, int DH, int DP>
-__global__ void __launch_bounds__(WG) attn_fwd_mfma_kernel(const T* __restrict__ q, const T* __restrict__ k,
+__global__ void __launch_bounds__(WG, (sizeof(T) == 4 && DH == 48) ? 3 : 4) attn_fwd_mfma_kernel(const T* __restrict__ q, const T* __restrict__ k,
                                                            const T* __restrict__ v, const int* __restrict__ key_valid,
                                                            T* __restrict__ o, float* __restrict__ lse, int L, int H,
                                                            float scale, HeadLayout lq, HeadLayout lo,
