@@ -17,6 +17,7 @@ wave; ResNet-50/ImageNet at batch 128 costs ≈20 GB of activations and runs in 
 
 from __future__ import annotations
 
+import gc
 import math
 import threading
 
@@ -30,6 +31,22 @@ from ..utils.logging import get_logger
 # probe (whose peak-memory counters are device-global). Re-entrant; uncontended in a
 # one-session process.
 DEVICE_LOCK = threading.RLock()
+
+# Held by every cyclic garbage collection, from its start to its end, in whatever thread it runs:
+# a capture takes it too (inside DEVICE_LOCK), so a collection another task thread started before
+# the capture — which can yield the GIL inside a finaliser and free device memory later —
+# finishes first. (gc.disable() only stops new collections from starting.)
+GC_LOCK = threading.RLock()
+
+
+def _gc_phase(phase: str, info: dict) -> None:
+    if phase == "start":
+        GC_LOCK.acquire()
+    else:
+        GC_LOCK.release()
+
+
+gc.callbacks.append(_gc_phase)
 
 
 def state_bytes_per_client(layout, compute_dtype, optimizer: str) -> int:

@@ -34,7 +34,7 @@ from ..ops import functional as Fn
 from ..utils.tracing import trace
 from .hooks import ExecutorHookPoint, HookRegistry, StopExecutingException
 from ..options import OPTIONS
-from .memory import DEVICE_LOCK
+from .memory import DEVICE_LOCK, GC_LOCK
 from .params import BoundParams, CohortBuffers, FusedSGD
 
 
@@ -493,6 +493,18 @@ class CohortTrainer:
             sg.samples[a:b] += vf
             self.optimizer_step(b - a, lr, active, first, row0=a, fused=fused)
 
+    def release_graphs(self) -> None:
+        """Destroy this trainer's step graphs now, under the device lock (a finished session's
+        graphs left to the cyclic garbage collector could be destroyed from another task thread in
+        the middle of that thread's capture, which HIP aborts on)."""
+        if not self._graphs:
+            return
+        with DEVICE_LOCK:
+            torch.cuda.synchronize(self.device)
+            for sg in self._graphs.values():
+                sg.graph = None
+            self._graphs.clear()
+
     def _step_graph(self, n: int, parts, full: bool = True, keep=()) -> _StepGraph | None:
         """The step graph of an n-row cohort split into `parts` (created empty; captured on its
         second use). Each captured graph owns a private pool sized for its step; n varies with
@@ -548,7 +560,7 @@ class CohortTrainer:
         else:
             # one capture at a time per process, and no device-wide synchronisation of another
             # task thread inside it (engine.memory.DEVICE_LOCK)
-            with DEVICE_LOCK:
+            with DEVICE_LOCK, GC_LOCK:
                 # the eager step's cached blocks go back to the driver so the graph's private pool
                 # can take them (else activation memory is held twice)
                 torch.cuda.synchronize(self.device)

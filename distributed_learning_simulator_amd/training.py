@@ -45,7 +45,13 @@ def _check_limits() -> None:
 
 def _run(config, practitioners=None, comm: Comm | None = None) -> dict:
     session = Session(config, practitioners=practitioners, comm=comm)
-    return session.run()
+    try:
+        return session.run()
+    finally:
+        # (concurrent tasks: no step graph of this session may outlive it into the garbage collector)
+        trainer = getattr(session, "trainer", None)
+        if trainer is not None and hasattr(trainer, "release_graphs"):
+            trainer.release_graphs()
 
 
 def _run_task(config, practitioners, comm: Comm) -> dict:
