@@ -1,7 +1,8 @@
-"""Tile sweep of the plane-GEMM forward (csrc/conv_pl.hip, every conv_nt_pl variant) on the
-GTG-Shapley evaluation shapes of ResNet-18: `--K` models x 8192 images per launch, fp32 planes
-operands, BN statistics in the epilogue — what CohortTrainer.evaluate launches for the strided
-3x3 convs, the 1x1 stride-2 shortcuts and l4. Best of `--rounds` interleaved rounds.
+"""Tile sweep of the plane-GEMM forward (csrc/conv_pl.hip, every conv_nt_pl variant) on large-M
+launches of the ResNet-18 layer shapes: `--K` clients x 8192 images per launch, fp32 planes
+operands, BN statistics in the epilogue — the strided 3x3 convs, the 1x1 stride-2 shortcuts and
+l4. (CohortTrainer.evaluate does not launch these: it runs each 64-image test batch as a virtual
+client; the large-M rule it informed serves ResNet-50's 56x56 layers.) Best of `--rounds`.
 
     python bench/eval_tiles_bench.py [--K 4] [--B 8192] [--iters 5]
 """

@@ -1,7 +1,8 @@
 """A/B of the pixel-major tap-skipping GEMMs (csrc/conv_pl.hip PIX, native option conv_pix) on the
 small-image convolutions they serve: ResNet-18 l4 (3x3, 4x4, 512 channels) and the strided l4a / l3a
-forwards, at a training cohort (K clients x 64 images, default tiles, planes operands) and at the
-GTG-Shapley evaluation shape (models x 8192 images, forward only). Interleaved rounds in one process,
+forwards, at a training cohort (K clients x 64 images, default tiles, planes operands) and at 8192
+images per client (forward only: one-pixel tiles; the GTG utility itself launches 64-image test
+batches as virtual clients, i.e. the training shapes). Interleaved rounds in one process,
 best of `--rounds`; TFLOP/s count every tap (the padded ones too), as bench/kernel_bench.py does.
 
     python bench/pix_bench.py [--K 50] [--iters 10] [--rounds 3]

@@ -87,8 +87,9 @@ __global__ void __launch_bounds__(WM* WN * 64, MINW) conv_nt_pl_kernel(ConvNTPar
   const int t = bid - client * per_client;
   int mt = t / tilesN;
   if constexpr (PIX) {
-    // one-pixel tiles (B % BM == 0): the tiles of every pixel of one image chunk are consecutive, so
-    // they run together on one XCD and the input rows their taps share are read from its L2
+    // one-pixel tiles (B % BM == 0, >= 256 images per client): the tiles of every pixel of one image
+    // chunk are consecutive, so they run together on one XCD and the input rows their taps share are
+    // read from its L2
     if (p.B % BM == 0) {
       const int npix = p.OH * p.OW;
       mt = (mt % npix) * (p.B / BM) + mt / npix;
@@ -372,9 +373,10 @@ static int pl_min_wg() {
   return native_option(g_opt_pl_min_wg, "DLS_PL_MIN_WG", 256);
 }
 
-// Evaluation-sized launches (GTG-Shapley utility: 8192 images per model, M >= 128 K rows per
-// client; bench/eval_tiles_bench.py, profiles/r6_c11_eval_tiles.log): N = 256 also takes the
-// 256x256 tile (l3a 3.63 vs 4.06 ms, l3sc 1.01 vs 1.06) and the 3x3 N = 128 conv the 3-stage
+// Large-M launches (>= 128 K rows per client: ResNet-50's 56x56 layers at 128 images per client;
+// bench/eval_tiles_bench.py at 8192 images, bench/r50_kernel_bench.py --nt-variants,
+// profiles/r6_c11_eval_tiles.log, r6_c11_r50_layer_variants.log): N = 256 also takes the 256x256
+// tile (l3a 3.63 vs 4.06 ms; ResNet-50 l1.c3 fwd 0.97 vs 1.07) and the 3x3 N = 128 conv the 3-stage
 // interleaved 256x128 tile (l2a 2.36 vs 2.53; the 1x1 shortcut keeps 128x128, 0.84 vs 0.97)
 int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
   if (p.N <= 64) return 2;
@@ -389,9 +391,9 @@ int conv_nt_pl_default_variant(const ConvNTParams& p, int K) {
 // pixel-major rows with tap skipping (conv_nt_pl_kernel PIX) for stride-1 convs on small images,
 // where the image border holds a large share of the tap-pixels: 3x3 on 4x4 (ResNet-18 l4) keeps 100
 // of 144. Measured (bench/pix_bench.py, profiles/r6_c10_pix_bench.log): the 256x256 tile gains on l4
-// (fwd / dgrad 1.03 / 1.06x at 50 clients, eval fwd 1.09x); the 128x128 tile of small cohorts loses
+// (fwd / dgrad 1.03 / 1.06x at 50 clients, 1.15x at 8192 images per client); the 128x128 tile of small cohorts loses
 // (0.87 / 0.94x at 7 clients: a 2-pixel tile's tap box is mostly the full 3x3) and so do the strided
-// forwards (l4a 0.97x, eval 0.91x), which keep the plain walk. Not for the sub-pixel dgrad classes,
+// forwards (l4a 0.97x, 0.91x at 8192 images), which keep the plain walk. Not for the sub-pixel dgrad classes,
 // compact shortcut gradients or dropout (their epilogues index GEMM rows). conv_pix = 0 turns it off
 static bool pix_ok(const ConvNTParams& p, int variant) {
   return native_option(g_opt_conv_pix, "DLS_CONV_PIX", 1) != 0 && variant == 3 && p.stride == 1 &&
