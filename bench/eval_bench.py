@@ -2,7 +2,7 @@
 CIFAR-10-shaped 10k test split, exactly as GTG-Shapley's batch metric function runs them
 (`method/shapley_value/__init__.py` batch_metric → Session.evaluate_tensors → CohortTrainer.evaluate).
 
-    python bench/eval_bench.py [--M 32] [--iters 3] [--max-images 8192 ...] [--streams 2 ...]
+    python bench/eval_bench.py [--M 32] [--iters 3] [--max-images 4096 ...] [--streams 2 ...]
 
 Prints one JSON line per (max_images, streams) setting — timed in interleaved rounds, best of
 `--rounds` — with ms per M-model chunk, ms per model, images/s and the useful forward TFLOP/s
@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=32)
     ap.add_argument("--iters", type=int, default=3)
-    ap.add_argument("--max-images", type=int, nargs="+", default=[8192])
+    ap.add_argument("--max-images", type=int, nargs="+", default=[4096])
     ap.add_argument("--streams", type=int, nargs="+", default=[2])
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--fused", type=int, nargs="+", default=[1],

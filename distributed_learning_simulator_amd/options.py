@@ -102,9 +102,11 @@ class RuntimeOptions:
     max_graphs: int = dataclasses.field(default_factory=lambda: _env_int("DLS_MAX_GRAPHS", 3))
     """Captured step graphs kept per trainer (each owns a private memory pool): a round uses the
     full cohort's and its ragged epoch-end step's (ragged_steps)."""
-    eval_max_images: int = dataclasses.field(default_factory=lambda: _env_int("DLS_EVAL_MAX_IMAGES", 8192))
+    eval_max_images: int = dataclasses.field(default_factory=lambda: _env_int("DLS_EVAL_MAX_IMAGES", 4096))
     """Images per evaluation launch (M models x batches): larger launches fill the GPU better and
-    cost activation memory. Per sub-cohort stream: evaluate() keeps up to `streams` launches in
+    cost activation memory; past 4096 they measured slower (GTG utility of 32 models: 38.8 ms per
+    model at 4096 vs 39.9 at 8192 and 40.5 at 16384, profiles/r6_c16_eval_max_images.log; the
+    headline's one-model test pass equal). Per sub-cohort stream: evaluate() keeps up to `streams` launches in
     flight on separate streams (whose freed blocks the caching allocator does not share), so its
     peak activation memory is about streams x this many images' worth."""
     shared_planes: bool = dataclasses.field(default_factory=lambda: _env_bool("DLS_SHARED_PLANES", True))
