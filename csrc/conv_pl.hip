@@ -365,12 +365,15 @@ bool conv_nt_pl_supported(const ConvNTParams& p) {
 // tile (l4 354 / 297 vs 333 / 278); otherwise 128x128 at 2 blocks per CU (l3 331 / 291 vs 309 /
 // 249 for 256x128)
 // Small cohorts (a rank's share of a multi-GPU round: 100 clients / 8 ranks / 2 streams ≈ 6-7 per
-// launch) leave the 256x256 grid far below the 256 CUs: below 256 workgroups N >= 512 takes the
+// launch) leave the 256x256 grid far below the 256 CUs: below 192 workgroups N >= 512 takes the
 // 128x128 tile (l4 at 7 clients: fwd / dgrad 282 / 213 vs 127 / 107 TFLOP/s; at 50 clients the
 // 256x256 tile keeps 380 / 325 vs 350 / 303, profiles/r3_kernel_bench_small_cohort_kref.log).
-// DLS_PL_MIN_WG overrides the threshold (0 = always 256x256)
+// 192 rather than 256 since the pixel-major walk: a 2-rank share (25 clients per launch, 200 l4
+// workgroups) runs 1779 → 1732 ms per round on the 256x256 tile, while the 4- and 8-rank shares
+// (96-104 and 56 workgroups) stay on 128x128 (threshold 96 / 48 measured +1.4 / +7.6 % there,
+// profiles/r6_c17_pl_min_wg.txt). DLS_PL_MIN_WG overrides it (0 = always 256x256)
 static int pl_min_wg() {
-  return native_option(g_opt_pl_min_wg, "DLS_PL_MIN_WG", 256);
+  return native_option(g_opt_pl_min_wg, "DLS_PL_MIN_WG", 192);
 }
 
 // Large-M launches (>= 128 K rows per client: ResNet-50's 56x56 layers at 128 images per client;
